@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark: VAMP iterations/s on BASELINE.json configs[1] (C2).
+
+Workload (C2): K = 1 cohort, M = 200,000 markers in 8 LD blocks of 25,000,
+N = 10,000 samples, the reference CLI's default flags (gamw 5, gam1 1e-6,
+rho 0.5, prior 0,1 / 0.99,0.01, cg-maxit 500, EM prior from it 1 with <= 100
+steps, learn-gamw 1, lmmse-damp 0, s 0).  Synthetic data generated on the
+device following simulation/sim_gen_phen_mult.py (X ~ Bin(2, 0.4), 50 %
+causal markers, h2 = 0.8).  A "step" is one VAMP outer iteration
+(src/sgvamp.py:222-387): EM prior update, denoiser, both CG solves, gamw
+learning, output files.  Inputs are resident in HBM before timing starts.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+the 8 LD blocks are sharded over the N ranks (strong scaling, one problem);
+CG dot products are ordered per-block sums exchanged with RCCL all-gathers.
+
+Prints ONE JSON line on rank 0 (other output goes to stderr).
+"""
+import argparse
+import glob
+import json
+import os
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sgvamp-py_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, MI355X_MICROARCH.md chip table
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--blocks", type=int, default=8)
+    p.add_argument("--block-size", type=int, default=25000)
+    p.add_argument("--nsamp", type=int, default=10000)
+    p.add_argument("--K", type=int, default=1)
+    p.add_argument("--seed", type=int, default=2025)
+    p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    p.add_argument("--cpu-iters", type=int, default=3)
+    p.add_argument("--no-files", action="store_true", help="skip the per-iteration output files")
+    return p.parse_args()
+
+
+def make_problem(eng, comm, args):
+    """beta and noise on the host (RandomState, as the reference recipe);
+    genotypes, LD blocks, g and r on the device."""
+    M, N = eng.M, args.nsamp
+    rs = np.random.RandomState(args.seed)
+    cm = int(M * 0.5)                                   # sim_gen_phen_mult.py:28-32
+    beta = np.zeros(M)
+    beta[rs.choice(M, cm, replace=False)] = rs.normal(0, np.sqrt(0.8 / cm), cm)
+    geno_seed = args.seed + 1
+    g_loc = eng.synth_ld_g(0, geno_seed, N, beta)       # (nblk_local, N)
+    g_all = np.concatenate(comm.allgather(g_loc)) if comm.Get_size() > 1 else g_loc
+    g = g_all[0].copy()
+    for b in range(1, g_all.shape[0]):                  # global block order
+        g = g + g_all[b]
+    ys = []
+    for k in range(eng.K):
+        w = np.random.RandomState(args.seed + 1000 + k).normal(0.0, np.sqrt(0.2), N)
+        y = g + w
+        eng.synth_r(k, geno_seed, N, y)
+        ys.append(y)
+    return beta, ys
+
+
+def read_traffic(kernel_prefix="k_ld_pass"):
+    """HBM bytes per LD-pass launch from the committed PMC summary, if any
+    (profiles/*pmc*.json written by tools/pmc_summary.py)."""
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    for path in reversed(cands):
+        try:
+            d = json.load(open(path))
+            if kernel_prefix in d.get("kernel", ""):
+                return float(d["hbm_bytes_per_launch"]), os.path.basename(path)
+        except Exception:
+            continue
+    return None, None
+
+
+def cpu_baseline(eng, args, ref_flags):
+    """The oracle (the build's NumPy restatement, OpenBLAS threads) on a bounded
+    sample: LD block 0 (n = block-size markers) of the same workload."""
+    import threadpoolctl
+
+    from oracle import vamp_oracle as vo
+    import hip_backend as hb
+
+    n = eng.block_sizes[0]
+    B = eng.get_ld_block(0, 0)
+    r = eng.get_vector(hb.VEC_R, 0)[:n].copy()
+    L = vo.BlockLD([B])
+    its = args.cpu_iters
+    t0 = time.perf_counter()
+    vo.infer([L], [0], [r], [args.nsamp], its, reducer=vo.Reducer(), seed=args.seed, **ref_flags)
+    dt = time.perf_counter() - t0
+    info = threadpoolctl.threadpool_info()
+    cores = max([i.get("num_threads", 1) for i in info if i.get("internal_api") in
+                 ("openblas", "mkl", "blis")] or [1])
+    frac = (n * n) / float(sum(b * b for b in eng.block_sizes))
+    return dict(value=its / dt * frac, unit="VAMP it/s", cores=int(cores), kind="port",
+                sample="oracle/vamp_oracle.py (NumPy+OpenBLAS) on LD block 0 only (%d markers, "
+                       "%.1f GB), iterations 0-%d, %.2f s; it/s scaled by the LD-byte fraction "
+                       "%.4f of the full workload" % (n, n * n * 8 / 1e9, its - 1, dt, frac))
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    import hip_backend as hb  # noqa: F401  (fails loudly if the library is missing)
+    from comm import world_from_env
+    from engine import Engine
+    from sgvamp import VAMP
+
+    comm = world_from_env()
+    rank = comm.Get_rank()
+    device = int(os.environ.get("LOCAL_RANK", "0"))
+    sizes = [args.block_size] * args.blocks
+    K = args.K
+    t_setup = time.perf_counter()
+    eng = Engine(sizes, K, ld_of=[0] * K, comm=comm, device=device)
+    beta, _ = make_problem(eng, comm, args)
+    N_list = [args.nsamp] * K
+    Nt = sum(N_list)
+    a = np.array(N_list) / Nt
+    flags = dict(rho=0.5, gamw=5.0, gam1=1e-6, prior_vars=[0.0, 1.0], prior_probs=[0.99, 0.01])
+    run = dict(cg_maxit=500, em_prior_maxit=100, learn_gamw=True, lmmse_damp=False,
+               prior_update="em", update_prior_from=1)
+    tmp = tempfile.mkdtemp(prefix="sgvamp_bench_")
+    v = VAMP(N=N_list if K > 1 else N_list[0], Nt=Nt, M=eng.M, K=K, a=a, out_dir=tmp,
+             out_name="bench", comm=comm, seed=args.seed, write_files=not args.no_files, **flags)
+    x0 = beta * np.sqrt(N_list[0])                      # main.py:276-279
+    v.attach_engine(eng, x0=x0)
+    v.begin(x0=x0, return_xhat=False, **run)
+    eng.sync()
+    comm.barrier()
+    log("[bench] setup (device data generation) %.1f s, M=%d, blocks=%d x %d, N=%d, K=%d, ranks=%d"
+        % (time.perf_counter() - t_setup, eng.M, args.blocks, args.block_size, args.nsamp, K,
+           world))
+
+    for it in range(args.warmup):
+        rec = v.step(it)
+        log("[bench] warmup it=%d cg=%s passes=%d %.1f ms" % (it, rec["cg_iters"], rec["ld_passes"],
+                                                              rec["wall_s"] * 1e3))
+    eng.timers(reset=True)
+    eng.sync()
+    comm.barrier()
+    t0 = time.perf_counter()
+    recs = []
+    for it in range(args.warmup, args.warmup + args.steps):
+        recs.append(v.step(it))
+    eng.sync()
+    t1 = time.perf_counter()
+    comm.barrier()
+    dt = max(comm.allgather(t1 - t0))
+    tm = eng.timers()
+    for rec in recs:
+        log("[bench] it=%d cg=%s em=%s passes=%d %.1f ms l2=%s" % (
+            rec["it"], rec["cg_iters"], rec.get("em_steps"), rec["ld_passes"], rec["wall_s"] * 1e3,
+            "%.4f" % rec["metrics"][1] if "metrics" in rec else "-"))
+
+    steps = args.steps
+    value = steps / dt
+    launches = max(tm["ld_launches"], 1)
+    avg_s = tm["ld_ms"] / 1e3 / launches
+    bytes_launch = tm["ld_bytes_per_pass"] + tm["rhs_bytes"] / launches
+    achieved = bytes_launch / avg_s / 1e9 if avg_s > 0 else None
+    traffic, traffic_src = read_traffic()
+    passes = sum(r["ld_passes"] for r in recs)
+    ld_bytes_total = tm["ld_bytes_per_pass"] * comm.Get_size()
+    result = {
+        "metric": "VAMP iterations/sec (and effective LD-matvec GB/s) at M markers, K cohorts",
+        "value": value,
+        "unit": "VAMP it/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: device generator following simulation/sim_gen_phen_mult.py "
+                "(Bin(2,0.4) genotypes, 50% causal, h2=0.8), seed %d" % args.seed,
+        "config": {
+            "workload": "C2 (BASELINE.json configs[1]): K=%d cohort, M=%d markers in %d LD blocks "
+                        "of %d, N=%d, reference CLI default flags, output files written each "
+                        "iteration" % (K, eng.M, args.blocks, args.block_size, args.nsamp),
+            "K": K, "M": eng.M, "ld_blocks": args.blocks, "block_size": args.block_size,
+            "N": args.nsamp, "parallelism": "LD blocks sharded over %d GPU rank(s)" % world,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic": traffic,
+            "kernel": "sgv::k_ld_pass (LD mat-vec, per GPU)",
+            "bytes_per_launch": bytes_launch,
+            "avg_launch_ms": avg_s * 1e3,
+            "launches": int(launches),
+            "traffic_source": traffic_src,
+        },
+        "ld_passes_per_step": passes / steps,
+        "effective_ld_gbps_end_to_end": passes * ld_bytes_total / dt / 1e9,
+        "cg_iters_per_step": [r["cg_iters"] for r in recs],
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+        log("[bench] cpu baseline ...")
+        result["cpu_baseline"] = cpu_baseline(eng, args, dict(flags, **run))
+    else:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,187 @@
+/*
+ * sgvamp_hip.h -- C ABI of the MI355X-native sgVAMP hot path (libsgvamp_hip.so).
+ *
+ * The reference (medical-genomics-group/sgVAMP-py) has no FFI layer; its hot path
+ * sits behind the class seam VAMP(...)/VAMP.infer(...) (src/sgvamp.py:15,196) and
+ * the operator seam con_grad(A, b, maxiter, x0) -> (x, info) (src/sgvamp.py:7,316,332).
+ * Every entry point below names the reference code it replaces.  The Python host
+ * (sgvamp-py_amd/sgvamp.py) binds them with ctypes; INTEGRATION.md shows the stub.
+ *
+ * Conventions
+ *  - Return 0 on success, a negative SGV_ERR_* code on failure; the message is in
+ *    sgv_last_error(ctx) (ctx may be NULL for errors raised before a ctx exists).
+ *    No C++ exception crosses the ABI.
+ *  - Host arrays are caller-owned, C-contiguous, borrowed for the call only.
+ *    Vectors are f64 in the rank-local DENSE marker order (the rank's blocks
+ *    concatenated).  Device memory is owned by the ctx.
+ *  - One ctx per process and GPU; one host thread drives it; not re-entrant.
+ *  - Markers are partitioned into LD blocks (block-diagonal LD).  A rank owns a
+ *    contiguous range of global blocks [blk0, blk0 + nblk).  All K cohorts of a
+ *    marker live on the same rank.  Every M-length reduction is summed per LD
+ *    block in a fixed order and then over blocks in global block order, so runs
+ *    on 1/2/4/8 GPUs give bit-identical results.
+ */
+#ifndef SGVAMP_HIP_H
+#define SGVAMP_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SGV_OK 0
+#define SGV_ERR_HIP (-1)
+#define SGV_ERR_ARG (-2)
+#define SGV_ERR_RCCL (-3)
+#define SGV_ERR_STATE (-4)
+
+#define SGV_MAX_COHORTS 8   /* 2K <= 16 right-hand sides per LD pass   */
+#define SGV_MAX_SLABS 8     /* L - 1 slab components of the prior      */
+
+/* vector ids for sgv_set_vector / sgv_get_vector */
+#define SGV_VEC_R 0       /* r_k = X_k^T y_k            (src/main.py:176-191,266)   */
+#define SGV_VEC_R1 1      /* r1_k, denoiser input        (src/sgvamp.py:204,348)     */
+#define SGV_VEC_XHAT1 2   /* xhat1 (shared)              (src/sgvamp.py:273-276)     */
+#define SGV_VEC_XHAT2 3   /* xhat2_k                     (src/sgvamp.py:316-323)     */
+#define SGV_VEC_SIG2U 4   /* Sigma2_u_k                  (src/sgvamp.py:332-333)     */
+#define SGV_VEC_X0 5      /* true signal for metrics     (src/main.py:268-285)       */
+
+/* sgv_lmmse per-cohort outputs, out[k * SGV_LMMSE_NOUT + i] */
+#define SGV_LMMSE_NOUT 8
+#define SGV_O_TRSIGMA2 0  /* u^T Sigma2 u                 src/sgvamp.py:338 */
+#define SGV_O_ALPHA2 1    /* alpha2 (after damping)       :340,345-346      */
+#define SGV_O_GAM1 2      /* gam2 (1-alpha2)/alpha2       :347              */
+#define SGV_O_Z 3         /* z (clamped at 0)             :352-354          */
+#define SGV_O_TRRSIGMA2 4 /* u^T R Sigma2 u               :359              */
+#define SGV_O_GAMW 5      /* 1/(z/N + TrRSigma2/N), not yet clamped at 1 :363 */
+#define SGV_O_XR 6        /* xhat2^T r                    :352              */
+#define SGV_O_XRX 7       /* xhat2^T R xhat2              :352              */
+
+typedef struct sgv_ctx sgv_ctx;
+
+/* ---- lifetime ------------------------------------------------------------ */
+
+/* Per-rank setup; replaces src/main.py:79-97 (K, N lists), :143 (M), :287 (a)
+ * and VAMP.__init__ src/sgvamp.py:15-31 for the device side.
+ *   device          HIP device ordinal this rank drives
+ *   K               cohorts (1..SGV_MAX_COHORTS)
+ *   nld             distinct LD matrices; ld_of[k] in [0, nld)
+ *   nblk, blk_sizes LD blocks owned by this rank, in marker order
+ *   blk0            global index of this rank's first block
+ *   nblk_global     total blocks over all ranks
+ *   M_total         total markers over all ranks (np.mean denominators) */
+int sgv_create(int device, int K, int nld, const int* ld_of, int nblk,
+               const int64_t* blk_sizes, int blk0, int nblk_global, int64_t M_total,
+               sgv_ctx** out);
+void sgv_destroy(sgv_ctx* ctx);
+const char* sgv_last_error(const sgv_ctx* ctx);
+
+/* ---- multi-GPU (RCCL over xGMI) ----------------------------------------- */
+
+/* Replaces mpi4py COMM_WORLD (src/main.py:16-18) and the per-iteration K x M
+ * bcast all-gather (src/sgvamp.py:228-233), which disappears because all cohorts
+ * of a marker are co-located.  What remains are ordered reductions of per-block
+ * partial sums (ncclAllGather).  id: 128 bytes (ncclUniqueId) from rank 0. */
+int sgv_comm_unique_id(char* id_out /* 128 bytes */);
+int sgv_comm_init(sgv_ctx* ctx, int nranks, int rank, const char* id /* 128 bytes */,
+                  const int* nblk_per_rank /* [nranks] */);
+
+/* ---- inputs -------------------------------------------------------------- */
+
+/* Upload one dense LD block (row-major n x n, host row stride ld_host elements).
+ * Replaces the R loaders src/main.py:199-202 (dense .npy / CSR .npz blocks). */
+int sgv_set_ld_block(sgv_ctx* ctx, int ld, int blk_local, const double* rowmajor,
+                     int64_t ld_host);
+/* Download one LD block (row-major n x n into a host array of row stride ld_host). */
+int sgv_get_ld_block(sgv_ctx* ctx, int ld, int blk_local, double* rowmajor, int64_t ld_host);
+/* R_s = (1 - s) R + s I, applied inside every LD pass (src/main.py:265). */
+int sgv_set_ridge(sgv_ctx* ctx, double s);
+/* Cohort sample size N_k (src/main.py:83-85; used by gamw learning :352,363). */
+int sgv_set_cohort_n(sgv_ctx* ctx, int k, double N);
+
+int sgv_set_vector(sgv_ctx* ctx, int which, int k, const double* host_local);
+int sgv_get_vector(sgv_ctx* ctx, int which, int k, double* host_local);
+
+/* ---- synthetic data on device (simulation/sim_gen_phen_mult.py:36-55) ------
+ * Genotypes x_{in} ~ Binomial(2, 0.4) from a counter-based hash of
+ * (geno_seed, global marker index, sample n); standardised per marker over the
+ * Nsamp samples (population std), X_std; G = X_std / sqrt(Nsamp).
+ * marker0 = global index of this rank's first marker (keys the hash, so the
+ * data does not depend on how blocks are spread over ranks).
+ * Step 1: for every owned block b: if ld >= 0 store R_b = G_b G_b^T into LD
+ *         matrix `ld`; write g_b[n] = sum_{i in b} X_std[i][n] beta_i to
+ *         g_blocks_out[b * Nsamp + n] (host, nblk x Nsamp).
+ * Step 2 (after the host forms y = sum_b g_b + w): r_k,b = G_b y. */
+int sgv_synth_ld_g(sgv_ctx* ctx, int ld, uint64_t geno_seed, int64_t marker0, int Nsamp,
+                   const double* beta_local, double* g_blocks_out);
+int sgv_synth_r(sgv_ctx* ctx, int k, uint64_t geno_seed, int64_t marker0, int Nsamp,
+                const double* y);
+
+/* ---- the hot path -------------------------------------------------------- */
+
+/* Meta denoiser + derivative over all markers: src/sgvamp.py:93-114 applied at
+ * :270-291.  xhat1 <- denoiser_meta(r1s, gam1s); if damp: xhat1 <- rho*xhat1 +
+ * (1-rho)*xhat1_prev.  der_sum_out[k] = sum_j der_denoiser_meta_k(r1s[:, j])
+ * (the host divides by M_total: np.mean, :285). */
+int sgv_denoise(sgv_ctx* ctx, const double* gam1s, const double* a, double lam,
+                int nslab, const double* omegas, const double* sigmas, double rho,
+                int damp, double* der_sum_out);
+
+/* EM prior update loop: src/sgvamp.py:116-136 driven as :250-257 (stop when the
+ * relative change of omegas and lam are both < 1e-6, at most maxit steps). */
+int sgv_em(sgv_ctx* ctx, const double* gam1s, const double* a, int nslab,
+           const double* sigmas, int maxit, double* lam_io, double* omegas_io,
+           int* steps_out, double* final_err_out);
+
+/* LMMSE step for all cohorts: src/sgvamp.py:301-364.  For every cohort k:
+ *   r2 = (xhat1 - alpha1 r1)/(1 - alpha1); mu2 = gamw r + gam2 r2;
+ *   CG #1: (gamw R_s + gam2 I) xhat2 = mu2, warm start xhat2_prev   (:316)
+ *   damping of xhat2 if lmmse_damp                                 (:322-323)
+ *   CG #2: (gamw R_s + gam2 I) Sigma2_u = u, warm start Sigma2_u_prev (:332)
+ *   alpha2, gam1, r1 update                                        (:338-348)
+ *   if learn_gamw: z, TrRSigma2, new gamw                          (:350-363)
+ * Both CG solves of all cohorts run batched: one pass over each LD matrix per
+ * CG iteration serves every right-hand side still iterating.  The CG is
+ * scipy 1.15.3's (iterative.py:375-422): rtol, atol 0, strict '<' stop test.
+ *   per-cohort inputs [K]: gamw, gam2, alpha1, alpha2_prev
+ *   probes: [K][M_local] int8 of +-1 (the host draws u, :326)
+ *   out: [K][SGV_LMMSE_NOUT]; cg_out: [K][4] = iters1, info1, iters2, info2
+ *   ld_passes_out: LD passes (full sweeps over all owned LD bytes) performed */
+int sgv_lmmse(sgv_ctx* ctx, int it, const double* gamw, const double* gam2,
+              const double* alpha1, const double* alpha2_prev, const int8_t* probes,
+              int cg_maxit, double rtol, int lmmse_damp, double rho, int learn_gamw,
+              double* out, int* cg_out, int* ld_passes_out);
+
+/* Metrics src/sgvamp.py:379-387: out[0] = <xhat1, x0>, out[1] = |xhat1|^2,
+ * out[2] = |xhat1 - x0|^2, out[3] = |x0|^2 (global sums). */
+int sgv_metrics(sgv_ctx* ctx, double* out4);
+
+/* ---- operator seam, exposed for tests ------------------------------------ */
+
+/* y = R_s v for LD matrix `ld` over the rank's blocks (one LD pass, up to 16
+ * columns).  v, y: [ncol][M_local] host, dense.  Replaces A.matvec inside
+ * scipy cg (src/sgvamp.py:316,332) and R @ x (:352,359). */
+int sgv_ld_matvec(sgv_ctx* ctx, int ld, int ncol, const double* v, double* y);
+
+/* Batched scipy-1.15.3 CG on (c1 R_s + c2 I) x = b for ncol columns sharing LD
+ * `ld` (operator seam con_grad, src/sgvamp.py:7).  x: in = x0, out = solution.
+ * iters_out/info_out [ncol]. */
+int sgv_cg_solve(sgv_ctx* ctx, int ld, int ncol, const double* c1, const double* c2,
+                 const double* b, double* x, int maxiter, double rtol, int* iters_out,
+                 int* info_out);
+
+/* ---- timing -------------------------------------------------------------- */
+/* t[0] = summed LD-pass kernel time (ms, HIP events on the ctx stream),
+ * t[1] = LD-pass launches, t[2] = algorithmic LD bytes per full pass (all owned
+ * blocks, all LD matrices: sum n_b^2 * 8), t[3] = RHS bytes moved by those
+ * launches (2 * ncol * M_local * 8 summed).  Reset with reset != 0. */
+int sgv_timers(sgv_ctx* ctx, double* t4, int reset);
+
+/* Synchronise the ctx stream. */
+int sgv_sync(sgv_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SGVAMP_HIP_H */

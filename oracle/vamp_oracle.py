@@ -1,0 +1,352 @@
+"""ORACLE -- CPU restatement of the reference sgVAMP hot path (TEST INFRASTRUCTURE).
+
+This module is a checker, never a product path.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it.  The shipped path (``sgvamp-py_amd/``) never imports anything from
+``oracle/`` and fails loudly when its HIP library is missing.
+
+Parity pinning
+--------------
+Pinned against the golden fixtures in ``tests/golden/*.npz``; those were
+produced by importing the reference (/root/reference/src/sgvamp.py) in the build
+container with ``tests/golden/make_golden.py``.  ``tests/test_oracle_golden.py``
+checks this restatement against every fixture.
+
+What it restates (reference file:line)
+---------------------------------------
+* ``VAMP.__init__``  src/sgvamp.py:15-31     (lam, sigmas*Nt, omegas)
+* ``denoiser_meta``  src/sgvamp.py:93-102    vectorised over markers
+* ``der_denoiser_meta`` src/sgvamp.py:104-114 vectorised, all K cohorts at once
+* ``prior_update_em`` src/sgvamp.py:116-136  + driver loop :247-259
+* ``VAMP.infer``      src/sgvamp.py:196-389  all K cohort ranks in one process
+* scipy 1.15.3 ``cg`` scipy/sparse/linalg/_isolve/iterative.py:305-422 (the
+  reference's ``con_grad``, src/sgvamp.py:7,316,332): rtol 1e-5, atol 0,
+  strict ``<`` stop test, warm-start residual only when ``x0.any()``.
+
+Arithmetic is IEEE f64 and follows the reference's operation order where that
+is cheap (builtin ``sum`` over slabs is sequential, ``np.mean`` for alpha1).
+The LD product uses ``A p = gamw*(R_s p) + gam2*p`` instead of materialising
+``A = gamw*R_s + gam2*I`` (src/sgvamp.py:312): same math, different rounding.
+
+Two reduction modes for the M-length dot products:
+* ``"numpy"``   np.dot / np.linalg.norm, as the reference (default);
+* ``"blocked"`` per-LD-block partial sums added in block order -- the order the
+  HIP path uses so that 1/2/4/8-GPU runs agree bit for bit.  ``BlockedComm``
+  lets a sharded run (each rank owning a contiguous range of blocks) exchange
+  per-block partials (tests/test_dist_gloo.py).
+"""
+import numpy as np
+
+
+# ----------------------------------------------------------------------------
+# element-wise pieces
+# ----------------------------------------------------------------------------
+def _seqsum_last(x):
+    """Python builtin sum() over the last axis: ((0 + x0) + x1) + ...
+    (src/sgvamp.py:95,99,101 use builtin sum over the L-1 slabs)."""
+    acc = x[..., 0].copy()
+    for l in range(1, x.shape[-1]):
+        acc = acc + x[..., l]
+    return acc
+
+
+def _seqsum(v):
+    acc = v[0]
+    for t in v[1:]:
+        acc = acc + t
+    return acc
+
+
+def denoiser_terms(r1s, gam1s, a, lam, omegas, sigmas):
+    """Shared sub-expressions of denoiser_meta / der_denoiser_meta
+    (src/sgvamp.py:95-101 and :105-111), vectorised over markers.
+
+    r1s (K, M); returns dict of (M, L-1) / (M,) arrays."""
+    ag = a * gam1s                                        # (K,)
+    sum_ag = _seqsum(list(ag))                            # builtin sum, :95
+    s2 = 1.0 / (sum_ag + 1.0 / sigmas)                    # (L-1,)  :95
+    inner = r1s[0] * ag[0]                                # np.inner(rs, a*gam1s) :96,
+    for k in range(1, r1s.shape[0]):                      # sequential over k (the HIP
+        inner = inner + r1s[k] * ag[k]                    # kernel's order)
+    mu = inner[:, None] * s2[None, :]                     # (M, L-1)
+    ratio = mu * mu / s2[None, :]                         # :97
+    m = np.argmax(ratio, axis=1)                          # first max, as ndarray.argmax
+    rows = np.arange(mu.shape[0])
+    s2m = s2[m]
+    mum = mu[rows, m]
+    EXP = np.exp(0.5 * (mu * mu * s2m[:, None] - (mum * mum)[:, None] * s2[None, :])
+                 / (s2[None, :] * s2m[:, None]))          # :98
+    sq = np.sqrt(s2 / sigmas)                             # (L-1,)
+    Num = lam * _seqsum_last(omegas * EXP * mu * sq)      # :99
+    EXP2 = np.exp(-0.5 * (mum ** 2 / s2m))                # :100
+    Den = (1 - lam) * EXP2 + lam * _seqsum_last(omegas * EXP * sq)   # :101
+    return dict(s2=s2, mu=mu, EXP=EXP, sq=sq, Num=Num, Den=Den)
+
+
+def denoiser_meta(r1s, gam1s, a, lam, omegas, sigmas):
+    """xhat1 (M,) -- src/sgvamp.py:93-102 applied per marker (:273)."""
+    t = denoiser_terms(r1s, gam1s, a, lam, omegas, sigmas)
+    return t["Num"] / t["Den"]
+
+
+def der_denoiser_meta(r1s, gam1s, a, lam, omegas, sigmas):
+    """(K, M) derivative for every cohort k -- src/sgvamp.py:104-114, with the
+    rank's factor a[rank]*gam1s[rank] (:112-113) taken for each k."""
+    t = denoiser_terms(r1s, gam1s, a, lam, omegas, sigmas)
+    s2, mu, EXP, sq, Num, Den = (t[k] for k in ("s2", "mu", "EXP", "sq", "Num", "Den"))
+    out = np.empty((len(a), mu.shape[0]))
+    for k in range(len(a)):
+        DerNum = lam * _seqsum_last(omegas * EXP * (mu * mu + s2) * a[k] * gam1s[k] * sq)
+        DerDen = lam * _seqsum_last(omegas * mu * EXP * a[k] * gam1s[k] * sq)
+        out[k] = (DerNum * Den - DerDen * Num) / (Den * Den)
+    return out
+
+
+def prior_update_em(r1s, gam1s, a, lam, omegas, sigmas, red=None, M_total=None):
+    """One EM step -- src/sgvamp.py:116-136.  Returns (lam, omegas).
+    With a "blocked" reducer the marker sums go through it (sharded runs)."""
+    K, M = r1s.shape
+    Lm1 = len(sigmas)
+    prior_vars0 = sigmas.reshape(1, 1, Lm1)
+    gam1s_rs = gam1s.reshape(K, 1, 1)
+    gam1invs = 1.0 / gam1s_rs
+    r1s_rs = r1s.reshape(K, M, 1)
+    r2 = np.power(r1s_rs, 2)
+    exp_max = (-r2 / 2 / (prior_vars0 + gam1invs)).max(axis=2).reshape(K, M, 1)   # :127
+    xi = lam * omegas.reshape(1, 1, Lm1) * np.exp(-r2 / 2 / (prior_vars0 + gam1invs) - exp_max) \
+        / np.sqrt(gam1invs + prior_vars0)                                        # :128
+    sum_xi = xi.sum(axis=2).reshape(K, M, 1)                                     # :129
+    xi_tilde = xi / sum_xi                                                       # :130
+    pi = 1.0 / (1.0 + (1 - lam) * np.exp(-r2 / 2 * gam1s_rs - exp_max) / np.sqrt(gam1invs) / sum_xi)  # :131
+    if red is None or red.mode == "numpy":
+        lam_new = np.mean(np.average(pi, axis=0, weights=a))                     # :134
+        omegas_new = np.sum(pi * xi_tilde * a.reshape(K, 1, 1), axis=(0, 1)) \
+            / np.sum(pi * a.reshape(K, 1, 1), axis=(0, 1))                       # :136
+        return lam_new, omegas_new
+    ones = np.ones(M)
+    avg = np.average(pi, axis=0, weights=a).ravel()
+    lam_new = red.dot(avg, ones) / M_total
+    num = (pi * xi_tilde * a.reshape(K, 1, 1)).sum(axis=0)                      # (M, L-1)
+    den = (pi * a.reshape(K, 1, 1)).sum(axis=0).ravel()
+    omegas_new = np.array([red.dot(num[:, l], ones) for l in range(Lm1)]) / red.dot(den, ones)
+    return lam_new, omegas_new
+
+
+# ----------------------------------------------------------------------------
+# reductions
+# ----------------------------------------------------------------------------
+class Reducer:
+    """M-length dot products.  mode "numpy" = np.dot; mode "blocked" = per-block
+    partial sums (block = LD block of the marker partition) added in global
+    block order.  A sharded run owns blocks [b0, b1) of ``bounds`` and hands
+    its per-block partials to ``comm.allgather_blocks`` (None = single rank)."""
+
+    def __init__(self, mode="numpy", bounds=None, comm=None):
+        self.mode, self.bounds, self.comm = mode, bounds, comm
+
+    def dot(self, x, y):
+        if self.mode == "numpy":
+            return np.dot(x, y)
+        part = np.array([np.dot(x[s0:s1], y[s0:s1])
+                         for s0, s1 in zip(self.bounds[:-1], self.bounds[1:])])
+        if self.comm is not None:
+            part = self.comm.allgather_blocks(part)
+        return _seqsum(list(part)) if len(part) else 0.0
+
+    def norm(self, x):
+        return np.sqrt(self.dot(x, x))     # numpy/linalg/_linalg.py: sqrt(dot(x, x))
+
+    def mean(self, x, n_total):
+        if self.mode == "numpy":
+            return np.mean(x)
+        return self.dot(x, np.ones_like(x)) / n_total
+
+
+# ----------------------------------------------------------------------------
+# LD operator and CG
+# ----------------------------------------------------------------------------
+class BlockLD:
+    """Block-diagonal LD matrix R (the build's storage model): dense f64 blocks
+    on the diagonal.  ``s`` applies R_s = (1-s) R + s I (src/main.py:265)."""
+
+    def __init__(self, blocks, s=0.0):
+        self.blocks = [np.ascontiguousarray(b, dtype=np.float64) for b in blocks]
+        self.bounds = np.cumsum([0] + [b.shape[0] for b in self.blocks])
+        self.s = s
+
+    def matvec_R(self, v):
+        out = np.empty_like(v)
+        for (s0, s1), B in zip(zip(self.bounds[:-1], self.bounds[1:]), self.blocks):
+            out[s0:s1] = B @ v[s0:s1]
+        return out
+
+    def matvec_Rs(self, v):
+        if self.s == 0.0:
+            return self.matvec_R(v)
+        return (1 - self.s) * self.matvec_R(v) + self.s * v
+
+
+def cg_scipy(matvec, b, x0, maxiter, red, rtol=1e-5):
+    """scipy 1.15.3 cg (iterative.py:375-422), with counters.
+    Returns (x, info, n_iter, n_matvec)."""
+    x = np.array(x0, dtype=np.float64).ravel().copy()
+    b = np.asarray(b, dtype=np.float64).ravel()
+    bnrm2 = red.norm(b)
+    atol = max(0.0, rtol * bnrm2)
+    if bnrm2 == 0:
+        return b.copy(), 0, 0, 0
+    nmv = 0
+    if x.any():
+        r = b - matvec(x)
+        nmv += 1
+    else:
+        r = b.copy()
+    rho_prev, p = None, None
+    for it in range(maxiter):
+        if red.norm(r) < atol:
+            return x, 0, it, nmv
+        rho_cur = red.dot(r, r)
+        if it > 0:
+            beta = rho_cur / rho_prev
+            p *= beta
+            p += r
+        else:
+            p = r.copy()
+        q = matvec(p)
+        nmv += 1
+        alpha = rho_cur / red.dot(p, q)
+        x += alpha * p
+        r -= alpha * q
+        rho_prev = rho_cur
+    return x, maxiter, maxiter, nmv
+
+
+# ----------------------------------------------------------------------------
+# probe vectors (the reference's global RNG, seeded per cohort rank)
+# ----------------------------------------------------------------------------
+class ProbeStream:
+    """u = binomial(p=1/2, n=1, size=M)*2-1 from RandomState(seed + k):
+    identical to the stream src/sgvamp.py:326 sees after np.random.seed(seed+k)."""
+
+    def __init__(self, seed, K):
+        self.rs = [np.random.RandomState(seed + k) for k in range(K)]
+
+    def draw(self, k, M):
+        return self.rs[k].binomial(p=1 / 2, n=1, size=M) * 2 - 1
+
+
+# ----------------------------------------------------------------------------
+# the outer loop
+# ----------------------------------------------------------------------------
+def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-6,
+          prior_vars=(0.0, 1.0), prior_probs=(0.99, 0.01), x0=None, cg_maxit=500,
+          em_prior_maxit=100, learn_gamw=True, lmmse_damp=False, prior_update="em",
+          update_prior_from=1, seed=0, reducer=None, M_total=None, probe=None):
+    """All K cohorts of src/sgvamp.py:196-389 in one process.
+
+    lds: list of BlockLD; ld_of[k]: which LD cohort k uses; r_list[k]: (M,)
+    x0: true signal in reference scale (beta*sqrt(N_0)) or None.
+    Sharded use: pass the local marker slice of everything, ``reducer`` with a
+    comm, ``M_total`` the global M and ``probe`` a callable (k, it) -> local u.
+    Returns a dict with per-iteration trajectories."""
+    K = len(r_list)
+    M = len(r_list[0])
+    M_tot = M if M_total is None else M_total
+    red = reducer or Reducer()
+    Nt = sum(N_list)
+    a = np.array(N_list, dtype=np.float64) / sum(N_list)                 # main.py:287
+    lam = 1 - prior_probs[0]                                             # sgvamp.py:26
+    sigmas = np.array(prior_vars[1:]) * Nt                              # :27
+    omegas = np.array([p / sum(prior_probs[1:]) for p in prior_probs[1:]])   # :28
+    probes = probe or (lambda k, it, _s=ProbeStream(seed, K): _s.draw(k, M))
+
+    r = [np.asarray(v, dtype=np.float64).ravel() for v in r_list]
+    r1 = [v.copy() for v in r]                                           # :204
+    xhat1 = np.zeros(M)
+    xhat2 = [np.zeros(M) for _ in range(K)]
+    sig2u_prev = [np.zeros(M) for _ in range(K)]
+    gam1_k = [gam1] * K
+    gamw_k = [gamw] * K
+    alpha1_k = [0] * K
+    alpha2_k = [0] * K
+    traj = dict(xhat=[], r1=[], csv=[[] for _ in range(K)], metrics=[], cg_iters=[],
+                cg_info=[], em_steps=[], gamws=[[] for _ in range(K)], ld_passes=[])
+
+    for it in range(iterations):
+        gam1s = np.array(gam1_k, dtype=np.float64)                      # :228-233
+        r1s = np.stack(r1)
+        if it >= update_prior_from and prior_update == "em":            # :242-259
+            for em_it in range(em_prior_maxit):
+                old_omegas, old_lam = omegas, lam
+                lam, omegas = prior_update_em(r1s, gam1s, a, lam, omegas, sigmas, red, M_tot)
+                om_err = np.linalg.norm(omegas - old_omegas) / np.linalg.norm(old_omegas)
+                lam_err = np.abs(lam - old_lam) / lam
+                if om_err < 1e-6 and lam_err < 1e-6:
+                    break
+            traj["em_steps"].append(em_it + 1)
+        elif it >= update_prior_from and prior_update == "mle":
+            raise NotImplementedError("MLE prior update is outside the oracle's scope")
+
+        xhat1_prev = xhat1
+        xhat1 = denoiser_meta(r1s, gam1s, a, lam, omegas, sigmas)       # :273
+        if it > 0:
+            xhat1 = rho * xhat1 + (1 - rho) * xhat1_prev                # :275-276
+        traj["xhat"].append(xhat1 / np.sqrt(Nt))                        # :281
+        traj["r1"].append([v / np.sqrt(Nt) for v in r1])                # :283
+        der = der_denoiser_meta(r1s, gam1s, a, lam, omegas, sigmas)     # :285
+        it_cg, it_info, passes = [], [], 0
+        for k in range(K):
+            alpha1 = red.mean(der[k], M_tot)
+            if it > 0:
+                alpha1 = rho * alpha1 + (1 - rho) * alpha1_k[k]         # :290-291
+            alpha1_k[k] = alpha1
+            gam2 = gam1_k[k] * (1 - alpha1) / alpha1                    # :305
+            r2 = (xhat1 - alpha1 * r1[k]) / (1 - alpha1)                # :310
+            L = lds[ld_of[k]]
+            gw = gamw_k[k]
+
+            def A(p, L=L, gw=gw, gam2=gam2):                            # :312
+                return gw * L.matvec_Rs(p) + gam2 * p
+            mu2 = gw * r[k] + gam2 * r2                                 # :313
+            x2_prev = xhat2[k]
+            x2, info1, n1, m1 = cg_scipy(A, mu2, x2_prev, cg_maxit, red)    # :316
+            if lmmse_damp:
+                x2 = rho * x2 + (1 - rho) * x2_prev                     # :322-323
+            xhat2[k] = x2
+            u = probes(k, it)                                           # :326
+            s2u, info2, n2, m2 = cg_scipy(A, u, sig2u_prev[k], cg_maxit, red)   # :332
+            sig2u_prev[k] = s2u
+            uf = u.astype(np.float64)
+            TrSigma2 = red.dot(uf, s2u)                                 # :338
+            alpha2 = gam2 * TrSigma2 / M_tot                            # :340
+            if lmmse_damp:
+                alpha2 = rho * alpha2 + (1 - rho) * alpha2_k[k]         # :345-346
+            alpha2_k[k] = alpha2
+            gam1_k[k] = gam2 * (1 - alpha2) / alpha2                    # :347
+            r1[k] = (x2 - alpha2 * r2) / (1 - alpha2)                   # :348
+            if learn_gamw:                                              # :350-364
+                N = N_list[k]
+                z = N - 2 * red.dot(x2, r[k]) + red.dot(x2, L.matvec_Rs(x2))
+                if z < 0:
+                    z = 0
+                TrRSigma2 = red.dot(uf, L.matvec_Rs(s2u))
+                gw = 1 / (z / N + TrRSigma2 / N)
+            traj["gamws"][k].append(gw)                                 # :373
+            gamw_k[k] = max(gw, 1.0)                                    # :374
+            traj["csv"][k].append([it, gamw_k[k], gam1_k[k], gam2, alpha1, alpha2, lam])   # :377
+            it_cg.append((n1, n2))
+            it_info.append((info1, info2))
+            passes += m1 + m2 + (2 if learn_gamw else 0)
+        traj["cg_iters"].append(it_cg)
+        traj["cg_info"].append(it_info)
+        traj["ld_passes"].append(passes)
+        if x0 is not None:                                              # :379-387
+            x0v = np.asarray(x0, dtype=np.float64).ravel()
+            nx = red.norm(xhat1)
+            n0 = red.norm(x0v)
+            alignment = red.dot(xhat1, x0v) / nx / n0
+            l2 = red.norm(xhat1 - x0v) / n0
+            traj["metrics"].append([it, alignment, l2])
+    traj["final"] = dict(lam=lam, omegas=omegas, gamw=gamw_k, gam1=gam1_k, xhat2=xhat2,
+                         sig2u=sig2u_prev)
+    return traj

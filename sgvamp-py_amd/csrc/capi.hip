@@ -1,0 +1,1127 @@
+// C ABI of libsgvamp_hip.so (declared in include/sgvamp_hip.h).
+//
+// Owns device memory, the HIP stream, the RCCL communicator and the host-side
+// drivers of the hot path: the batched scipy-1.15.3 CG loop (one LD pass per CG
+// iteration serves every right-hand side still iterating), the LMMSE step,
+// the denoiser and the EM prior loop.  Scalar bookkeeping mirrors the
+// reference expressions (src/sgvamp.py cited per line); all vector arithmetic
+// runs in the HIP kernels of ld_pass.hip / vec.hip / synth.hip.
+#include "common.h"
+#include "../../include/sgvamp_hip.h"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <utility>
+#include <vector>
+
+using namespace sgv;
+
+static thread_local std::string g_last_err;
+
+struct sgv_ctx {
+  int dev = 0;
+  hipStream_t st = nullptr;
+  int K = 0, nld = 0;
+  std::vector<int> ld_of;
+  // marker partition
+  int nblk = 0;
+  std::vector<int64_t> bn, boff, bvoff;
+  int64_t Mloc = 0, Mpad = 0;
+  int blk0 = 0, nblk_global = 0;
+  int64_t Mtot = 0;
+  double s = 0.0;
+  std::vector<double> Ncoh;
+  // LD storage [ld][b]
+  std::vector<std::vector<double*>> ldR;
+  std::vector<int64_t> lda;
+  std::vector<BlkDesc*> d_blks;
+  // chunk / row-group layouts
+  int nch = 0;
+  ChunkDesc* d_ch = nullptr;
+  int64_t* d_ch_doff = nullptr;
+  int* d_ch_begin = nullptr;
+  int nrg = 0;
+  RowGroup* d_rg = nullptr;
+  int* d_rg_begin = nullptr;
+  // vectors (padded layout, zero padding)
+  double* pool = nullptr;
+  std::vector<double*> r, r1, r2, U, X, X0, Rr, P, Q, RX0, S;
+  double* xhat1 = nullptr;
+  double* x0 = nullptr;
+  // reductions
+  double* d_part = nullptr;
+  double* d_bsum = nullptr;
+  double* d_bsum_all = nullptr;
+  int* d_counts = nullptr;
+  double* d_tot = nullptr;
+  double* h_tot = nullptr;
+  double* d_pq = nullptr;
+  int nbmax = 0;
+  // staging
+  void* d_stage = nullptr;
+  size_t stage_bytes = 0;
+  // comm
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  // solver state
+  std::vector<int> xnz;        // x0.any() per CG column (2K)
+  std::vector<int> rx0_valid;  // RX0[c] == R_s X[c]
+  // timers
+  std::vector<hipEvent_t> evpool;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  double ld_ms = 0.0, ld_launches = 0.0, rhs_bytes = 0.0;
+  std::string err;
+};
+
+// ---------------------------------------------------------------------------
+// error handling
+// ---------------------------------------------------------------------------
+static int fail(sgv_ctx* c, int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  g_last_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(c, SGV_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                  __LINE__);                                                              \
+  } while (0)
+
+#define NCCLCHK(expr)                                                                     \
+  do {                                                                                    \
+    ncclResult_t e_ = (expr);                                                             \
+    if (e_ != ncclSuccess)                                                                \
+      return fail(c, SGV_ERR_RCCL, "%s: %s (%s:%d)", #expr, ncclGetErrorString(e_),        \
+                  __FILE__, __LINE__);                                                    \
+  } while (0)
+
+#define CHK(expr)               \
+  do {                          \
+    int rc_ = (expr);           \
+    if (rc_ != SGV_OK) return rc_; \
+  } while (0)
+
+#define ENTER(c)                                                   \
+  do {                                                             \
+    if (!(c)) return fail(nullptr, SGV_ERR_ARG, "null context");   \
+    HIPCHK(hipSetDevice((c)->dev));                                \
+  } while (0)
+
+static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+// ---------------------------------------------------------------------------
+// reductions
+// ---------------------------------------------------------------------------
+static Map16 identity_map() {
+  Map16 m;
+  for (int i = 0; i < MAXC * 2; ++i) m.d[i] = i;
+  return m;
+}
+
+static void resolve_timers(sgv_ctx* c) {
+  for (auto& pr : c->pending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) c->ld_ms += ms;
+    c->evpool.push_back(pr.first);
+    c->evpool.push_back(pr.second);
+  }
+  c->pending.clear();
+}
+
+// partials [nparts][nv] -> d_dst[map.d[v]] (global, ordered); stays on device
+static int reduce_dev(sgv_ctx* c, int nv, const int* d_begin, const Map16& map, double* d_dst) {
+  HIPCHK(launch_reduce_blocks(c->d_part, nv, d_begin, c->nblk, c->d_bsum, c->st));
+  const double* src = c->d_bsum;
+  int nr = 1, nbm = c->nblk;
+  if (c->comm) {
+    NCCLCHK(ncclAllGather(c->d_bsum, c->d_bsum_all, (size_t)c->nbmax * nv, ncclDouble, c->comm,
+                          c->st));
+    src = c->d_bsum_all;
+    nr = c->nranks;
+    nbm = c->nbmax;
+  }
+  HIPCHK(launch_reduce_total(src, nr, nbm, nv, c->d_counts, map, d_dst, c->st));
+  return SGV_OK;
+}
+
+static int reduce_host(sgv_ctx* c, int nv, const int* d_begin, double* out) {
+  CHK(reduce_dev(c, nv, d_begin, identity_map(), c->d_tot));
+  HIPCHK(hipMemcpyAsync(c->h_tot, c->d_tot, sizeof(double) * nv, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  resolve_timers(c);
+  std::memcpy(out, c->h_tot, sizeof(double) * nv);
+  return SGV_OK;
+}
+
+static int ensure_stage(sgv_ctx* c, size_t bytes) {
+  if (bytes <= c->stage_bytes) return SGV_OK;
+  if (c->d_stage) HIPCHK(hipFree(c->d_stage));
+  c->d_stage = nullptr;
+  HIPCHK(hipMalloc(&c->d_stage, bytes));
+  c->stage_bytes = bytes;
+  return SGV_OK;
+}
+
+static int upload_vec(sgv_ctx* c, const double* host, double* dpad) {
+  CHK(ensure_stage(c, sizeof(double) * std::max<int64_t>(c->Mloc, 1)));
+  HIPCHK(hipMemcpyAsync(c->d_stage, host, sizeof(double) * c->Mloc, hipMemcpyHostToDevice, c->st));
+  HIPCHK(launch_unpack(c->d_ch, c->nch, c->d_ch_doff, (const double*)c->d_stage, dpad, c->st));
+  return SGV_OK;
+}
+
+static int download_vec(sgv_ctx* c, const double* dpad, double* host) {
+  CHK(ensure_stage(c, sizeof(double) * std::max<int64_t>(c->Mloc, 1)));
+  HIPCHK(launch_pack(c->d_ch, c->nch, c->d_ch_doff, dpad, (double*)c->d_stage, c->st));
+  HIPCHK(hipMemcpyAsync(host, c->d_stage, sizeof(double) * c->Mloc, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return SGV_OK;
+}
+
+static bool host_any(const double* v, int64_t n) {
+  for (int64_t i = 0; i < n; ++i)
+    if (v[i] != 0.0) return true;
+  return false;
+}
+
+// ---------------------------------------------------------------------------
+// LD pass (timed with HIP events on the ctx stream)
+// ---------------------------------------------------------------------------
+static int ld_ensure(sgv_ctx* c, int ld, int b) {
+  if (c->ldR[ld][b]) return SGV_OK;
+  const size_t bytes = sizeof(double) * (size_t)c->lda[b] * (size_t)c->bn[b];
+  double* p = nullptr;
+  HIPCHK(hipMalloc(&p, bytes));
+  HIPCHK(hipMemsetAsync(p, 0, bytes, c->st));
+  c->ldR[ld][b] = p;
+  BlkDesc d{p, c->lda[b], c->bn[b], c->bvoff[b]};
+  HIPCHK(hipMemcpyAsync(c->d_blks[ld] + b, &d, sizeof d, hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return SGV_OK;
+}
+
+static int ld_ready(sgv_ctx* c, int ld) {
+  for (int b = 0; b < c->nblk; ++b)
+    if (!c->ldR[ld][b])
+      return fail(c, SGV_ERR_STATE, "LD matrix %d block %d has not been set", ld, b);
+  return SGV_OK;
+}
+
+static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa) {
+  if (nc <= 0) return SGV_OK;
+  CHK(ld_ready(c, ld));
+  hipEvent_t e0, e1;
+  if (c->evpool.size() < 2) {
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+  } else {
+    e0 = c->evpool.back();
+    c->evpool.pop_back();
+    e1 = c->evpool.back();
+    c->evpool.pop_back();
+  }
+  HIPCHK(hipEventRecord(e0, c->st));
+  HIPCHK(launch_ld_pass(nc, c->d_blks[ld], c->d_rg, c->nrg, pa, c->d_part, c->st));
+  HIPCHK(hipEventRecord(e1, c->st));
+  c->pending.emplace_back(e0, e1);
+  c->ld_launches += 1.0;
+  c->rhs_bytes += 2.0 * nc * (double)c->Mloc * 8.0;
+  return SGV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// batched CG (scipy 1.15.3, iterative.py:375-422) on columns 0..ncol-1.
+// On entry: X = x0, Rr = P = r0 (= b - A x0 or b), rho[c] = r0.r0,
+// atol[c] = rtol*|b|.  Columns with active[c] = 0 are skipped (bnrm2 == 0).
+// Column c uses LD matrix col_ld[c] and A = c1[c] R + c2[c] I.
+// ---------------------------------------------------------------------------
+struct CgCols {
+  int ncol = 0;
+  int col_ld[MAXC];
+  double c1[MAXC], c2[MAXC];
+  double* X[MAXC];
+  double* Rr[MAXC];
+  double* P[MAXC];
+  double* Q[MAXC];
+};
+
+static int cg_loop(sgv_ctx* c, const CgCols& cc, double* rho, const double* atol, int maxiter,
+                   const int* active_in, int* iters, int* info, int* passes) {
+  const int ncol = cc.ncol;
+  int active[MAXC];
+  double rho_prev[MAXC];
+  for (int j = 0; j < ncol; ++j) {
+    active[j] = active_in[j];
+    rho_prev[j] = 0.0;
+    if (!active[j]) {
+      iters[j] = 0;
+      info[j] = 0;
+    }
+  }
+  for (int it = 0; it < maxiter; ++it) {
+    unsigned mask = 0;
+    for (int j = 0; j < ncol; ++j) {
+      if (!active[j]) continue;
+      if (std::sqrt(rho[j]) < atol[j]) {  // iterative.py:398 (strict <)
+        active[j] = 0;
+        iters[j] = it;
+        info[j] = 0;
+        continue;
+      }
+      mask |= 1u << j;
+    }
+    if (!mask) return SGV_OK;
+    if (it > 0) {  // iterative.py:403-407
+      PArgs pa{};
+      pa.ncol = ncol;
+      pa.mask = mask;
+      for (int j = 0; j < ncol; ++j) {
+        pa.P[j] = cc.P[j];
+        pa.Rr[j] = cc.Rr[j];
+        pa.beta[j] = (mask >> j & 1u) ? rho[j] / rho_prev[j] : 0.0;
+      }
+      HIPCHK(launch_cg_p(c->d_ch, c->nch, pa, c->st));
+    }
+    // q = A p (iterative.py:411): one pass per LD matrix over its active columns
+    for (int ld = 0; ld < c->nld; ++ld) {
+      PassArgs pa{};
+      Map16 map = identity_map();
+      int nc = 0;
+      for (int j = 0; j < ncol; ++j) {
+        if (!(mask >> j & 1u) || cc.col_ld[j] != ld) continue;
+        pa.in[nc] = cc.P[j];
+        pa.out[nc] = cc.Q[j];
+        pa.dot[nc] = cc.P[j];
+        pa.c1[nc] = cc.c1[j];
+        pa.c2[nc] = cc.c2[j];
+        map.d[nc] = j;
+        ++nc;
+      }
+      if (!nc) continue;
+      CHK(ld_pass(c, ld, nc, pa));
+      CHK(reduce_dev(c, nc, c->d_rg_begin, map, c->d_pq));
+      if (passes) ++*passes;
+    }
+    // alpha = rho / p.q; x += alpha p; r -= alpha q; rho_new = r.r (:412-415)
+    XrArgs xa{};
+    xa.ncol = ncol;
+    xa.mask = mask;
+    xa.pq = c->d_pq;
+    for (int j = 0; j < ncol; ++j) {
+      xa.X[j] = cc.X[j];
+      xa.Rr[j] = cc.Rr[j];
+      xa.P[j] = cc.P[j];
+      xa.Q[j] = cc.Q[j];
+      xa.rho[j] = rho[j];
+    }
+    HIPCHK(launch_cg_xr(c->d_ch, c->nch, xa, c->d_part, c->st));
+    double rn[MAXC];
+    CHK(reduce_host(c, MAXC, c->d_ch_begin, rn));
+    for (int j = 0; j < ncol; ++j)
+      if (mask >> j & 1u) {
+        rho_prev[j] = rho[j];
+        rho[j] = rn[j];
+      }
+  }
+  for (int j = 0; j < ncol; ++j)
+    if (active[j]) {  // for-loop exhausted (iterative.py:420-422)
+      iters[j] = maxiter;
+      info[j] = maxiter;
+    }
+  return SGV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// lifetime
+// ---------------------------------------------------------------------------
+extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk,
+                          const int64_t* blk_sizes, int blk0, int nblk_global, int64_t M_total,
+                          sgv_ctx** out) {
+  sgv_ctx* c = nullptr;
+  if (!out) return fail(nullptr, SGV_ERR_ARG, "out is null");
+  *out = nullptr;
+  if (K < 1 || K > MAXK) return fail(nullptr, SGV_ERR_ARG, "K=%d outside [1,%d]", K, MAXK);
+  if (nld < 1 || nld > K) return fail(nullptr, SGV_ERR_ARG, "nld=%d outside [1,K]", nld);
+  if (nblk < 1 || !blk_sizes) return fail(nullptr, SGV_ERR_ARG, "need >= 1 LD block");
+  for (int k = 0; k < K; ++k)
+    if (!ld_of || ld_of[k] < 0 || ld_of[k] >= nld)
+      return fail(nullptr, SGV_ERR_ARG, "ld_of[%d] invalid", k);
+  for (int b = 0; b < nblk; ++b)
+    if (blk_sizes[b] < 1 || blk_sizes[b] > (int64_t)1 << 30)
+      return fail(nullptr, SGV_ERR_ARG, "block %d size %lld invalid", b,
+                  (long long)blk_sizes[b]);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(nullptr, SGV_ERR_HIP, "no HIP device visible");
+  if (device < 0 || device >= ndev)
+    return fail(nullptr, SGV_ERR_ARG, "device %d outside [0,%d)", device, ndev);
+
+  c = new sgv_ctx();
+  c->dev = device;
+  c->K = K;
+  c->nld = nld;
+  c->ld_of.assign(ld_of, ld_of + K);
+  c->nblk = nblk;
+  c->blk0 = blk0;
+  c->nblk_global = nblk_global;
+  c->Mtot = M_total;
+  c->Ncoh.assign(K, 1.0);
+  int rc = SGV_OK;
+  auto cleanup = [&](int code) {
+    sgv_destroy(c);
+    return code;
+  };
+  if (hipSetDevice(device) != hipSuccess) return cleanup(fail(nullptr, SGV_ERR_HIP, "hipSetDevice"));
+  if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(nullptr, SGV_ERR_HIP, "hipStreamCreate"));
+
+  // marker layout
+  int64_t off = 0, voff = 0;
+  for (int b = 0; b < nblk; ++b) {
+    c->bn.push_back(blk_sizes[b]);
+    c->boff.push_back(off);
+    c->bvoff.push_back(voff);
+    c->lda.push_back(round_up(blk_sizes[b], PADV));
+    off += blk_sizes[b];
+    voff += round_up(blk_sizes[b], PADV);
+  }
+  c->Mloc = off;
+  c->Mpad = std::max<int64_t>(voff, PADV);
+
+  // chunks and row groups (restart at every block start)
+  std::vector<ChunkDesc> ch;
+  std::vector<int64_t> chdoff;
+  std::vector<int> chb(nblk + 1, 0);
+  std::vector<RowGroup> rg;
+  std::vector<int> rgb(nblk + 1, 0);
+  const int rows = ld_pass_rows_per_group();
+  for (int b = 0; b < nblk; ++b) {
+    chb[b] = (int)ch.size();
+    for (int64_t o = 0; o < c->bn[b]; o += CHUNK) {
+      ch.push_back(ChunkDesc{c->bvoff[b] + o, (int32_t)std::min<int64_t>(CHUNK, c->bn[b] - o), b});
+      chdoff.push_back(c->boff[b] + o);
+    }
+    rgb[b] = (int)rg.size();
+    for (int64_t r0 = 0; r0 < c->bn[b]; r0 += rows) rg.push_back(RowGroup{b, (int32_t)r0});
+  }
+  chb[nblk] = (int)ch.size();
+  rgb[nblk] = (int)rg.size();
+  c->nch = (int)ch.size();
+  c->nrg = (int)rg.size();
+
+#define CREATE_HIP(expr)                                                          \
+  do {                                                                            \
+    hipError_t e_ = (expr);                                                       \
+    if (e_ != hipSuccess)                                                         \
+      return cleanup(fail(nullptr, SGV_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_))); \
+  } while (0)
+
+  CREATE_HIP(hipMalloc(&c->d_ch, sizeof(ChunkDesc) * ch.size()));
+  CREATE_HIP(hipMemcpy(c->d_ch, ch.data(), sizeof(ChunkDesc) * ch.size(), hipMemcpyHostToDevice));
+  CREATE_HIP(hipMalloc(&c->d_ch_doff, sizeof(int64_t) * chdoff.size()));
+  CREATE_HIP(hipMemcpy(c->d_ch_doff, chdoff.data(), sizeof(int64_t) * chdoff.size(),
+                       hipMemcpyHostToDevice));
+  CREATE_HIP(hipMalloc(&c->d_ch_begin, sizeof(int) * chb.size()));
+  CREATE_HIP(hipMemcpy(c->d_ch_begin, chb.data(), sizeof(int) * chb.size(), hipMemcpyHostToDevice));
+  CREATE_HIP(hipMalloc(&c->d_rg, sizeof(RowGroup) * rg.size()));
+  CREATE_HIP(hipMemcpy(c->d_rg, rg.data(), sizeof(RowGroup) * rg.size(), hipMemcpyHostToDevice));
+  CREATE_HIP(hipMalloc(&c->d_rg_begin, sizeof(int) * rgb.size()));
+  CREATE_HIP(hipMemcpy(c->d_rg_begin, rgb.data(), sizeof(int) * rgb.size(), hipMemcpyHostToDevice));
+
+  // LD descriptors
+  c->ldR.assign(nld, std::vector<double*>(nblk, nullptr));
+  for (int l = 0; l < nld; ++l) {
+    BlkDesc* d = nullptr;
+    CREATE_HIP(hipMalloc(&d, sizeof(BlkDesc) * nblk));
+    std::vector<BlkDesc> h(nblk);
+    for (int b = 0; b < nblk; ++b) h[b] = BlkDesc{nullptr, c->lda[b], c->bn[b], c->bvoff[b]};
+    CREATE_HIP(hipMemcpy(d, h.data(), sizeof(BlkDesc) * nblk, hipMemcpyHostToDevice));
+    c->d_blks.push_back(d);
+  }
+
+  // vectors: r, r1, r2, U (K each); xhat1, x0; X, X0, Rr, P, Q, RX0 (2K each);
+  // S: 5 * MAXC scratch columns for the operator-seam entry points
+  const int nvec = 4 * K + 2 + 12 * K + 5 * MAXC;
+  const size_t vbytes = sizeof(double) * (size_t)c->Mpad * nvec;
+  CREATE_HIP(hipMalloc(&c->pool, vbytes));
+  CREATE_HIP(hipMemset(c->pool, 0, vbytes));
+  double* p = c->pool;
+  auto take = [&](std::vector<double*>& v, int n) {
+    for (int i = 0; i < n; ++i) {
+      v.push_back(p);
+      p += c->Mpad;
+    }
+  };
+  take(c->r, K);
+  take(c->r1, K);
+  take(c->r2, K);
+  take(c->U, K);
+  c->xhat1 = p;
+  p += c->Mpad;
+  c->x0 = p;
+  p += c->Mpad;
+  take(c->X, 2 * K);
+  take(c->X0, 2 * K);
+  take(c->Rr, 2 * K);
+  take(c->P, 2 * K);
+  take(c->Q, 2 * K);
+  take(c->RX0, 2 * K);
+  take(c->S, 5 * MAXC);
+
+  const size_t part_n = std::max<size_t>((size_t)c->nch * 32, (size_t)c->nrg * MAXC);
+  CREATE_HIP(hipMalloc(&c->d_part, sizeof(double) * part_n));
+  c->nbmax = nblk;
+  CREATE_HIP(hipMalloc(&c->d_bsum, sizeof(double) * (size_t)nblk * 32));
+  CREATE_HIP(hipMalloc(&c->d_counts, sizeof(int)));
+  CREATE_HIP(hipMemcpy(c->d_counts, &nblk, sizeof(int), hipMemcpyHostToDevice));
+  CREATE_HIP(hipMalloc(&c->d_tot, sizeof(double) * 64));
+  CREATE_HIP(hipMalloc(&c->d_pq, sizeof(double) * 2 * MAXC));
+  CREATE_HIP(hipHostMalloc(&c->h_tot, sizeof(double) * 64));
+  c->xnz.assign(2 * K, 0);
+  c->rx0_valid.assign(2 * K, 0);
+#undef CREATE_HIP
+  (void)rc;
+  *out = c;
+  return SGV_OK;
+}
+
+extern "C" void sgv_destroy(sgv_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->dev);
+  if (c->st) (void)hipStreamSynchronize(c->st);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  for (auto& v : c->ldR)
+    for (double* p : v)
+      if (p) (void)hipFree(p);
+  for (BlkDesc* d : c->d_blks) (void)hipFree(d);
+  (void)hipFree(c->d_ch);
+  (void)hipFree(c->d_ch_doff);
+  (void)hipFree(c->d_ch_begin);
+  (void)hipFree(c->d_rg);
+  (void)hipFree(c->d_rg_begin);
+  (void)hipFree(c->pool);
+  (void)hipFree(c->d_part);
+  (void)hipFree(c->d_bsum);
+  if (c->d_bsum_all) (void)hipFree(c->d_bsum_all);
+  (void)hipFree(c->d_counts);
+  (void)hipFree(c->d_tot);
+  (void)hipFree(c->d_pq);
+  if (c->h_tot) (void)hipHostFree(c->h_tot);
+  if (c->d_stage) (void)hipFree(c->d_stage);
+  for (auto& pr : c->pending) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
+  if (c->st) (void)hipStreamDestroy(c->st);
+  delete c;
+}
+
+extern "C" const char* sgv_last_error(const sgv_ctx* c) {
+  return c ? c->err.c_str() : g_last_err.c_str();
+}
+
+// ---------------------------------------------------------------------------
+// comm
+// ---------------------------------------------------------------------------
+extern "C" int sgv_comm_unique_id(char* id_out) {
+  sgv_ctx* c = nullptr;
+  if (!id_out) return fail(nullptr, SGV_ERR_ARG, "id_out is null");
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  std::memcpy(id_out, &id, sizeof id);
+  return SGV_OK;
+}
+
+extern "C" int sgv_comm_init(sgv_ctx* c, int nranks, int rank, const char* id,
+                             const int* nblk_per_rank) {
+  ENTER(c);
+  if (nranks < 1 || rank < 0 || rank >= nranks || !id || !nblk_per_rank)
+    return fail(c, SGV_ERR_ARG, "bad comm arguments");
+  if (nblk_per_rank[rank] != c->nblk)
+    return fail(c, SGV_ERR_ARG, "nblk_per_rank[%d]=%d != %d", rank, nblk_per_rank[rank], c->nblk);
+  if (nranks == 1) return SGV_OK;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof uid);
+  NCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
+  c->nranks = nranks;
+  c->rank = rank;
+  c->nbmax = *std::max_element(nblk_per_rank, nblk_per_rank + nranks);
+  HIPCHK(hipFree(c->d_bsum));
+  c->d_bsum = nullptr;
+  HIPCHK(hipMalloc(&c->d_bsum, sizeof(double) * (size_t)c->nbmax * 32));
+  HIPCHK(hipMemset(c->d_bsum, 0, sizeof(double) * (size_t)c->nbmax * 32));
+  HIPCHK(hipMalloc(&c->d_bsum_all, sizeof(double) * (size_t)c->nbmax * 32 * nranks));
+  HIPCHK(hipFree(c->d_counts));
+  c->d_counts = nullptr;
+  HIPCHK(hipMalloc(&c->d_counts, sizeof(int) * nranks));
+  HIPCHK(hipMemcpy(c->d_counts, nblk_per_rank, sizeof(int) * nranks, hipMemcpyHostToDevice));
+  return SGV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// inputs
+// ---------------------------------------------------------------------------
+extern "C" int sgv_set_ld_block(sgv_ctx* c, int ld, int b, const double* host, int64_t ld_host) {
+  ENTER(c);
+  if (ld < 0 || ld >= c->nld || b < 0 || b >= c->nblk || !host || ld_host < c->bn[b])
+    return fail(c, SGV_ERR_ARG, "sgv_set_ld_block: bad arguments (ld=%d b=%d)", ld, b);
+  CHK(ld_ensure(c, ld, b));
+  const int64_t n = c->bn[b];
+  HIPCHK(hipMemcpy2D(c->ldR[ld][b], sizeof(double) * c->lda[b], host, sizeof(double) * ld_host,
+                     sizeof(double) * n, n, hipMemcpyHostToDevice));
+  std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), 0);
+  return SGV_OK;
+}
+
+extern "C" int sgv_get_ld_block(sgv_ctx* c, int ld, int b, double* host, int64_t ld_host) {
+  ENTER(c);
+  if (ld < 0 || ld >= c->nld || b < 0 || b >= c->nblk || !host || ld_host < c->bn[b])
+    return fail(c, SGV_ERR_ARG, "sgv_get_ld_block: bad arguments (ld=%d b=%d)", ld, b);
+  CHK(ld_ready(c, ld));
+  const int64_t n = c->bn[b];
+  HIPCHK(hipStreamSynchronize(c->st));
+  HIPCHK(hipMemcpy2D(host, sizeof(double) * ld_host, c->ldR[ld][b], sizeof(double) * c->lda[b],
+                     sizeof(double) * n, n, hipMemcpyDeviceToHost));
+  return SGV_OK;
+}
+
+extern "C" int sgv_set_ridge(sgv_ctx* c, double s) {
+  ENTER(c);
+  c->s = s;
+  std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), 0);
+  return SGV_OK;
+}
+
+extern "C" int sgv_set_cohort_n(sgv_ctx* c, int k, double N) {
+  ENTER(c);
+  if (k < 0 || k >= c->K) return fail(c, SGV_ERR_ARG, "cohort %d", k);
+  c->Ncoh[k] = N;
+  return SGV_OK;
+}
+
+static double* vec_ptr(sgv_ctx* c, int which, int k) {
+  const bool kok = k >= 0 && k < c->K;
+  switch (which) {
+    case SGV_VEC_R: return kok ? c->r[k] : nullptr;
+    case SGV_VEC_R1: return kok ? c->r1[k] : nullptr;
+    case SGV_VEC_XHAT1: return c->xhat1;
+    case SGV_VEC_XHAT2: return kok ? c->X[2 * k] : nullptr;
+    case SGV_VEC_SIG2U: return kok ? c->X[2 * k + 1] : nullptr;
+    case SGV_VEC_X0: return c->x0;
+    default: return nullptr;
+  }
+}
+
+extern "C" int sgv_set_vector(sgv_ctx* c, int which, int k, const double* host) {
+  ENTER(c);
+  double* d = vec_ptr(c, which, k);
+  if (!d || !host) return fail(c, SGV_ERR_ARG, "sgv_set_vector: which=%d k=%d", which, k);
+  CHK(upload_vec(c, host, d));
+  HIPCHK(hipStreamSynchronize(c->st));
+  if (which == SGV_VEC_XHAT2 || which == SGV_VEC_SIG2U) {
+    const int col = 2 * k + (which == SGV_VEC_SIG2U);
+    c->xnz[col] = host_any(host, c->Mloc);
+    c->rx0_valid[col] = 0;
+  }
+  return SGV_OK;
+}
+
+extern "C" int sgv_get_vector(sgv_ctx* c, int which, int k, double* host) {
+  ENTER(c);
+  double* d = vec_ptr(c, which, k);
+  if (!d || !host) return fail(c, SGV_ERR_ARG, "sgv_get_vector: which=%d k=%d", which, k);
+  return download_vec(c, d, host);
+}
+
+// ---------------------------------------------------------------------------
+// synthetic inputs
+// ---------------------------------------------------------------------------
+struct SynthBufs {
+  double *G = nullptr, *mean = nullptr, *sd = nullptr, *vec = nullptr, *g = nullptr;
+  ~SynthBufs() {
+    if (G) (void)hipFree(G);
+    if (mean) (void)hipFree(mean);
+    if (sd) (void)hipFree(sd);
+    if (vec) (void)hipFree(vec);
+    if (g) (void)hipFree(g);
+  }
+};
+
+extern "C" int sgv_synth_ld_g(sgv_ctx* c, int ld, uint64_t seed, int64_t marker0, int Nsamp,
+                              const double* beta, double* g_out) {
+  ENTER(c);
+  if (ld >= c->nld || Nsamp < 2 || !beta || !g_out)
+    return fail(c, SGV_ERR_ARG, "sgv_synth_ld_g: bad arguments");
+  const int64_t nmax = *std::max_element(c->bn.begin(), c->bn.end());
+  const int ldg = (int)round_up(Nsamp, 16);
+  SynthBufs sb;
+  HIPCHK(hipMalloc(&sb.G, sizeof(double) * (size_t)nmax * ldg));
+  HIPCHK(hipMalloc(&sb.mean, sizeof(double) * nmax));
+  HIPCHK(hipMalloc(&sb.sd, sizeof(double) * nmax));
+  HIPCHK(hipMalloc(&sb.vec, sizeof(double) * std::max<int64_t>(c->Mloc, 1)));
+  HIPCHK(hipMalloc(&sb.g, sizeof(double) * Nsamp));
+  HIPCHK(hipMemcpy(sb.vec, beta, sizeof(double) * c->Mloc, hipMemcpyHostToDevice));
+  for (int b = 0; b < c->nblk; ++b) {
+    const int n = (int)c->bn[b];
+    const int64_t gm0 = marker0 + c->boff[b];
+    HIPCHK(launch_geno_stats(seed, gm0, n, Nsamp, sb.mean, sb.sd, c->st));
+    if (ld >= 0) {
+      CHK(ld_ensure(c, ld, b));
+      HIPCHK(launch_geno_G(seed, gm0, n, Nsamp, ldg, sb.mean, sb.sd, sb.G, c->st));
+      HIPCHK(launch_syrk_nt(sb.G, n, Nsamp, ldg, c->ldR[ld][b], c->lda[b], c->st));
+    }
+    HIPCHK(launch_g_accum(seed, gm0, n, Nsamp, sb.mean, sb.sd, sb.vec + c->boff[b], sb.g, c->st));
+    HIPCHK(hipMemcpyAsync(g_out + (size_t)b * Nsamp, sb.g, sizeof(double) * Nsamp,
+                          hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+  }
+  std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), 0);
+  return SGV_OK;
+}
+
+extern "C" int sgv_synth_r(sgv_ctx* c, int k, uint64_t seed, int64_t marker0, int Nsamp,
+                           const double* y) {
+  ENTER(c);
+  if (k < 0 || k >= c->K || Nsamp < 2 || !y) return fail(c, SGV_ERR_ARG, "sgv_synth_r: bad arguments");
+  const int64_t nmax = *std::max_element(c->bn.begin(), c->bn.end());
+  const int ldg = (int)round_up(Nsamp, 16);
+  SynthBufs sb;
+  HIPCHK(hipMalloc(&sb.G, sizeof(double) * (size_t)nmax * ldg));
+  HIPCHK(hipMalloc(&sb.mean, sizeof(double) * nmax));
+  HIPCHK(hipMalloc(&sb.sd, sizeof(double) * nmax));
+  HIPCHK(hipMalloc(&sb.g, sizeof(double) * Nsamp));
+  HIPCHK(hipMemcpy(sb.g, y, sizeof(double) * Nsamp, hipMemcpyHostToDevice));
+  for (int b = 0; b < c->nblk; ++b) {
+    const int n = (int)c->bn[b];
+    const int64_t gm0 = marker0 + c->boff[b];
+    HIPCHK(launch_geno_stats(seed, gm0, n, Nsamp, sb.mean, sb.sd, c->st));
+    HIPCHK(launch_geno_G(seed, gm0, n, Nsamp, ldg, sb.mean, sb.sd, sb.G, c->st));
+    HIPCHK(launch_row_dot(sb.G, n, Nsamp, ldg, sb.g, c->r[k] + c->bvoff[b], c->st));
+  }
+  HIPCHK(hipStreamSynchronize(c->st));
+  return SGV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// denoiser (src/sgvamp.py:93-114, 270-291)
+// ---------------------------------------------------------------------------
+extern "C" int sgv_denoise(sgv_ctx* c, const double* gam1s, const double* a, double lam,
+                           int nslab, const double* omegas, const double* sigmas, double rho,
+                           int damp, double* der_sum) {
+  ENTER(c);
+  if (nslab < 1 || nslab > MAXL || !gam1s || !a || !omegas || !sigmas || !der_sum)
+    return fail(c, SGV_ERR_ARG, "sgv_denoise: bad arguments (nslab=%d)", nslab);
+  DenoiseArgs da{};
+  da.xhat1 = c->xhat1;
+  da.K = c->K;
+  da.nslab = nslab;
+  da.lam = lam;
+  da.rho = rho;
+  da.damp = damp;
+  for (int k = 0; k < c->K; ++k) {
+    da.r1[k] = c->r1[k];
+    da.a[k] = a[k];
+    da.gam1[k] = gam1s[k];
+    da.ag[k] = a[k] * gam1s[k];                        // self.a * gam1s
+    da.sum_ag = (k == 0) ? da.ag[0] : da.sum_ag + da.ag[k];   // builtin sum (:95)
+  }
+  for (int l = 0; l < nslab; ++l) {
+    da.omegas[l] = omegas[l];
+    da.sigmas[l] = sigmas[l];
+    da.s2[l] = 1.0 / (da.sum_ag + 1.0 / sigmas[l]);     // :95
+    da.sq[l] = std::sqrt(da.s2[l] / sigmas[l]);         // np.sqrt(sigma2_meta / sigmas)
+  }
+  HIPCHK(launch_denoise(c->d_ch, c->nch, da, c->d_part, c->st));
+  double tot[MAXK];
+  CHK(reduce_host(c, MAXK, c->d_ch_begin, tot));
+  for (int k = 0; k < c->K; ++k) der_sum[k] = tot[k];
+  return SGV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// EM prior loop (src/sgvamp.py:116-136, 250-257)
+// ---------------------------------------------------------------------------
+extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nslab,
+                      const double* sigmas, int maxit, double* lam_io, double* omegas_io,
+                      int* steps_out, double* final_err_out) {
+  ENTER(c);
+  if (nslab < 1 || nslab > MAXL || !gam1s || !a || !sigmas || !lam_io || !omegas_io)
+    return fail(c, SGV_ERR_ARG, "sgv_em: bad arguments");
+  EmArgs ea{};
+  ea.K = c->K;
+  ea.nslab = nslab;
+  for (int k = 0; k < c->K; ++k) {
+    ea.r1[k] = c->r1[k];
+    ea.a[k] = a[k];
+    ea.gam1[k] = gam1s[k];
+    ea.scl = (k == 0) ? a[0] : ea.scl + a[k];
+  }
+  for (int l = 0; l < nslab; ++l) ea.sigmas[l] = sigmas[l];
+  double lam = *lam_io;
+  double om[MAXL];
+  for (int l = 0; l < nslab; ++l) om[l] = omegas_io[l];
+  double om_err = 0.0, lam_err = 0.0;
+  int steps = 0;
+  for (int it = 0; it < maxit; ++it) {
+    ea.lam = lam;
+    for (int l = 0; l < nslab; ++l) ea.omegas[l] = om[l];
+    HIPCHK(launch_em(c->d_ch, c->nch, ea, c->d_part, c->st));
+    double tot[EM_NV];
+    CHK(reduce_host(c, EM_NV, c->d_ch_begin, tot));
+    const double lam_new = tot[0] / (double)c->Mtot;   // np.mean (:134)
+    double om_new[MAXL];
+    double dn = 0.0, on = 0.0;
+    for (int l = 0; l < nslab; ++l) {
+      om_new[l] = tot[1 + l] / tot[1 + nslab];         // :136
+      const double d = om_new[l] - om[l];
+      dn += d * d;
+      on += om[l] * om[l];
+    }
+    om_err = std::sqrt(dn) / std::sqrt(on);            // :254
+    lam_err = std::fabs(lam_new - lam) / lam_new;      // :255
+    lam = lam_new;
+    for (int l = 0; l < nslab; ++l) om[l] = om_new[l];
+    steps = it + 1;
+    if (om_err < 1e-6 && lam_err < 1e-6) break;        // :256
+  }
+  *lam_io = lam;
+  for (int l = 0; l < nslab; ++l) omegas_io[l] = om[l];
+  if (steps_out) *steps_out = steps;
+  if (final_err_out) *final_err_out = std::max(om_err, lam_err);
+  return SGV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// LMMSE (src/sgvamp.py:301-364)
+// ---------------------------------------------------------------------------
+extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* gam2,
+                         const double* alpha1, const double* alpha2_prev, const int8_t* probes,
+                         int cg_maxit, double rtol, int lmmse_damp, double rho, int learn_gamw,
+                         double* out, int* cg_out, int* passes_out) {
+  ENTER(c);
+  (void)it;
+  if (!gamw || !gam2 || !alpha1 || !alpha2_prev || !probes || !out || !cg_out || cg_maxit < 0)
+    return fail(c, SGV_ERR_ARG, "sgv_lmmse: bad arguments");
+  const int K = c->K, ncol = 2 * K;
+  const double s = c->s;
+  int passes = 0;
+
+  // probes u_k (:326), int8 +-1 -> f64
+  CHK(ensure_stage(c, (size_t)K * std::max<int64_t>(c->Mloc, 1)));
+  HIPCHK(hipMemcpyAsync(c->d_stage, probes, (size_t)K * c->Mloc, hipMemcpyHostToDevice, c->st));
+  for (int k = 0; k < K; ++k)
+    HIPCHK(launch_unpack_i8(c->d_ch, c->nch, c->d_ch_doff,
+                            (const int8_t*)c->d_stage + (size_t)k * c->Mloc, c->U[k], c->st));
+
+  // warm start needs R_s x0 (reused from the previous gamw pass when valid)
+  for (int ld = 0; ld < c->nld; ++ld) {
+    PassArgs pa{};
+    int nc = 0;
+    for (int j = 0; j < ncol; ++j) {
+      if (!c->xnz[j] || c->rx0_valid[j] || c->ld_of[j / 2] != ld) continue;
+      pa.in[nc] = c->X[j];
+      pa.out[nc] = c->RX0[j];
+      pa.dot[nc] = nullptr;
+      pa.c1[nc] = 1.0 - s;
+      pa.c2[nc] = s;
+      ++nc;
+      c->rx0_valid[j] = 1;
+    }
+    if (nc) {
+      CHK(ld_pass(c, ld, nc, pa));
+      ++passes;
+    }
+  }
+
+  // r2, mu2, r0 = b - A x0, p0 = r0 (:305-313, iterative.py:376-392)
+  InitArgs ia{};
+  ia.xhat1 = c->xhat1;
+  ia.K = K;
+  ia.save_x0 = lmmse_damp;
+  for (int k = 0; k < K; ++k) {
+    ia.cp.r[k] = c->r[k];
+    ia.cp.r1[k] = c->r1[k];
+    ia.cp.r2[k] = c->r2[k];
+    ia.cp.u[k] = c->U[k];
+    ia.alpha1[k] = alpha1[k];
+    ia.gamw[k] = gamw[k];
+    ia.gam2[k] = gam2[k];
+  }
+  for (int j = 0; j < ncol; ++j) {
+    ia.col.X[j] = c->X[j];
+    ia.col.X0[j] = c->X0[j];
+    ia.col.Rr[j] = c->Rr[j];
+    ia.col.P[j] = c->P[j];
+    ia.col.Q[j] = c->Q[j];
+    ia.col.RX0[j] = c->RX0[j];
+    ia.warm[j] = c->xnz[j];
+  }
+  HIPCHK(launch_lmmse_init(c->d_ch, c->nch, ia, c->d_part, c->st));
+  double tot[2 * MAXC];
+  CHK(reduce_host(c, 2 * MAXC, c->d_ch_begin, tot));
+  std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), 0);
+
+  CgCols cc;
+  cc.ncol = ncol;
+  double rhov[MAXC], atol[MAXC];
+  int active[MAXC], iters[MAXC], info[MAXC];
+  for (int j = 0; j < ncol; ++j) {
+    const int k = j / 2;
+    cc.col_ld[j] = c->ld_of[k];
+    cc.c1[j] = gamw[k] * (1.0 - s);           // A = gamw R_s + gam2 I (:312)
+    cc.c2[j] = gamw[k] * s + gam2[k];
+    cc.X[j] = c->X[j];
+    cc.Rr[j] = c->Rr[j];
+    cc.P[j] = c->P[j];
+    cc.Q[j] = c->Q[j];
+    const double bn = std::sqrt(tot[j]);      // bnrm2 (iterative.py:376)
+    atol[j] = std::max(0.0, rtol * bn);
+    rhov[j] = tot[MAXC + j];
+    active[j] = 1;
+    if (bn == 0.0) {                          // iterative.py:380-381: return b
+      HIPCHK(hipMemsetAsync(c->X[j], 0, sizeof(double) * c->Mpad, c->st));
+      active[j] = 0;
+    }
+  }
+  CHK(cg_loop(c, cc, rhov, atol, cg_maxit, active, iters, info, &passes));
+
+  // damping, u.Sigma2_u, xhat2.r, x.any() (:322-323, 338, 352)
+  PostArgs po{};
+  po.K = K;
+  po.damp = lmmse_damp;
+  po.rho = rho;
+  for (int j = 0; j < ncol; ++j) {
+    po.X[j] = c->X[j];
+    po.X0[j] = c->X0[j];
+  }
+  for (int k = 0; k < K; ++k) {
+    po.u[k] = c->U[k];
+    po.r[k] = c->r[k];
+  }
+  HIPCHK(launch_lmmse_post(c->d_ch, c->nch, po, c->d_part, c->st));
+  double pt[2 * MAXK + MAXC];
+  CHK(reduce_host(c, 2 * MAXK + MAXC, c->d_ch_begin, pt));
+  for (int j = 0; j < ncol; ++j) c->xnz[j] = pt[2 * MAXK + j] > 0.0;
+
+  R1Args ra{};
+  ra.K = K;
+  for (int k = 0; k < K; ++k) {
+    const double TrSigma2 = pt[k];
+    double a2 = gam2[k] * TrSigma2 / (double)c->Mtot;              // :340
+    if (lmmse_damp) a2 = rho * a2 + (1 - rho) * alpha2_prev[k];    // :345-346
+    const double g1 = gam2[k] * (1 - a2) / a2;                    // :347
+    double* o = out + (size_t)k * SGV_LMMSE_NOUT;
+    o[SGV_O_TRSIGMA2] = TrSigma2;
+    o[SGV_O_ALPHA2] = a2;
+    o[SGV_O_GAM1] = g1;
+    o[SGV_O_XR] = pt[MAXK + k];
+    o[SGV_O_Z] = 0.0;
+    o[SGV_O_TRRSIGMA2] = 0.0;
+    o[SGV_O_XRX] = 0.0;
+    o[SGV_O_GAMW] = gamw[k];
+    ra.X[k] = c->X[2 * k];
+    ra.r2[k] = c->r2[k];
+    ra.r1[k] = c->r1[k];
+    ra.alpha2[k] = a2;
+    cg_out[4 * k + 0] = iters[2 * k];
+    cg_out[4 * k + 1] = info[2 * k];
+    cg_out[4 * k + 2] = iters[2 * k + 1];
+    cg_out[4 * k + 3] = info[2 * k + 1];
+  }
+  HIPCHK(launch_r1_update(c->d_ch, c->nch, ra, c->st));   // :348
+
+  if (learn_gamw) {  // :350-363; R_s [xhat2, Sigma2_u] is also the next warm start's R_s x0
+    for (int ld = 0; ld < c->nld; ++ld) {
+      PassArgs pa{};
+      Map16 map = identity_map();
+      int nc = 0;
+      for (int j = 0; j < ncol; ++j) {
+        const int k = j / 2;
+        if (c->ld_of[k] != ld) continue;
+        pa.in[nc] = c->X[j];
+        pa.out[nc] = c->RX0[j];
+        pa.dot[nc] = (j % 2 == 0) ? c->X[j] : c->U[k];
+        pa.c1[nc] = 1.0 - s;
+        pa.c2[nc] = s;
+        map.d[nc] = j;
+        ++nc;
+        c->rx0_valid[j] = 1;
+      }
+      if (!nc) continue;
+      CHK(ld_pass(c, ld, nc, pa));
+      ++passes;
+      double gt[MAXC];
+      CHK(reduce_dev(c, nc, c->d_rg_begin, map, c->d_tot));
+      HIPCHK(hipMemcpyAsync(c->h_tot, c->d_tot, sizeof(double) * ncol, hipMemcpyDeviceToHost,
+                            c->st));
+      HIPCHK(hipStreamSynchronize(c->st));
+      resolve_timers(c);
+      std::memcpy(gt, c->h_tot, sizeof(double) * ncol);
+      for (int k = 0; k < K; ++k) {
+        if (c->ld_of[k] != ld) continue;
+        const double N = c->Ncoh[k];
+        double* o = out + (size_t)k * SGV_LMMSE_NOUT;
+        const double xRx = gt[2 * k];
+        const double TrRSigma2 = gt[2 * k + 1];
+        double z = N - 2 * o[SGV_O_XR] + xRx;                      // :352
+        if (z < 0) z = 0;                                          // :353-354
+        o[SGV_O_Z] = z;
+        o[SGV_O_XRX] = xRx;
+        o[SGV_O_TRRSIGMA2] = TrRSigma2;
+        o[SGV_O_GAMW] = 1 / (z / N + TrRSigma2 / N);               // :363
+      }
+    }
+  } else {
+    HIPCHK(hipStreamSynchronize(c->st));
+  }
+  if (passes_out) *passes_out = passes;
+  return SGV_OK;
+}
+
+extern "C" int sgv_metrics(sgv_ctx* c, double* out4) {
+  ENTER(c);
+  if (!out4) return fail(c, SGV_ERR_ARG, "out4 is null");
+  HIPCHK(launch_metrics(c->d_ch, c->nch, c->xhat1, c->x0, c->d_part, c->st));
+  return reduce_host(c, 4, c->d_ch_begin, out4);
+}
+
+// ---------------------------------------------------------------------------
+// operator seam (tests): R_s v and a batched CG on (c1 R_s + c2 I)
+// ---------------------------------------------------------------------------
+extern "C" int sgv_ld_matvec(sgv_ctx* c, int ld, int ncol, const double* v, double* y) {
+  ENTER(c);
+  if (ld < 0 || ld >= c->nld || ncol < 1 || ncol > MAXC || !v || !y)
+    return fail(c, SGV_ERR_ARG, "sgv_ld_matvec: bad arguments");
+  PassArgs pa{};
+  for (int j = 0; j < ncol; ++j) {
+    CHK(upload_vec(c, v + (size_t)j * c->Mloc, c->S[j]));
+    pa.in[j] = c->S[j];
+    pa.out[j] = c->S[MAXC + j];
+    pa.dot[j] = nullptr;
+    pa.c1[j] = 1.0 - c->s;
+    pa.c2[j] = c->s;
+  }
+  CHK(ld_pass(c, ld, ncol, pa));
+  for (int j = 0; j < ncol; ++j) CHK(download_vec(c, c->S[MAXC + j], y + (size_t)j * c->Mloc));
+  resolve_timers(c);
+  return SGV_OK;
+}
+
+extern "C" int sgv_cg_solve(sgv_ctx* c, int ld, int ncol, const double* c1, const double* c2,
+                            const double* b, double* x, int maxiter, double rtol, int* iters_out,
+                            int* info_out) {
+  ENTER(c);
+  if (ld < 0 || ld >= c->nld || ncol < 1 || ncol > MAXC || !c1 || !c2 || !b || !x ||
+      !iters_out || !info_out || maxiter < 0)
+    return fail(c, SGV_ERR_ARG, "sgv_cg_solve: bad arguments");
+  double* SB[MAXC];
+  CgCols cc;
+  cc.ncol = ncol;
+  int warm[MAXC];
+  for (int j = 0; j < ncol; ++j) {
+    SB[j] = c->S[j];
+    cc.X[j] = c->S[MAXC + j];
+    cc.Rr[j] = c->S[2 * MAXC + j];
+    cc.P[j] = c->S[3 * MAXC + j];
+    cc.Q[j] = c->S[4 * MAXC + j];
+    cc.col_ld[j] = ld;
+    cc.c1[j] = c1[j] * (1.0 - c->s);
+    cc.c2[j] = c1[j] * c->s + c2[j];
+    CHK(upload_vec(c, b + (size_t)j * c->Mloc, SB[j]));
+    CHK(upload_vec(c, x + (size_t)j * c->Mloc, cc.X[j]));
+    warm[j] = host_any(x + (size_t)j * c->Mloc, c->Mloc);
+  }
+  // r = b - A x0 if x0.any() else b (iterative.py:392)
+  PassArgs pa{};
+  int nc = 0;
+  AxpbyArgs ax{};
+  for (int j = 0; j < ncol; ++j) {
+    HIPCHK(hipMemcpyAsync(cc.Rr[j], SB[j], sizeof(double) * c->Mpad, hipMemcpyDeviceToDevice, c->st));
+    ax.y[j] = cc.Rr[j];
+    ax.x[j] = cc.Q[j];
+    ax.a[j] = 1.0;
+    ax.b[j] = warm[j] ? -1.0 : 0.0;
+    if (!warm[j]) continue;
+    pa.in[nc] = cc.X[j];
+    pa.out[nc] = cc.Q[j];
+    pa.dot[nc] = nullptr;
+    pa.c1[nc] = cc.c1[j];
+    pa.c2[nc] = cc.c2[j];
+    ++nc;
+  }
+  ax.ncol = ncol;
+  if (nc) CHK(ld_pass(c, ld, nc, pa));
+  // map back: the pass wrote Q for warm columns in order; non-warm Q unused (b = 0 weight)
+  HIPCHK(launch_axpby(c->d_ch, c->nch, ax, c->st));
+  DotsArgs da{};
+  da.ncol = 2 * ncol;
+  for (int j = 0; j < ncol; ++j) {
+    da.x[j] = SB[j];
+    da.y[j] = SB[j];
+    da.x[ncol + j] = cc.Rr[j];
+    da.y[ncol + j] = cc.Rr[j];
+    HIPCHK(hipMemcpyAsync(cc.P[j], cc.Rr[j], sizeof(double) * c->Mpad, hipMemcpyDeviceToDevice,
+                          c->st));
+  }
+  if (2 * ncol > MAXC) return fail(c, SGV_ERR_ARG, "sgv_cg_solve: ncol <= %d", MAXC / 2);
+  HIPCHK(launch_dots(c->d_ch, c->nch, da, c->d_part, c->st));
+  double tot[MAXC];
+  CHK(reduce_host(c, MAXC, c->d_ch_begin, tot));
+  double rho[MAXC], atol[MAXC];
+  int active[MAXC];
+  for (int j = 0; j < ncol; ++j) {
+    const double bn = std::sqrt(tot[j]);
+    atol[j] = std::max(0.0, rtol * bn);
+    rho[j] = tot[ncol + j];
+    active[j] = 1;
+    if (bn == 0.0) {
+      HIPCHK(hipMemcpyAsync(cc.X[j], SB[j], sizeof(double) * c->Mpad, hipMemcpyDeviceToDevice, c->st));
+      active[j] = 0;
+    }
+  }
+  CHK(cg_loop(c, cc, rho, atol, maxiter, active, iters_out, info_out, nullptr));
+  for (int j = 0; j < ncol; ++j) CHK(download_vec(c, cc.X[j], x + (size_t)j * c->Mloc));
+  return SGV_OK;
+}
+
+extern "C" int sgv_timers(sgv_ctx* c, double* t4, int reset) {
+  ENTER(c);
+  HIPCHK(hipStreamSynchronize(c->st));
+  resolve_timers(c);
+  if (t4) {
+    double bytes = 0.0;
+    for (int b = 0; b < c->nblk; ++b) bytes += (double)c->bn[b] * (double)c->bn[b] * 8.0;
+    t4[0] = c->ld_ms;
+    t4[1] = c->ld_launches;
+    t4[2] = bytes;
+    t4[3] = c->rhs_bytes;
+  }
+  if (reset) {
+    c->ld_ms = 0.0;
+    c->ld_launches = 0.0;
+    c->rhs_bytes = 0.0;
+  }
+  return SGV_OK;
+}
+
+extern "C" int sgv_sync(sgv_ctx* c) {
+  ENTER(c);
+  HIPCHK(hipStreamSynchronize(c->st));
+  resolve_timers(c);
+  return SGV_OK;
+}

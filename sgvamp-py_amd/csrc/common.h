@@ -1,0 +1,243 @@
+// Internal declarations shared by the HIP translation units of libsgvamp_hip.so.
+// Target: gfx950 (MI355X, CDNA4), wave64.  No other target is built.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace sgv {
+
+constexpr int WAVE = 64;
+constexpr int VTHREADS = 256;   // threads per workgroup of the vector kernels
+constexpr int CHUNK = 1024;     // markers per chunk (vector-kernel workgroup)
+constexpr int PADV = 128;       // per-block padding of device vectors and LD rows (doubles = 1 KiB)
+constexpr int MAXC = 16;        // right-hand-side columns per LD pass (2 x 8 cohorts)
+constexpr int MAXK = 8;         // cohorts
+constexpr int MAXL = 8;         // slab components (L - 1)
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+// One LD block of one LD matrix: n x n dense f64, row-major, row stride lda
+// (multiple of PADV, zero padded); voff = offset of the block's first marker
+// in the padded device vector layout.
+struct BlkDesc {
+  const double* R;
+  int64_t lda;
+  int64_t n;
+  int64_t voff;
+};
+
+// Marker chunk (never crosses an LD block; chunking restarts at every block
+// start, so per-block partial sums do not depend on how blocks are spread
+// over ranks).
+struct ChunkDesc {
+  int64_t voff;
+  int32_t len;
+  int32_t blk;
+};
+
+// Row group of the LD pass: 4 waves x RW rows of block `blk` from row0.
+struct RowGroup {
+  int32_t blk;
+  int32_t row0;
+};
+
+// Columns of one LD pass: out[c] = c1[c] * (R in[c]) + c2[c] * in[c];
+// partial[c] = sum_rows dot[c] * out[c] (dot[c] may be null).
+struct PassArgs {
+  const double* in[MAXC];
+  double* out[MAXC];
+  const double* dot[MAXC];
+  double c1[MAXC];
+  double c2[MAXC];
+};
+
+struct Map16 {
+  int d[MAXC * 2];
+};
+
+// ---- deterministic reductions --------------------------------------------
+// xor-butterfly: every lane ends with the same value (each step adds two
+// values in commutative order), fixed order -> bitwise reproducible.
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+  return v;
+}
+
+// Sum NV per-thread values over a 256-thread workgroup and store NV results
+// at out[0..NV) (fixed order: wave butterfly, then waves 0..3 in order).
+template <int NV>
+__device__ __forceinline__ void block_reduce_store(double (&v)[NV], double* __restrict__ out,
+                                                   int nv_used) {
+  __shared__ double sm[VTHREADS / WAVE][NV];
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double s = wave_sum(v[k]);
+    if (lane == 0) sm[wid][k] = s;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nv_used) {
+    const int t = threadIdx.x;
+    out[t] = ((sm[0][t] + sm[1][t]) + sm[2][t]) + sm[3][t];
+  }
+}
+
+// ---- launchers (defined in the .hip files) ------------------------------
+// LD pass: one workgroup per row group; partials[g * nc + c].
+hipError_t launch_ld_pass(int nc, const BlkDesc* d_blks, const RowGroup* d_rg, int nrg,
+                          const PassArgs& pa, double* d_partials, hipStream_t st);
+int ld_pass_rows_per_group();
+
+// Reductions: partials[part * nv + v] with parts of local block b in
+// [begin[b], begin[b+1]) -> bsum[b * nv + v] (fixed order), then
+// total[v] = sum over all ranks' blocks in global block order, written to
+// dst[map.d[v]].
+hipError_t launch_reduce_blocks(const double* d_part, int nv, const int* d_begin, int nblk,
+                                double* d_bsum, hipStream_t st);
+hipError_t launch_reduce_total(const double* d_bsum_all, int nranks, int nbmax, int nv,
+                               const int* d_counts, const Map16& map, double* d_dst,
+                               hipStream_t st);
+
+// Vector kernels (vec.hip) ------------------------------------------------
+struct DenoiseArgs {
+  const double* r1[MAXK];
+  double* xhat1;
+  double ag[MAXK];          // a_k * gam1_k
+  double a[MAXK], gam1[MAXK];
+  double sum_ag;            // builtin sum over k, src/sgvamp.py:95
+  double lam;
+  int K, nslab;
+  double omegas[MAXL], sigmas[MAXL];
+  double s2[MAXL];          // sigma2_meta (shared by all markers)
+  double sq[MAXL];          // sqrt(sigma2_meta / sigmas)
+  double rho;
+  int damp;
+};
+hipError_t launch_denoise(const ChunkDesc* d_ch, int nch, const DenoiseArgs& a, double* d_part,
+                          hipStream_t st);
+
+struct EmArgs {
+  const double* r1[MAXK];
+  double a[MAXK];
+  double gam1[MAXK];
+  double scl;               // sum_k a_k (np.average weights)
+  double lam;
+  int K, nslab;
+  double omegas[MAXL], sigmas[MAXL];
+};
+constexpr int EM_NV = MAXL + 2;   // [0] sum_j avg_k(pi); [1..L-1] omega numerators; [nslab+1] denominator
+hipError_t launch_em(const ChunkDesc* d_ch, int nch, const EmArgs& a, double* d_part,
+                     hipStream_t st);
+
+struct CohortPtrs {
+  const double* r[MAXK];
+  const double* r1[MAXK];
+  double* r2[MAXK];
+  const double* u[MAXK];
+};
+struct ColPtrs {
+  double* X[MAXC];
+  double* X0[MAXC];
+  double* Rr[MAXC];
+  double* P[MAXC];
+  double* Q[MAXC];
+  const double* RX0[MAXC];
+};
+struct InitArgs {
+  CohortPtrs cp;
+  ColPtrs col;
+  const double* xhat1;
+  int K;
+  double alpha1[MAXK], gamw[MAXK], gam2[MAXK];
+  int warm[MAXC];           // residual r = b - A x0 (x0.any()); else r = b
+  int save_x0;              // copy X[2k] to X0[2k] (LMMSE damping)
+};
+hipError_t launch_lmmse_init(const ChunkDesc* d_ch, int nch, const InitArgs& a, double* d_part,
+                             hipStream_t st);
+
+struct XrArgs {
+  double* X[MAXC];
+  double* Rr[MAXC];
+  const double* P[MAXC];
+  const double* Q[MAXC];
+  double rho[MAXC];
+  const double* pq;         // device, indexed by column
+  unsigned mask;
+  int ncol;
+};
+hipError_t launch_cg_xr(const ChunkDesc* d_ch, int nch, const XrArgs& a, double* d_part,
+                        hipStream_t st);
+
+struct PArgs {
+  double* P[MAXC];
+  const double* Rr[MAXC];
+  double beta[MAXC];
+  unsigned mask;
+  int ncol;
+};
+hipError_t launch_cg_p(const ChunkDesc* d_ch, int nch, const PArgs& a, hipStream_t st);
+
+struct PostArgs {
+  double* X[MAXC];
+  const double* X0[MAXC];
+  const double* u[MAXK];
+  const double* r[MAXK];
+  int K;
+  int damp;
+  double rho;
+};
+hipError_t launch_lmmse_post(const ChunkDesc* d_ch, int nch, const PostArgs& a, double* d_part,
+                             hipStream_t st);
+
+struct R1Args {
+  const double* X[MAXK];    // xhat2_k
+  const double* r2[MAXK];
+  double* r1[MAXK];
+  double alpha2[MAXK];
+  int K;
+};
+hipError_t launch_r1_update(const ChunkDesc* d_ch, int nch, const R1Args& a, hipStream_t st);
+
+hipError_t launch_metrics(const ChunkDesc* d_ch, int nch, const double* xhat1, const double* x0,
+                          double* d_part, hipStream_t st);
+
+// generic column dots over chunks: part[c] = sum x[c]*y[c]
+struct DotsArgs {
+  const double* x[MAXC];
+  const double* y[MAXC];
+  int ncol;
+};
+hipError_t launch_dots(const ChunkDesc* d_ch, int nch, const DotsArgs& a, double* d_part,
+                       hipStream_t st);
+
+// scatter dense local vector -> padded layout and back
+hipError_t launch_unpack(const ChunkDesc* d_ch, int nch, const int64_t* d_dense_off,
+                         const double* src_dense, double* dst_pad, hipStream_t st);
+hipError_t launch_unpack_i8(const ChunkDesc* d_ch, int nch, const int64_t* d_dense_off,
+                            const int8_t* src_dense, double* dst_pad, hipStream_t st);
+hipError_t launch_pack(const ChunkDesc* d_ch, int nch, const int64_t* d_dense_off,
+                       const double* src_pad, double* dst_dense, hipStream_t st);
+// y[c] = a[c] * y[c] + b[c] * x[c]
+struct AxpbyArgs {
+  double* y[MAXC];
+  const double* x[MAXC];
+  double a[MAXC], b[MAXC];
+  int ncol;
+};
+hipError_t launch_axpby(const ChunkDesc* d_ch, int nch, const AxpbyArgs& a, hipStream_t st);
+
+// Synthetic generator (synth.hip) ----------------------------------------
+hipError_t launch_geno_stats(uint64_t seed, int64_t gmarker0, int n, int nsamp, double* d_mean,
+                             double* d_std, hipStream_t st);
+hipError_t launch_geno_G(uint64_t seed, int64_t gmarker0, int n, int nsamp, int ldg,
+                         const double* d_mean, const double* d_std, double* d_G,
+                         hipStream_t st);
+hipError_t launch_syrk_nt(const double* d_G, int n, int nsamp, int ldg, double* d_R, int64_t lda,
+                          hipStream_t st);
+hipError_t launch_g_accum(uint64_t seed, int64_t gmarker0, int n, int nsamp, const double* d_mean,
+                          const double* d_std, const double* d_beta, double* d_g, hipStream_t st);
+hipError_t launch_row_dot(const double* d_G, int n, int nsamp, int ldg, const double* d_y,
+                          double* d_out, hipStream_t st);
+
+}  // namespace sgv

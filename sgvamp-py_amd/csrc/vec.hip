@@ -1,0 +1,458 @@
+// Marker-wise kernels of the sgVAMP outer iteration and the ordered reductions.
+// Compiled with -ffp-contract=off so expressions round like the reference's
+// NumPy code (one rounding per operation, reference operand order).
+//
+// Every kernel walks "chunks" (<= CHUNK markers inside one LD block) and writes
+// one partial per chunk; launch_reduce_* turn those into per-block sums and
+// the global total in block order (bitwise independent of the GPU count).
+#include "common.h"
+
+namespace sgv {
+
+#define CHUNK_LOOP(ch)                                                  \
+  for (int t = threadIdx.x; t < (ch).len; t += VTHREADS)
+
+// ---------------------------------------------------------------------------
+// denoiser_meta + der_denoiser_meta, src/sgvamp.py:93-114, per marker (:273,285)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restrict__ chs,
+                                                      DenoiseArgs a,
+                                                      double* __restrict__ part) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  double acc[MAXK];
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) acc[k] = 0.0;
+  CHUNK_LOOP(ch) {
+    const int64_t i = ch.voff + t;
+    // np.inner(rs, a*gam1s) (:96)
+    double inner = 0.0;
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k)
+      if (k < a.K) inner = (k == 0) ? a.r1[0][i] * a.ag[0] : inner + a.r1[k][i] * a.ag[k];
+    double mu[MAXL];
+    int m = 0;
+    double best = 0.0;
+#pragma unroll
+    for (int l = 0; l < MAXL; ++l)
+      if (l < a.nslab) {
+        mu[l] = inner * a.s2[l];
+        const double ratio = mu[l] * mu[l] / a.s2[l];   // :97
+        if (l == 0 || ratio > best) {                   // argmax: first maximum
+          best = ratio;
+          m = l;
+        }
+      }
+    double s2m = a.s2[0], mum = mu[0];
+#pragma unroll
+    for (int l = 1; l < MAXL; ++l)
+      if (l < a.nslab && l == m) {
+        s2m = a.s2[l];
+        mum = mu[l];
+      }
+    double EXP[MAXL];
+    double sumN = 0.0, sumD = 0.0;
+#pragma unroll
+    for (int l = 0; l < MAXL; ++l)
+      if (l < a.nslab) {
+        EXP[l] = exp(0.5 * (mu[l] * mu[l] * s2m - mum * mum * a.s2[l]) / (a.s2[l] * s2m));  // :98
+        const double tn = a.omegas[l] * EXP[l] * mu[l] * a.sq[l];                           // :99
+        const double td = a.omegas[l] * EXP[l] * a.sq[l];                                   // :101
+        sumN = (l == 0) ? tn : sumN + tn;
+        sumD = (l == 0) ? td : sumD + td;
+      }
+    const double Num = a.lam * sumN;
+    const double EXP2 = exp(-0.5 * (mum * mum / s2m));   // :100
+    const double Den = (1 - a.lam) * EXP2 + a.lam * sumD;
+    double x = Num / Den;
+    if (a.damp) x = a.rho * x + (1 - a.rho) * a.xhat1[i];   // :275-276
+    a.xhat1[i] = x;
+    // der_denoiser_meta for every cohort k (:112-114 with a[k]*gam1s[k])
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k)
+      if (k < a.K) {
+        double dn = 0.0, dd = 0.0;
+#pragma unroll
+        for (int l = 0; l < MAXL; ++l)
+          if (l < a.nslab) {
+            const double tn = a.omegas[l] * EXP[l] * (mu[l] * mu[l] + a.s2[l]) * a.a[k] *
+                              a.gam1[k] * a.sq[l];
+            const double td = a.omegas[l] * mu[l] * EXP[l] * a.a[k] * a.gam1[k] * a.sq[l];
+            dn = (l == 0) ? tn : dn + tn;
+            dd = (l == 0) ? td : dd + td;
+          }
+        const double DerNum = a.lam * dn;
+        const double DerDen = a.lam * dd;
+        acc[k] += (DerNum * Den - DerDen * Num) / (Den * Den);
+      }
+  }
+  block_reduce_store<MAXK>(acc, part + (int64_t)blockIdx.x * MAXK, MAXK);
+}
+
+hipError_t launch_denoise(const ChunkDesc* d_ch, int nch, const DenoiseArgs& a, double* d_part,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(k_denoise, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// prior_update_em, src/sgvamp.py:116-136 (one EM step)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(VTHREADS) void k_em(const ChunkDesc* __restrict__ chs, EmArgs a,
+                                                 double* __restrict__ part) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  double acc[EM_NV];
+#pragma unroll
+  for (int v = 0; v < EM_NV; ++v) acc[v] = 0.0;
+  CHUNK_LOOP(ch) {
+    const int64_t i = ch.voff + t;
+    double avg = 0.0;   // sum_k pi_k a_k (np.average numerator, sequential over k)
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k)
+      if (k < a.K) {
+        const double r = a.r1[k][i];
+        const double r2 = r * r;                  // np.power(r1s, 2)
+        const double ginv = 1.0 / a.gam1[k];      // gam1invs
+        double tl[MAXL];
+        double emax = 0.0;
+#pragma unroll
+        for (int l = 0; l < MAXL; ++l)
+          if (l < a.nslab) {
+            tl[l] = -r2 / 2 / (a.sigmas[l] + ginv);          // :127
+            emax = (l == 0 || tl[l] > emax) ? tl[l] : emax;
+          }
+        double xi[MAXL];
+        double sum_xi = 0.0;
+#pragma unroll
+        for (int l = 0; l < MAXL; ++l)
+          if (l < a.nslab) {
+            xi[l] = a.lam * a.omegas[l] * exp(tl[l] - emax) / sqrt(ginv + a.sigmas[l]);   // :128
+            sum_xi = (l == 0) ? xi[l] : sum_xi + xi[l];                                   // :129
+          }
+        const double pi =
+            1.0 / (1.0 + (1 - a.lam) * exp(-r2 / 2 * a.gam1[k] - emax) / sqrt(ginv) / sum_xi);  // :131
+        const double pa = pi * a.a[k];
+        avg = (k == 0) ? pa : avg + pa;
+#pragma unroll
+        for (int l = 0; l < MAXL; ++l)
+          if (l < a.nslab) acc[1 + l] += pi * (xi[l] / sum_xi) * a.a[k];   // :136 numerator
+        acc[1 + a.nslab] += pa;                                           // :136 denominator
+      }
+    acc[0] += avg / a.scl;   // np.average(pi, axis=0, weights=a)  (:134)
+  }
+  block_reduce_store<EM_NV>(acc, part + (int64_t)blockIdx.x * EM_NV, EM_NV);
+}
+
+hipError_t launch_em(const ChunkDesc* d_ch, int nch, const EmArgs& a, double* d_part,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(k_em, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// LMMSE set-up, src/sgvamp.py:305-313 + scipy cg prologue (iterative.py:375-392)
+// partials: [c] = |b_c|^2, [MAXC + c] = |r0_c|^2
+// ---------------------------------------------------------------------------
+constexpr int INIT_NV = 2 * MAXC;
+__global__ __launch_bounds__(VTHREADS) void k_lmmse_init(const ChunkDesc* __restrict__ chs,
+                                                         InitArgs a,
+                                                         double* __restrict__ part) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  double acc[INIT_NV];
+#pragma unroll
+  for (int v = 0; v < INIT_NV; ++v) acc[v] = 0.0;
+  CHUNK_LOOP(ch) {
+    const int64_t i = ch.voff + t;
+    const double x1 = a.xhat1[i];
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k)
+      if (k < a.K) {
+        const double r2 = (x1 - a.alpha1[k] * a.cp.r1[k][i]) / (1 - a.alpha1[k]);   // :310
+        a.cp.r2[k][i] = r2;
+        const double b1 = a.gamw[k] * a.cp.r[k][i] + a.gam2[k] * r2;               // :313
+        const double b2 = a.cp.u[k][i];                                            // :326
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int c = 2 * k + h;
+          const double b = h == 0 ? b1 : b2;
+          double r = b;
+          if (a.warm[c]) {
+            // r = b - A x0, A x0 = gamw (R_s x0) + gam2 x0 (:312; R_s x0 from the last gamw pass)
+            const double ax = a.gamw[k] * a.col.RX0[c][i] + a.gam2[k] * a.col.X[c][i];
+            r = b - ax;
+          }
+          a.col.Rr[c][i] = r;
+          a.col.P[c][i] = r;
+          acc[c] += b * b;
+          acc[MAXC + c] += r * r;
+        }
+        if (a.save_x0) a.col.X0[2 * k][i] = a.col.X[2 * k][i];
+      }
+  }
+  block_reduce_store<INIT_NV>(acc, part + (int64_t)blockIdx.x * INIT_NV, INIT_NV);
+}
+
+hipError_t launch_lmmse_init(const ChunkDesc* d_ch, int nch, const InitArgs& a, double* d_part,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(k_lmmse_init, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// CG update (iterative.py:412-415): alpha = rho / (p.q); x += alpha p;
+// r -= alpha q; partial rho_new = r.r  (partials [c], stride MAXC)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(VTHREADS) void k_cg_xr(const ChunkDesc* __restrict__ chs, XrArgs a,
+                                                    double* __restrict__ part) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  double acc[MAXC];
+  double alpha[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    acc[c] = 0.0;
+    alpha[c] = (c < a.ncol && ((a.mask >> c) & 1u)) ? a.rho[c] / a.pq[c] : 0.0;
+  }
+  CHUNK_LOOP(ch) {
+    const int64_t i = ch.voff + t;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      if (c < a.ncol && ((a.mask >> c) & 1u)) {
+        a.X[c][i] = a.X[c][i] + alpha[c] * a.P[c][i];
+        const double r = a.Rr[c][i] - alpha[c] * a.Q[c][i];
+        a.Rr[c][i] = r;
+        acc[c] += r * r;
+      }
+  }
+  block_reduce_store<MAXC>(acc, part + (int64_t)blockIdx.x * MAXC, MAXC);
+}
+
+hipError_t launch_cg_xr(const ChunkDesc* d_ch, int nch, const XrArgs& a, double* d_part,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(k_cg_xr, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part);
+  return hipGetLastError();
+}
+
+// p = beta p + r   (iterative.py:405-407: p *= beta; p += z)
+__global__ __launch_bounds__(VTHREADS) void k_cg_p(const ChunkDesc* __restrict__ chs, PArgs a) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  CHUNK_LOOP(ch) {
+    const int64_t i = ch.voff + t;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      if (c < a.ncol && ((a.mask >> c) & 1u)) a.P[c][i] = a.P[c][i] * a.beta[c] + a.Rr[c][i];
+  }
+}
+
+hipError_t launch_cg_p(const ChunkDesc* d_ch, int nch, const PArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(k_cg_p, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// after both CG solves (src/sgvamp.py:322-338,352):
+//   xhat2 damping; partials [k] = u.Sigma2_u, [MAXK + k] = xhat2.r,
+//   [2 MAXK + c] = count(x_c != 0)  (next iteration's x0.any())
+// ---------------------------------------------------------------------------
+constexpr int POST_NV = 2 * MAXK + MAXC;
+__global__ __launch_bounds__(VTHREADS) void k_lmmse_post(const ChunkDesc* __restrict__ chs,
+                                                         PostArgs a,
+                                                         double* __restrict__ part) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  double acc[POST_NV];
+#pragma unroll
+  for (int v = 0; v < POST_NV; ++v) acc[v] = 0.0;
+  CHUNK_LOOP(ch) {
+    const int64_t i = ch.voff + t;
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k)
+      if (k < a.K) {
+        double x2 = a.X[2 * k][i];
+        if (a.damp) {
+          x2 = a.rho * x2 + (1 - a.rho) * a.X0[2 * k][i];   // :322-323
+          a.X[2 * k][i] = x2;
+        }
+        const double s2u = a.X[2 * k + 1][i];
+        acc[k] += a.u[k][i] * s2u;                          // :338
+        acc[MAXK + k] += x2 * a.r[k][i];                    // :352
+        acc[2 * MAXK + 2 * k] += (x2 != 0.0) ? 1.0 : 0.0;
+        acc[2 * MAXK + 2 * k + 1] += (s2u != 0.0) ? 1.0 : 0.0;
+      }
+  }
+  block_reduce_store<POST_NV>(acc, part + (int64_t)blockIdx.x * POST_NV, POST_NV);
+}
+
+hipError_t launch_lmmse_post(const ChunkDesc* d_ch, int nch, const PostArgs& a, double* d_part,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(k_lmmse_post, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part);
+  return hipGetLastError();
+}
+
+// r1 = (xhat2 - alpha2 r2) / (1 - alpha2)   (src/sgvamp.py:348)
+__global__ __launch_bounds__(VTHREADS) void k_r1_update(const ChunkDesc* __restrict__ chs,
+                                                        R1Args a) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  CHUNK_LOOP(ch) {
+    const int64_t i = ch.voff + t;
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k)
+      if (k < a.K) a.r1[k][i] = (a.X[k][i] - a.alpha2[k] * a.r2[k][i]) / (1 - a.alpha2[k]);
+  }
+}
+
+hipError_t launch_r1_update(const ChunkDesc* d_ch, int nch, const R1Args& a, hipStream_t st) {
+  hipLaunchKernelGGL(k_r1_update, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a);
+  return hipGetLastError();
+}
+
+// metrics (src/sgvamp.py:381-382): <x,x0>, |x|^2, |x-x0|^2, |x0|^2
+__global__ __launch_bounds__(VTHREADS) void k_metrics(const ChunkDesc* __restrict__ chs,
+                                                      const double* __restrict__ x,
+                                                      const double* __restrict__ x0,
+                                                      double* __restrict__ part) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  CHUNK_LOOP(ch) {
+    const int64_t i = ch.voff + t;
+    const double a = x[i], b = x0[i], d = a - b;
+    acc[0] += a * b;
+    acc[1] += a * a;
+    acc[2] += d * d;
+    acc[3] += b * b;
+  }
+  block_reduce_store<4>(acc, part + (int64_t)blockIdx.x * 4, 4);
+}
+
+hipError_t launch_metrics(const ChunkDesc* d_ch, int nch, const double* xhat1, const double* x0,
+                          double* d_part, hipStream_t st) {
+  hipLaunchKernelGGL(k_metrics, dim3(nch), dim3(VTHREADS), 0, st, d_ch, xhat1, x0, d_part);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(VTHREADS) void k_dots(const ChunkDesc* __restrict__ chs, DotsArgs a,
+                                                   double* __restrict__ part) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  double acc[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) acc[c] = 0.0;
+  CHUNK_LOOP(ch) {
+    const int64_t i = ch.voff + t;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      if (c < a.ncol) acc[c] += a.x[c][i] * a.y[c][i];
+  }
+  block_reduce_store<MAXC>(acc, part + (int64_t)blockIdx.x * MAXC, MAXC);
+}
+
+hipError_t launch_dots(const ChunkDesc* d_ch, int nch, const DotsArgs& a, double* d_part,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(k_dots, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(VTHREADS) void k_axpby(const ChunkDesc* __restrict__ chs,
+                                                    AxpbyArgs a) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  CHUNK_LOOP(ch) {
+    const int64_t i = ch.voff + t;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      if (c < a.ncol) a.y[c][i] = a.a[c] * a.y[c][i] + a.b[c] * a.x[c][i];
+  }
+}
+
+hipError_t launch_axpby(const ChunkDesc* d_ch, int nch, const AxpbyArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(k_axpby, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a);
+  return hipGetLastError();
+}
+
+// dense <-> padded layout ----------------------------------------------------
+__global__ __launch_bounds__(VTHREADS) void k_unpack(const ChunkDesc* __restrict__ chs,
+                                                     const int64_t* __restrict__ doff,
+                                                     const double* __restrict__ src,
+                                                     double* __restrict__ dst) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  const int64_t o = doff[blockIdx.x];
+  CHUNK_LOOP(ch) dst[ch.voff + t] = src[o + t];
+}
+__global__ __launch_bounds__(VTHREADS) void k_unpack_i8(const ChunkDesc* __restrict__ chs,
+                                                        const int64_t* __restrict__ doff,
+                                                        const int8_t* __restrict__ src,
+                                                        double* __restrict__ dst) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  const int64_t o = doff[blockIdx.x];
+  CHUNK_LOOP(ch) dst[ch.voff + t] = (double)src[o + t];
+}
+__global__ __launch_bounds__(VTHREADS) void k_pack(const ChunkDesc* __restrict__ chs,
+                                                   const int64_t* __restrict__ doff,
+                                                   const double* __restrict__ src,
+                                                   double* __restrict__ dst) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  const int64_t o = doff[blockIdx.x];
+  CHUNK_LOOP(ch) dst[o + t] = src[ch.voff + t];
+}
+
+hipError_t launch_unpack(const ChunkDesc* d_ch, int nch, const int64_t* d_doff,
+                         const double* src, double* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_unpack, dim3(nch), dim3(VTHREADS), 0, st, d_ch, d_doff, src, dst);
+  return hipGetLastError();
+}
+hipError_t launch_unpack_i8(const ChunkDesc* d_ch, int nch, const int64_t* d_doff,
+                            const int8_t* src, double* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_unpack_i8, dim3(nch), dim3(VTHREADS), 0, st, d_ch, d_doff, src, dst);
+  return hipGetLastError();
+}
+hipError_t launch_pack(const ChunkDesc* d_ch, int nch, const int64_t* d_doff, const double* src,
+                       double* dst, hipStream_t st) {
+  hipLaunchKernelGGL(k_pack, dim3(nch), dim3(VTHREADS), 0, st, d_ch, d_doff, src, dst);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// ordered reductions
+// ---------------------------------------------------------------------------
+// grid (nblk, nv), one wave: bsum[b * nv + v] = sum of parts [begin[b], begin[b+1])
+__global__ __launch_bounds__(WAVE) void k_reduce_blocks(const double* __restrict__ part, int nv,
+                                                        const int* __restrict__ begin,
+                                                        double* __restrict__ bsum) {
+  const int b = blockIdx.x, v = blockIdx.y, lane = threadIdx.x;
+  const int p0 = begin[b], p1 = begin[b + 1];
+  double s = 0.0;
+  for (int p = p0 + lane; p < p1; p += WAVE) s += part[(int64_t)p * nv + v];
+  s = wave_sum(s);
+  if (lane == 0) bsum[(int64_t)b * nv + v] = s;
+}
+
+hipError_t launch_reduce_blocks(const double* d_part, int nv, const int* d_begin, int nblk,
+                                double* d_bsum, hipStream_t st) {
+  hipLaunchKernelGGL(k_reduce_blocks, dim3(nblk, nv), dim3(WAVE), 0, st, d_part, nv, d_begin,
+                     d_bsum);
+  return hipGetLastError();
+}
+
+// total[v] = sum over ranks r, local blocks b < counts[r] (global block order)
+__global__ void k_reduce_total(const double* __restrict__ bsum_all, int nranks, int nbmax, int nv,
+                               const int* __restrict__ counts, Map16 map,
+                               double* __restrict__ dst) {
+  const int v = threadIdx.x;
+  if (v >= nv) return;
+  double s = 0.0;
+  bool first = true;
+  for (int r = 0; r < nranks; ++r) {
+    const int nb = counts[r];
+    for (int b = 0; b < nb; ++b) {
+      const double x = bsum_all[((int64_t)r * nbmax + b) * nv + v];
+      s = first ? x : s + x;
+      first = false;
+    }
+  }
+  dst[map.d[v]] = s;
+}
+
+hipError_t launch_reduce_total(const double* d_bsum_all, int nranks, int nbmax, int nv,
+                               const int* d_counts, const Map16& map, double* d_dst,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(k_reduce_total, dim3(1), dim3(64), 0, st, d_bsum_all, nranks, nbmax, nv,
+                     d_counts, map, d_dst);
+  return hipGetLastError();
+}
+
+}  // namespace sgv

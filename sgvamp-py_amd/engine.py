@@ -1,0 +1,167 @@
+"""Shard-aware wrapper over one sgv_ctx: this rank's LD blocks, all cohorts.
+
+An Engine owns the rank-local slice [marker0, marker0 + Mloc) of every
+marker-length vector; every M-length reduction inside the library is ordered
+by global LD block, so the scalars it returns are identical on every rank and
+for any number of ranks.
+"""
+import numpy as np
+
+import hip_backend as hb
+from partition import marker_offsets, partition_blocks
+
+
+class Engine:
+    def __init__(self, block_sizes, K, ld_of=None, comm=None, device=None):
+        """block_sizes: global LD block sizes (marker order).  ld_of[k]: index of
+        the LD matrix cohort k uses (cohorts sharing an LD share LD passes)."""
+        from comm import SingleComm
+
+        self.comm = comm or SingleComm()
+        self.rank = self.comm.Get_rank()
+        self.nranks = self.comm.Get_size()
+        self.block_sizes = [int(b) for b in block_sizes]
+        self.K = int(K)
+        self.ld_of = list(ld_of) if ld_of is not None else [0] * self.K
+        if len(self.ld_of) != self.K:
+            raise ValueError("ld_of must have K entries")
+        # canonical LD ids 0..nld-1 in order of first use
+        remap = {}
+        for l in self.ld_of:
+            remap.setdefault(l, len(remap))
+        self.ld_of = [remap[l] for l in self.ld_of]
+        self.nld = len(remap)
+        self.ranges = partition_blocks(self.block_sizes, self.nranks)
+        self.b0, self.b1 = self.ranges[self.rank]
+        offs = marker_offsets(self.block_sizes)
+        self.M = int(offs[-1])
+        self.marker0 = int(offs[self.b0])
+        self.Mloc = int(offs[self.b1] - offs[self.b0])
+        self.local_sizes = self.block_sizes[self.b0:self.b1]
+        self.sl = slice(self.marker0, self.marker0 + self.Mloc)
+        if device is None:
+            device = self.rank if self.nranks > 1 else 0
+        self.ctx = hb.Context(device, self.K, self.ld_of, self.local_sizes, self.b0,
+                              len(self.block_sizes), self.M)
+        if self.nranks > 1:
+            uid = hb.unique_id() if self.rank == 0 else None
+            uid = self.comm.bcast(uid, root=0)
+            counts = np.array([r1 - r0 for r0, r1 in self.ranges], dtype=np.int32)
+            self.ctx.sgv_comm_init(self.nranks, self.rank, uid, hb.iptr(counts))
+
+    # ---- inputs ----------------------------------------------------------
+    def set_ld_block(self, ld, b_global, block):
+        """Upload LD block b_global of LD matrix `ld` if this rank owns it."""
+        if not (self.b0 <= b_global < self.b1):
+            return
+        B = np.ascontiguousarray(block, dtype=np.float64)
+        n = self.block_sizes[b_global]
+        if B.shape != (n, n):
+            raise ValueError("LD block %d has shape %s, expected (%d, %d)" % (b_global, B.shape, n, n))
+        self.ctx.sgv_set_ld_block(ld, b_global - self.b0, hb.dptr(B), n)
+
+    def get_ld_block(self, ld, b_global):
+        n = self.block_sizes[b_global]
+        out = np.empty((n, n), dtype=np.float64)
+        self.ctx.sgv_get_ld_block(ld, b_global - self.b0, hb.dptr(out), n)
+        return out
+
+    def set_ridge(self, s):
+        self.ctx.sgv_set_ridge(float(s))
+
+    def set_cohort_n(self, k, N):
+        self.ctx.sgv_set_cohort_n(k, float(N))
+
+    def set_vector(self, which, k, full_or_local):
+        v = np.asarray(full_or_local, dtype=np.float64).ravel()
+        if v.shape[0] == self.M and self.M != self.Mloc:
+            v = v[self.sl]
+        v = np.ascontiguousarray(v)
+        if v.shape[0] != self.Mloc:
+            raise ValueError("vector length %d != local M %d" % (v.shape[0], self.Mloc))
+        self.ctx.sgv_set_vector(which, k, hb.dptr(v))
+
+    def get_vector(self, which, k=0):
+        out = np.empty(self.Mloc, dtype=np.float64)
+        self.ctx.sgv_get_vector(which, k, hb.dptr(out))
+        return out
+
+    # ---- synthetic inputs (device generator) -------------------------------
+    def synth_ld_g(self, ld, geno_seed, nsamp, beta_full):
+        beta = np.ascontiguousarray(np.asarray(beta_full, dtype=np.float64)[self.sl])
+        g = np.empty((len(self.local_sizes), nsamp), dtype=np.float64)
+        self.ctx.sgv_synth_ld_g(int(ld), int(geno_seed), self.marker0, int(nsamp), hb.dptr(beta),
+                                hb.dptr(g))
+        return g
+
+    def synth_r(self, k, geno_seed, nsamp, y):
+        y = np.ascontiguousarray(y, dtype=np.float64)
+        self.ctx.sgv_synth_r(int(k), int(geno_seed), self.marker0, int(nsamp), hb.dptr(y))
+
+    # ---- hot path ------------------------------------------------------------
+    def denoise(self, gam1s, a, lam, omegas, sigmas, rho, damp):
+        out = np.zeros(self.K)
+        om = hb.f64(omegas)
+        sg = hb.f64(sigmas)
+        self.ctx.sgv_denoise(hb.dptr(hb.f64(gam1s)), hb.dptr(hb.f64(a)), float(lam), len(sg),
+                             hb.dptr(om), hb.dptr(sg), float(rho), int(bool(damp)), hb.dptr(out))
+        return out
+
+    def em(self, gam1s, a, sigmas, maxit, lam, omegas):
+        lam_io = np.array([lam], dtype=np.float64)
+        om = hb.f64(np.array(omegas, dtype=np.float64).copy())
+        sg = hb.f64(sigmas)
+        steps = np.zeros(1, dtype=np.int32)
+        err = np.zeros(1)
+        self.ctx.sgv_em(hb.dptr(hb.f64(gam1s)), hb.dptr(hb.f64(a)), len(sg), hb.dptr(sg),
+                        int(maxit), hb.dptr(lam_io), hb.dptr(om), hb.iptr(steps), hb.dptr(err))
+        return float(lam_io[0]), om, int(steps[0]), float(err[0])
+
+    def lmmse(self, it, gamw, gam2, alpha1, alpha2_prev, probes_local, cg_maxit, lmmse_damp, rho,
+              learn_gamw, rtol=1e-5):
+        K = self.K
+        out = np.zeros((K, hb.LMMSE_NOUT))
+        cg = np.zeros((K, 4), dtype=np.int32)
+        passes = np.zeros(1, dtype=np.int32)
+        pr = np.ascontiguousarray(probes_local, dtype=np.int8)
+        if pr.shape != (K, self.Mloc):
+            raise ValueError("probes must be (K, Mloc) int8")
+        self.ctx.sgv_lmmse(int(it), hb.dptr(hb.f64(gamw)), hb.dptr(hb.f64(gam2)),
+                           hb.dptr(hb.f64(alpha1)), hb.dptr(hb.f64(alpha2_prev)),
+                           pr.ctypes.data_as(hb._c_i8_p), int(cg_maxit), float(rtol),
+                           int(bool(lmmse_damp)), float(rho), int(bool(learn_gamw)), hb.dptr(out),
+                           hb.iptr(cg), hb.iptr(passes))
+        return out, cg, int(passes[0])
+
+    def metrics(self):
+        out = np.zeros(4)
+        self.ctx.sgv_metrics(hb.dptr(out))
+        return out
+
+    # ---- operator seam (tests) ------------------------------------------------
+    def ld_matvec(self, ld, V_local):
+        V = np.ascontiguousarray(np.atleast_2d(V_local), dtype=np.float64)
+        Y = np.empty_like(V)
+        self.ctx.sgv_ld_matvec(int(ld), V.shape[0], hb.dptr(V), hb.dptr(Y))
+        return Y
+
+    def cg_solve(self, ld, c1, c2, B_local, X0_local, maxiter, rtol=1e-5):
+        B = np.ascontiguousarray(np.atleast_2d(B_local), dtype=np.float64)
+        X = np.ascontiguousarray(np.atleast_2d(X0_local), dtype=np.float64).copy()
+        n = B.shape[0]
+        it = np.zeros(n, dtype=np.int32)
+        info = np.zeros(n, dtype=np.int32)
+        self.ctx.sgv_cg_solve(int(ld), n, hb.dptr(hb.f64(c1)), hb.dptr(hb.f64(c2)), hb.dptr(B),
+                              hb.dptr(X), int(maxiter), float(rtol), hb.iptr(it), hb.iptr(info))
+        return X, it, info
+
+    def timers(self, reset=False):
+        t = np.zeros(4)
+        self.ctx.sgv_timers(hb.dptr(t), int(bool(reset)))
+        return dict(ld_ms=t[0], ld_launches=int(t[1]), ld_bytes_per_pass=t[2], rhs_bytes=t[3])
+
+    def sync(self):
+        self.ctx.sgv_sync()
+
+    def close(self):
+        self.ctx.close()

@@ -1,0 +1,151 @@
+"""ctypes binding of libsgvamp_hip.so (C ABI declared in include/sgvamp_hip.h).
+
+There is no CPU fallback: if the library or a HIP device is missing, every entry
+point raises.  Build the library with ``make -C sgvamp-py_amd/csrc`` (or
+``python -c "import __graft_entry__ as g; g.build()"``).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsgvamp_hip.so")
+
+SGV_OK = 0
+VEC_R, VEC_R1, VEC_XHAT1, VEC_XHAT2, VEC_SIG2U, VEC_X0 = range(6)
+LMMSE_NOUT = 8
+O_TRSIGMA2, O_ALPHA2, O_GAM1, O_Z, O_TRRSIGMA2, O_GAMW, O_XR, O_XRX = range(8)
+MAX_COHORTS = 8
+MAX_SLABS = 8
+
+_c_int_p = ctypes.POINTER(ctypes.c_int)
+_c_i64_p = ctypes.POINTER(ctypes.c_int64)
+_c_dbl_p = ctypes.POINTER(ctypes.c_double)
+_c_i8_p = ctypes.POINTER(ctypes.c_int8)
+_vp = ctypes.c_void_p
+
+# name -> argtypes (restype int unless listed in _RESTYPES)
+_SIGS = {
+    "sgv_create": [ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_int_p, ctypes.c_int, _c_i64_p,
+                   ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(_vp)],
+    "sgv_destroy": [_vp],
+    "sgv_last_error": [_vp],
+    "sgv_comm_unique_id": [ctypes.c_char_p],
+    "sgv_comm_init": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _c_int_p],
+    "sgv_set_ld_block": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, ctypes.c_int64],
+    "sgv_get_ld_block": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, ctypes.c_int64],
+    "sgv_set_ridge": [_vp, ctypes.c_double],
+    "sgv_set_cohort_n": [_vp, ctypes.c_int, ctypes.c_double],
+    "sgv_set_vector": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p],
+    "sgv_get_vector": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p],
+    "sgv_synth_ld_g": [_vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, _c_dbl_p,
+                       _c_dbl_p],
+    "sgv_synth_r": [_vp, ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, _c_dbl_p],
+    "sgv_denoise": [_vp, _c_dbl_p, _c_dbl_p, ctypes.c_double, ctypes.c_int, _c_dbl_p, _c_dbl_p,
+                    ctypes.c_double, ctypes.c_int, _c_dbl_p],
+    "sgv_em": [_vp, _c_dbl_p, _c_dbl_p, ctypes.c_int, _c_dbl_p, ctypes.c_int, _c_dbl_p, _c_dbl_p,
+               _c_int_p, _c_dbl_p],
+    "sgv_lmmse": [_vp, ctypes.c_int, _c_dbl_p, _c_dbl_p, _c_dbl_p, _c_dbl_p, _c_i8_p, ctypes.c_int,
+                  ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_int, _c_dbl_p, _c_int_p,
+                  _c_int_p],
+    "sgv_metrics": [_vp, _c_dbl_p],
+    "sgv_ld_matvec": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, _c_dbl_p],
+    "sgv_cg_solve": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, _c_dbl_p, _c_dbl_p, _c_dbl_p,
+                     ctypes.c_int, ctypes.c_double, _c_int_p, _c_int_p],
+    "sgv_timers": [_vp, _c_dbl_p, ctypes.c_int],
+    "sgv_sync": [_vp],
+}
+_RESTYPES = {"sgv_destroy": None, "sgv_last_error": ctypes.c_char_p}
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load and type the library (cached).  Raises if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise HipError("libsgvamp_hip.so not found at %s -- build it with "
+                       "`make -C sgvamp-py_amd/csrc` (there is no CPU fallback)" % path)
+    lib = ctypes.CDLL(path)
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    _lib = lib
+    return lib
+
+
+def dptr(a):
+    return a.ctypes.data_as(_c_dbl_p)
+
+
+def iptr(a):
+    return a.ctypes.data_as(_c_int_p)
+
+
+def f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+class Context:
+    """Owns one sgv_ctx (one GPU, one rank)."""
+
+    def __init__(self, device, K, ld_of, block_sizes_local, blk0, nblk_global, M_total):
+        self.lib = load()
+        ld_of = np.ascontiguousarray(ld_of, dtype=np.int32)
+        sizes = np.ascontiguousarray(block_sizes_local, dtype=np.int64)
+        nld = int(ld_of.max()) + 1
+        h = _vp()
+        rc = self.lib.sgv_create(int(device), int(K), nld, iptr(ld_of), len(sizes),
+                                 sizes.ctypes.data_as(_c_i64_p), int(blk0), int(nblk_global),
+                                 int(M_total), ctypes.byref(h))
+        if rc != SGV_OK:
+            raise HipError("sgv_create failed (%d): %s" % (
+                rc, self.lib.sgv_last_error(None).decode(errors="replace")))
+        self.h = h
+        self.K, self.nld = K, nld
+        self.Mloc = int(sizes.sum())
+
+    def check(self, rc, what):
+        if rc != SGV_OK:
+            msg = self.lib.sgv_last_error(self.h).decode(errors="replace")
+            raise HipError("%s failed (%d): %s" % (what, rc, msg))
+
+    def close(self):
+        if self.h:
+            self.lib.sgv_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __getattr__(self, name):
+        """ctx.sgv_xxx(args...) -> checked call with the handle prepended."""
+        if not name.startswith("sgv_"):
+            raise AttributeError(name)
+        fn = getattr(self.lib, name)
+
+        def call(*args):
+            self.check(fn(self.h, *args), name)
+
+        return call
+
+
+def unique_id():
+    lib = load()
+    buf = ctypes.create_string_buffer(128)
+    rc = lib.sgv_comm_unique_id(buf)
+    if rc != SGV_OK:
+        raise HipError("sgv_comm_unique_id failed: %s" % lib.sgv_last_error(None).decode())
+    return buf.raw

@@ -1,0 +1,381 @@
+"""sgVAMP for summary statistics on MI355X -- drop-in for the reference's
+``src/sgvamp.py`` class seam (``VAMP(...)``, ``VAMP.infer(...)``).
+
+Same constructor and ``infer`` arguments, same log lines, same output files
+(names, headers, delimiters, value formatting).  Differences by design:
+
+* one process drives all K cohorts of its marker range (the reference runs one
+  MPI rank per cohort and all-gathers K x M vectors every iteration,
+  src/sgvamp.py:228-233); ``comm`` is the communicator of GPU ranks that each
+  own a contiguous range of LD blocks.  Hence ``N`` is the list of per-cohort
+  sample sizes (a scalar is accepted for K = 1), and ``R``/``r`` hold every
+  cohort (``R``: one ``BlockLD`` shared by all cohorts, or a list of K);
+* the LD matrix is block-diagonal and handed over as dense diagonal blocks
+  (``BlockLD``); ``R_s = (1 - s) R + s I`` is applied inside the LD pass;
+* the Hutchinson probes come from ``RandomState(seed + k)`` per cohort, the
+  stream the reference draws after ``np.random.seed(seed + rank)``
+  (src/sgvamp.py:326; the reference itself never seeds);
+* all vector arithmetic runs in libsgvamp_hip.so; there is no CPU fallback.
+"""
+import csv
+import logging
+import os
+import time
+
+import numpy as np
+
+import hip_backend as hb
+from engine import Engine
+from partition import detect_blocks_csr, detect_blocks_dense
+
+
+class BlockLD:
+    """Block-diagonal LD matrix: dense f64 diagonal blocks in marker order.
+
+    ``s`` is the ridge of src/main.py:265 (R_s = (1-s) R + s I); it is applied
+    on the device, the blocks stay unregularised."""
+
+    def __init__(self, blocks=None, block_sizes=None, loader=None, s=0.0):
+        if blocks is not None:
+            self._blocks = [np.asarray(b, dtype=np.float64) for b in blocks]
+            self.block_sizes = [b.shape[0] for b in self._blocks]
+            self._loader = None
+        else:
+            if block_sizes is None or loader is None:
+                raise ValueError("BlockLD needs blocks, or block_sizes and a loader")
+            self._blocks = None
+            self.block_sizes = [int(b) for b in block_sizes]
+            self._loader = loader
+        self.s = float(s)
+
+    @property
+    def M(self):
+        return int(sum(self.block_sizes))
+
+    def block(self, b):
+        if self._blocks is not None:
+            return self._blocks[b]
+        return np.asarray(self._loader(b), dtype=np.float64)
+
+    @classmethod
+    def from_dense(cls, R, block_sizes=None, s=0.0):
+        """A dense M x M LD matrix (the reference's .npy path, src/main.py:201-202);
+        block structure detected from its zero pattern unless given."""
+        R = np.asarray(R, dtype=np.float64)
+        sizes = block_sizes or detect_blocks_dense(R)
+        offs = np.concatenate([[0], np.cumsum(sizes)])
+        return cls(block_sizes=sizes, loader=lambda b: R[offs[b]:offs[b + 1], offs[b]:offs[b + 1]],
+                   s=s)
+
+    @classmethod
+    def from_csr(cls, A, block_sizes=None, s=0.0):
+        """A scipy CSR LD matrix (the reference's .npz path, src/main.py:199-200)."""
+        A = A.tocsr()
+        M = A.shape[0]
+        sizes = block_sizes or detect_blocks_csr(A.indptr, A.indices, M)
+        offs = np.concatenate([[0], np.cumsum(sizes)])
+        return cls(block_sizes=sizes,
+                   loader=lambda b: A[offs[b]:offs[b + 1], offs[b]:offs[b + 1]].toarray(), s=s)
+
+    def regroup(self, sizes):
+        """The same matrix on a coarser partition (every boundary of ``sizes`` must
+        be a boundary of this matrix)."""
+        if list(sizes) == list(self.block_sizes):
+            return self
+        mine = np.concatenate([[0], np.cumsum(self.block_sizes)])
+        theirs = np.concatenate([[0], np.cumsum(sizes)])
+        if not set(theirs.tolist()) <= set(mine.tolist()):
+            raise ValueError("partition is not a coarsening of the LD block structure")
+
+        def load(b):
+            s0, s1 = theirs[b], theirs[b + 1]
+            out = np.zeros((s1 - s0, s1 - s0))
+            for j in range(len(self.block_sizes)):
+                if mine[j] >= s0 and mine[j + 1] <= s1:
+                    o = mine[j] - s0
+                    n = self.block_sizes[j]
+                    out[o:o + n, o:o + n] = self.block(j)
+            return out
+
+        return BlockLD(block_sizes=sizes, loader=load, s=self.s)
+
+
+def common_partition(size_lists):
+    """Coarsest partition on which every LD matrix is block-diagonal: the
+    boundaries shared by all of them."""
+    sets = [set(np.concatenate([[0], np.cumsum(s)]).tolist()) for s in size_lists]
+    common = sorted(set.intersection(*sets))
+    return [int(b - a) for a, b in zip(common[:-1], common[1:])]
+
+
+class VAMP:
+    def __init__(self, N, Nt, M, K, rho, gamw, gam1, a, prior_vars, prior_probs, out_dir,
+                 out_name, comm=None, seed=None, device=None, write_files=True):
+        # src/sgvamp.py:15-31
+        self.eps = 1e-32
+        self.K = int(K)
+        if np.ndim(N) == 0:
+            if self.K != 1:
+                raise ValueError("N must list the sample size of every cohort when K > 1")
+            N = [N]
+        self.N_list = [float(n) for n in N]
+        if len(self.N_list) != self.K:
+            raise ValueError("len(N) != K")
+        self.N = self.N_list[0]
+        self.Nt = Nt
+        self.M = M
+        self.L = len(prior_probs)
+        if self.L - 1 > hb.MAX_SLABS:
+            raise ValueError("at most %d slab components" % hb.MAX_SLABS)
+        self.rho = rho
+        self.gamw = gamw
+        self.gam1 = gam1
+        self.a = np.asarray(a, dtype=np.float64)
+        self.lam = 1 - prior_probs[0]
+        self.sigmas = np.array(prior_vars[1:]) * Nt
+        self.omegas = np.array([p / sum(prior_probs[1:]) for p in prior_probs[1:]])
+        from comm import SingleComm
+
+        self.comm = comm or SingleComm()
+        self.rank = self.comm.Get_rank()
+        self.seed = seed
+        self.device = device
+        self.write_files = write_files
+        self.gam = None
+        self.engine = None
+        self.history = []
+        self.setup_io(out_dir, out_name)
+
+    # ---- output files (src/sgvamp.py:33-76) -----------------------------------
+    def setup_io(self, out_dir, out_name):
+        self.out_dir = out_dir
+        self.out_name = out_name
+        if not self.write_files or self.rank != 0:
+            return
+        for i in range(self.K):
+            with open(os.path.join(self.out_dir, "%s_cohort_%d.csv" % (self.out_name, i + 1)), "w",
+                      newline="") as f:
+                csv.writer(f, delimiter="\t").writerow(
+                    ["it", "gamw", "gam1", "gam2", "alpha1", "alpha2", "lam"])
+        with open(os.path.join(self.out_dir, "%s_metrics.csv" % self.out_name), "w", newline="") as f:
+            csv.writer(f, delimiter="\t").writerow(["it", "alignment", "l2"])
+
+    def write_params_to_file(self, params, cohort_idx):
+        with open(os.path.join(self.out_dir, "%s_cohort_%d.csv" % (self.out_name, cohort_idx + 1)),
+                  "a", newline="") as f:
+            csv.writer(f, delimiter="\t").writerow(params)
+
+    def write_metrics_to_file(self, metrics):
+        with open(os.path.join(self.out_dir, "%s_metrics.csv" % self.out_name), "a", newline="") as f:
+            csv.writer(f, delimiter="\t").writerow(metrics)
+
+    def _write_slice(self, fname, local):
+        """Native-endian f64, M values, no header.  Each rank writes its marker
+        slice at its byte offset, so no gather is needed."""
+        path = os.path.join(self.out_dir, fname)
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
+        try:
+            if self.rank == 0:
+                os.ftruncate(fd, self.M * 8)
+            os.pwrite(fd, np.ascontiguousarray(local, dtype=np.float64).tobytes(),
+                      self.engine.marker0 * 8)
+        finally:
+            os.close(fd)
+
+    def write_xhat_to_file(self, it, xhat_local):
+        self._write_slice("%s_xhat_it_%d.bin" % (self.out_name, it), xhat_local)
+
+    def write_r1_to_file(self, it, r1_local, k):
+        self._write_slice("%s_r1_cohort_%d_it_%d.bin" % (self.out_name, k, it), r1_local)
+
+    # ---- set-up ----------------------------------------------------------------
+    def _setup(self, R, r, x0):
+        K = self.K
+        lds = list(R) if isinstance(R, (list, tuple)) else [R] * K
+        if len(lds) != K:
+            raise ValueError("R must be one BlockLD or a list of K")
+        uniq, ld_of = [], []
+        for L in lds:
+            for j, U in enumerate(uniq):
+                if U is L:
+                    ld_of.append(j)
+                    break
+            else:
+                uniq.append(L)
+                ld_of.append(len(uniq) - 1)
+        s_vals = {L.s for L in uniq}
+        if len(s_vals) != 1:
+            raise ValueError("all LD matrices must use the same ridge s")
+        sizes = common_partition([L.block_sizes for L in uniq])
+        if sum(sizes) != self.M:
+            raise ValueError("LD matrices cover %d markers, M = %d" % (sum(sizes), self.M))
+        uniq = [L.regroup(sizes) for L in uniq]
+        self.engine = eng = Engine(sizes, K, ld_of, comm=self.comm, device=self.device)
+        eng.set_ridge(s_vals.pop())
+        for l, L in enumerate(uniq):
+            for b in range(eng.b0, eng.b1):
+                eng.set_ld_block(l, b, L.block(b))
+        rr = np.asarray(r, dtype=np.float64)
+        rr = rr.reshape(K, -1) if rr.size == K * self.M else rr
+        for k in range(K):
+            eng.set_vector(hb.VEC_R, k, rr[k].ravel())
+            eng.set_vector(hb.VEC_R1, k, rr[k].ravel())       # r1 = r (:204)
+            eng.set_cohort_n(k, self.N_list[k])
+        if x0 is not None:
+            eng.set_vector(hb.VEC_X0, 0, np.asarray(x0, dtype=np.float64).ravel())
+
+    def _probe_streams(self):
+        seed = self.seed
+        if seed is None and self.comm.Get_size() > 1:
+            seed = self.comm.bcast(int(np.random.SeedSequence().entropy % (2 ** 31))
+                                   if self.rank == 0 else None, root=0)
+        if seed is None:
+            return [np.random.RandomState() for _ in range(self.K)]
+        return [np.random.RandomState(seed + k) for k in range(self.K)]
+
+    def attach_engine(self, engine, x0=None):
+        """Use an Engine whose LD blocks and r vectors are already on the device
+        (e.g. generated there); sets r1 = r (src/sgvamp.py:204) and N_k."""
+        self.engine = engine
+        for k in range(self.K):
+            engine.set_vector(hb.VEC_R1, k, engine.get_vector(hb.VEC_R, k))
+            engine.set_cohort_n(k, self.N_list[k])
+        if x0 is not None:
+            engine.set_vector(hb.VEC_X0, 0, np.asarray(x0, dtype=np.float64).ravel())
+        self._has_x0 = x0 is not None
+
+    # ---- the outer loop (src/sgvamp.py:196-389) --------------------------------
+    def infer(self, R, r, iterations, x0, cg_maxit=500, em_prior_maxit=100, learn_gamw=True,
+              lmmse_damp=True, prior_update=None, update_prior_from=1, return_xhat=True):
+        self.begin(R, r, x0, cg_maxit=cg_maxit, em_prior_maxit=em_prior_maxit,
+                   learn_gamw=learn_gamw, lmmse_damp=lmmse_damp, prior_update=prior_update,
+                   update_prior_from=update_prior_from, return_xhat=return_xhat)
+        for it in range(iterations):
+            self.step(it)
+        self.gamws = self._st["gamws"]
+        return self._st["xhat1s"]
+
+    def begin(self, R=None, r=None, x0=None, cg_maxit=500, em_prior_maxit=100, learn_gamw=True,
+              lmmse_damp=True, prior_update=None, update_prior_from=1, return_xhat=True):
+        """Initialisation of src/sgvamp.py:198-220 (uploads R, r, x0 unless an
+        engine was attached)."""
+        if self.engine is None:
+            self._setup(R, r, x0)
+            self._has_x0 = x0 is not None
+        K = self.K
+        self._st = dict(gam1=[self.gam1] * K, gamw=[self.gamw] * K, alpha1=[0] * K,
+                        alpha2=[0] * K, gamws=[[] for _ in range(K)], xhat1s=[],
+                        probes=self._probe_streams(), cg_maxit=cg_maxit,
+                        em_prior_maxit=em_prior_maxit, learn_gamw=learn_gamw,
+                        lmmse_damp=lmmse_damp, prior_update=prior_update,
+                        update_prior_from=update_prior_from, return_xhat=return_xhat)
+        if self.rank == 0:
+            logging.debug(f"a = {self.a}")
+
+    def step(self, it):
+        """One outer iteration, src/sgvamp.py:222-387."""
+        st = self._st
+        eng = self.engine
+        K, M, Nt, rho, rank = self.K, self.M, self.Nt, self.rho, self.rank
+        gam1, gamw, alpha1, alpha2 = st["gam1"], st["gamw"], st["alpha1"], st["alpha2"]
+        t_it = time.perf_counter()
+        rec = dict(it=it)
+        if rank == 0:
+            logging.info(f"\n -----ITERATION {it} -----")
+        gam1s = np.array(gam1, dtype=np.float64)                      # :228-233
+        if rank == 0:
+            logging.debug(f"gam1s={gam1s}")
+            logging.info("...Data from all ranks collected")
+
+        if it >= st["update_prior_from"]:                             # :242-259
+            if st["prior_update"] == "mle":
+                if rank == 0:
+                    logging.info("...Updating prior parameters using MLE")
+                self.prior_update_mle(gam1s)
+            elif st["prior_update"] == "em":
+                if rank == 0:
+                    logging.info("...Updating prior parameters using EM")
+                self.lam, self.omegas, steps, err = eng.em(
+                    gam1s, self.a, self.sigmas, st["em_prior_maxit"], self.lam, self.omegas)
+                rec["em_steps"] = steps
+                if rank == 0:
+                    logging.info(f"... prior-learning EM algorithm performed {steps} steps "
+                                 f"and had final relative error = {err:0.9f}")
+        if rank == 0:
+            logging.debug(f"lam={self.lam}")
+            logging.debug(f"omegas={self.omegas}")
+            logging.debug(f"sigmas={self.sigmas}")
+            logging.info("...Denoising")
+
+        alpha1_prev = list(alpha1)
+        der_sum = eng.denoise(gam1s, self.a, self.lam, self.omegas, self.sigmas, rho,
+                              damp=it > 0)                            # :273-276, 285
+        if self.write_files or st["return_xhat"]:
+            xhat_loc = eng.get_vector(hb.VEC_XHAT1)
+            if self.write_files:
+                self.write_xhat_to_file(it, xhat_loc / np.sqrt(Nt))   # :281
+                for k in range(K):
+                    self.write_r1_to_file(it, eng.get_vector(hb.VEC_R1, k) / np.sqrt(Nt),
+                                          k + 1)                     # :283
+            if st["return_xhat"]:
+                full = xhat_loc
+                if self.comm.Get_size() > 1:
+                    full = np.concatenate(self.comm.allgather(xhat_loc))
+                st["xhat1s"].append(full.reshape((M, 1)))
+        gam2 = [0.0] * K
+        for k in range(K):
+            a1 = der_sum[k] / M                                       # np.mean (:285)
+            if it > 0:
+                a1 = rho * a1 + (1 - rho) * alpha1_prev[k]            # :290-291
+            alpha1[k] = a1
+            gam2[k] = gam1[k] * (1 - a1) / a1                         # :305
+        if rank == 0:
+            logging.debug(f"[rank = {rank}] alpha1 = {alpha1[0]}")
+            logging.debug(f"[rank = {rank}] gam2 = {gam2[0]}")
+        for k in range(K):
+            logging.info(f"...LMMSE cohort {k}")
+        u = np.empty((K, eng.Mloc), dtype=np.int8)
+        for k in range(K):
+            u[k] = (st["probes"][k].binomial(p=1 / 2, n=1, size=M) * 2 - 1)[eng.sl]   # :326
+        out, cg, passes = eng.lmmse(it, gamw, gam2, alpha1, alpha2, u, st["cg_maxit"],
+                                    st["lmmse_damp"], rho, st["learn_gamw"])
+        rec.update(cg_iters=cg[:, [0, 2]].tolist(), cg_info=cg[:, [1, 3]].tolist(),
+                   ld_passes=passes)
+        for k in range(K):
+            if cg[k, 1] > 0:
+                logging.info(f"Rank {k} WARNING: CG 1 convergence after {cg[k, 1]} "
+                             f"iterations not achieved!")
+            if cg[k, 3] > 0:
+                logging.info(f"Rank {k} WARNING: CG 2 convergence after {cg[k, 3]} "
+                             f"iterations not achieved!")
+            alpha2[k] = out[k, hb.O_ALPHA2]
+            gam1[k] = out[k, hb.O_GAM1]
+            if st["learn_gamw"]:
+                gamw[k] = float(out[k, hb.O_GAMW])                    # :363-364
+        if rank == 0:
+            logging.debug(f"[rank = {rank}] alpha2 = {alpha2[0]}")
+            logging.debug(f"gamw = {gamw[0]:0.9f} \n")
+        for k in range(K):
+            st["gamws"][k].append(gamw[k])                            # :373
+            gamw[k] = max(gamw[k], 1.0)                               # :374
+            if rank == 0 and self.write_files:
+                self.write_params_to_file([it, gamw[k], gam1[k], gam2[k], alpha1[k],
+                                           alpha2[k], self.lam], k)  # :377
+        if self._has_x0:                                              # :379-387
+            s = eng.metrics()
+            alignment = s[0] / np.sqrt(s[1]) / np.sqrt(s[3])
+            l2 = np.sqrt(s[2]) / np.sqrt(s[3])
+            rec["metrics"] = (alignment, l2)
+            if rank == 0:
+                logging.debug(f"Alignment(xhat1, x0) = {alignment:0.9f} \n")
+                logging.debug(f"L2_error(xhat1, x0) = {l2:0.9f} \n")
+                if self.write_files:
+                    self.write_metrics_to_file([it, alignment, l2])
+        rec.update(gamw=list(gamw), gam1=list(gam1), gam2=gam2, alpha1=list(alpha1),
+                   alpha2=list(alpha2), lam=self.lam, wall_s=time.perf_counter() - t_it)
+        self.history.append(rec)
+        return rec
+
+    def prior_update_mle(self, gam1s):
+        raise NotImplementedError("--prior-update mle (src/sgvamp.py:139-194) is not implemented "
+                                  "yet; use em")

@@ -1,0 +1,103 @@
+"""N > 1 path on CPU: world_size-2 gloo.
+
+* the product's host communicator (comm.TorchGlooComm: RCCL-id bootstrap,
+  barrier, allgather) and block partition agree across ranks;
+* the sharded decomposition the GPU path uses -- each rank owns a contiguous
+  range of LD blocks for all cohorts, every M-length sum is a per-block partial
+  exchanged by all-gather and added in global block order -- reproduces the
+  single-rank run BIT FOR BIT (checked with the oracle's restatement, the
+  same algorithm the HIP kernels implement).
+"""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import vamp_oracle as vo
+from tests.golden import Case
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+class _GlooBlocks:
+    def __init__(self, comm):
+        self.comm = comm
+
+    def allgather_blocks(self, part):
+        return np.concatenate(self.comm.allgather(np.asarray(part)))
+
+
+def _rank(rank, world, port, case_name, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world))
+        from comm import TorchGlooComm
+        from partition import marker_offsets, partition_blocks
+
+        comm = TorchGlooComm()
+        uid = comm.bcast(b"\x01" * 128 if rank == 0 else None, root=0)
+        assert uid == b"\x01" * 128
+        c = Case(case_name)
+        ranges = partition_blocks(c.block_sizes, world)
+        assert comm.allgather(ranges) == [ranges] * world
+        b0, b1 = ranges[rank]
+        offs = marker_offsets(c.block_sizes)
+        sl = slice(offs[b0], offs[b1])
+        lds = [vo.BlockLD(blocks[b0:b1], s=c.flags["s"]) for blocks in c.ld_blocks]
+        red = vo.Reducer("blocked", bounds=lds[0].bounds, comm=_GlooBlocks(comm))
+        streams = vo.ProbeStream(c.flags["seed"], c.K)
+        probe = lambda k, it: streams.draw(k, c.M)[sl]     # same stream on every rank
+        with np.errstate(all="ignore"):
+            t = vo.infer(lds, c.ld_of, [v[sl] for v in c.r], c.N, c.flags["iterations"],
+                         x0=c.x0[sl], reducer=red, M_total=c.M, probe=probe, **c.kwargs())
+        comm.barrier()
+        q.put((rank, np.array(t["xhat"]), np.array(t["csv"]), np.array(t["cg_iters"]),
+               list(t["em_steps"]), np.array(t["metrics"])))
+    except Exception as e:  # surface the failure in the parent
+        import traceback
+
+        q.put((rank, "ERROR", traceback.format_exc(), None, None, None))
+
+
+def _single(case_name):
+    c = Case(case_name)
+    lds = [vo.BlockLD(b, s=c.flags["s"]) for b in c.ld_blocks]
+    red = vo.Reducer("blocked", bounds=lds[0].bounds)
+    with np.errstate(all="ignore"):
+        return vo.infer(lds, c.ld_of, list(c.r), c.N, c.flags["iterations"], x0=c.x0,
+                        reducer=red, **c.kwargs())
+
+
+@pytest.mark.parametrize("case_name", ["k2_shared", "k1_blocks_csr_s_damp", "k4_shared_s_damp"])
+def test_two_rank_sharded_run_is_bit_identical(case_name):
+    world = 2
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank, args=(r, world, port, case_name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        item = q.get(timeout=300)
+        assert not isinstance(item[1], str), item[2]
+        res[item[0]] = item
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = _single(case_name)
+    xh = np.concatenate([res[r][1] for r in range(world)], axis=1)
+    np.testing.assert_array_equal(xh, np.array(ref["xhat"]))
+    for r in range(world):
+        np.testing.assert_array_equal(res[r][2], np.array(ref["csv"]))
+        np.testing.assert_array_equal(res[r][3], np.array(ref["cg_iters"]))
+        assert res[r][4] == list(ref["em_steps"])
+        np.testing.assert_array_equal(res[r][5], np.array(ref["metrics"]))

@@ -1,0 +1,297 @@
+"""Parity of the HIP path (through the C ABI) with the oracle and with the
+reference's golden outputs.  Run on an MI355X: python -m pytest tests -m gpu.
+
+Tolerances (f64 everywhere; only the summation order differs from the oracle):
+* LD pass, CG solution, denoiser, EM, generator: <= 1e-11 relative;
+* full VAMP trajectories vs the reference fixtures: xhat/r1 <= 1e-8 relative to
+  max|.| per iteration (the north-star bar is 1e-5), CG iteration counts and EM
+  steps exact, cohort CSV values rtol 1e-5 (gam2 = gam1(1-a1)/a1 amplifies
+  rounding when alpha1 -> 0; the oracle itself sits at 6e-7 there).
+"""
+import csv
+import os
+
+import numpy as np
+import pytest
+
+import hip_backend as hb
+from engine import Engine
+from oracle import synth_oracle as so
+from oracle import vamp_oracle as vo
+from sgvamp import VAMP, BlockLD
+from tests.golden import Case, case_names
+
+pytestmark = pytest.mark.gpu
+
+
+def maxrel(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), 1e-300))
+
+
+def rand_blocks(sizes, seed=0, nsamp=None):
+    rs = np.random.RandomState(seed)
+    out = []
+    for n in sizes:
+        X = rs.normal(size=(nsamp or max(2 * n, 8), n))
+        X /= np.sqrt(X.shape[0])
+        out.append(X.T @ X)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# the LD pass (operator seam)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("sizes", [[1], [7, 1, 130], [127, 128, 129], [300, 64, 1000, 33]])
+@pytest.mark.parametrize("ncol", [1, 2, 5, 8, 16])
+@pytest.mark.parametrize("s", [0.0, 0.1])
+def test_ld_matvec_vs_numpy(sizes, ncol, s):
+    blocks = rand_blocks(sizes, seed=len(sizes) + ncol)
+    eng = Engine(sizes, K=1)
+    for b, B in enumerate(blocks):
+        eng.set_ld_block(0, b, B)
+    eng.set_ridge(s)
+    M = sum(sizes)
+    V = np.random.RandomState(ncol).normal(size=(ncol, M))
+    Y = eng.ld_matvec(0, V)
+    L = vo.BlockLD(blocks, s=s)
+    for j in range(ncol):
+        ref = L.matvec_Rs(V[j])
+        assert maxrel(Y[j], ref) < 1e-12, (j, maxrel(Y[j], ref))
+    eng.close()
+
+
+def test_ld_block_roundtrip():
+    sizes = [33, 200]
+    blocks = rand_blocks(sizes, 3)
+    eng = Engine(sizes, K=1)
+    for b, B in enumerate(blocks):
+        eng.set_ld_block(0, b, B)
+    for b, B in enumerate(blocks):
+        np.testing.assert_array_equal(eng.get_ld_block(0, b), B)
+    eng.close()
+
+
+def test_ld_matvec_symmetry_and_linearity_large():
+    """Size-independent properties at BASELINE block size (25k x 25k, 5 GB):
+    u^T(Rv) = v^T(Ru) for symmetric R, linearity R(au+bv) = aRu + bRv."""
+    sizes = [25000]
+    eng = Engine(sizes, K=1)
+    beta = np.zeros(25000)
+    eng.synth_ld_g(0, 5, 2000, beta)        # R = G G^T, exactly symmetric by construction
+    rs = np.random.RandomState(1)
+    U = rs.normal(size=(3, 25000))
+    U[2] = 0.3 * U[0] - 1.7 * U[1]
+    Y = eng.ld_matvec(0, U)
+    assert abs(U[0] @ Y[1] - U[1] @ Y[0]) <= 1e-11 * abs(U[0] @ Y[1])
+    assert maxrel(Y[2], 0.3 * Y[0] - 1.7 * Y[1]) < 1e-11
+    eng.close()
+
+
+# ---------------------------------------------------------------------------
+# CG (operator seam con_grad)
+# ---------------------------------------------------------------------------
+def test_cg_solve_vs_oracle():
+    sizes = [150, 90, 260]
+    blocks = rand_blocks(sizes, 11, nsamp=100)   # rank-deficient blocks, like simulated LD
+    M = sum(sizes)
+    eng = Engine(sizes, K=1)
+    for b, B in enumerate(blocks):
+        eng.set_ld_block(0, b, B)
+    eng.set_ridge(0.05)
+    L = vo.BlockLD(blocks, s=0.05)
+    rs = np.random.RandomState(2)
+    c1 = np.array([4.0, 2.0, 1.0, 6.0])
+    c2 = np.array([0.3, 0.05, 1.0, 0.0])
+    Bm = rs.normal(size=(4, M))
+    X0 = np.zeros((4, M))
+    X0[1] = rs.normal(size=M) * 0.1
+    X0[3] = rs.normal(size=M) * 0.01
+    X, it, info = eng.cg_solve(0, c1, c2, Bm, X0, maxiter=500)
+    for j in range(4):
+        A = lambda p, j=j: c1[j] * L.matvec_Rs(p) + c2[j] * p
+        xr, info_r, it_r, _ = vo.cg_scipy(A, Bm[j], X0[j], 500, vo.Reducer())
+        assert (it[j], info[j]) == (it_r, info_r), j
+        assert maxrel(X[j], xr) < 1e-9, j
+        res = np.linalg.norm(Bm[j] - A(X[j])) / np.linalg.norm(Bm[j])
+        assert res < 1e-5
+    # maxiter exhaustion and a zero right-hand side
+    X, it, info = eng.cg_solve(0, c1[:2], c2[:2], np.stack([Bm[0], np.zeros(M)]),
+                               np.stack([np.zeros(M), np.ones(M)]), maxiter=2)
+    assert (it[0], info[0]) == (2, 2)
+    assert (it[1], info[1]) == (0, 0) and not X[1].any()
+    eng.close()
+
+
+# ---------------------------------------------------------------------------
+# element-wise kernels
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("K,nslab", [(1, 1), (3, 3), (8, 8)])
+def test_denoise_and_em_vs_oracle(K, nslab):
+    sizes = [4000, 3000, 5000]
+    M = sum(sizes)
+    rs = np.random.RandomState(K * 10 + nslab)
+    r1s = rs.normal(scale=3.0, size=(K, M)) * (rs.uniform(size=(K, M)) < 0.3)
+    gam1s = rs.uniform(0.5, 3.0, size=K)
+    a = rs.uniform(1, 2, size=K)
+    a /= a.sum()
+    sigmas = np.sort(rs.uniform(1, 50, size=nslab))
+    omegas = rs.uniform(0.5, 1, size=nslab)
+    omegas /= omegas.sum()
+    lam = 0.12
+    eng = Engine(sizes, K=K)
+    for k in range(K):
+        eng.set_vector(hb.VEC_R1, k, r1s[k])
+    der = eng.denoise(gam1s, a, lam, omegas, sigmas, rho=0.5, damp=False)
+    x = eng.get_vector(hb.VEC_XHAT1)
+    assert maxrel(x, vo.denoiser_meta(r1s, gam1s, a, lam, omegas, sigmas)) < 1e-12
+    ref_der = vo.der_denoiser_meta(r1s, gam1s, a, lam, omegas, sigmas).sum(axis=1)
+    assert maxrel(der, ref_der) < 1e-11
+    # damping (:275-276)
+    eng.denoise(gam1s * 1.1, a, lam, omegas, sigmas, rho=0.5, damp=True)
+    x2 = eng.get_vector(hb.VEC_XHAT1)
+    ref2 = 0.5 * vo.denoiser_meta(r1s, gam1s * 1.1, a, lam, omegas, sigmas) + 0.5 * x
+    assert maxrel(x2, ref2) < 1e-12
+    # one EM step == oracle prior_update_em
+    lam_g, om_g, steps, _ = eng.em(gam1s, a, sigmas, 1, lam, omegas)
+    lam_r, om_r = vo.prior_update_em(r1s, gam1s, a, lam, omegas, sigmas)
+    assert steps == 1
+    assert abs(lam_g - lam_r) <= 1e-12 * abs(lam_r)
+    assert maxrel(om_g, om_r) < 1e-12
+    eng.close()
+
+
+# ---------------------------------------------------------------------------
+# full VAMP vs the reference's golden outputs
+# ---------------------------------------------------------------------------
+def run_vamp_case(c, out_dir, device=None):
+    f = c.flags
+    lds = [BlockLD(blocks, s=f["s"]) for blocks in c.ld_blocks]
+    R = lds[0] if len(lds) == 1 else [lds[c.ld_of[k]] for k in range(c.K)]
+    Nt = sum(c.N)
+    a = np.array(c.N) / Nt
+    v = VAMP(N=c.N, Nt=Nt, M=c.M, K=c.K, rho=f["rho"], gamw=f["gamw"], gam1=f["gam1"], a=a,
+             prior_vars=f["prior_vars"], prior_probs=f["prior_probs"], out_dir=str(out_dir),
+             out_name=c.name, seed=f["seed"], device=device)
+    xh = v.infer(R, c.r, f["iterations"], x0=c.x0, cg_maxit=f["cg_maxit"],
+                 em_prior_maxit=f["em_prior_maxit"], learn_gamw=f["learn_gamw"],
+                 lmmse_damp=f["lmmse_damp"], prior_update=f["prior_update"],
+                 update_prior_from=f["update_prior_from"])
+    return v, xh
+
+
+def read_tsv(path):
+    with open(path) as fh:
+        text = fh.read()
+    rows = [[float(x) for x in ln.split("\t")] for ln in text.splitlines()[1:]]
+    return text, np.array(rows)
+
+
+@pytest.mark.parametrize("name", case_names())
+def test_vamp_matches_reference_golden(name, tmp_path):
+    c = Case(name)
+    v, xh = run_vamp_case(c, tmp_path)
+    its = c.flags["iterations"]
+    Nt = sum(c.N)
+    for it in range(its):
+        xb = np.fromfile(tmp_path / ("%s_xhat_it_%d.bin" % (name, it)), dtype=np.float64)
+        assert xb.shape == (c.M,)
+        assert maxrel(xb, c.xhat[it]) < 1e-8, (it, maxrel(xb, c.xhat[it]))
+        assert maxrel(xh[it].ravel() / np.sqrt(Nt), c.xhat[it]) < 1e-8
+        for k in range(c.K):
+            rb = np.fromfile(tmp_path / ("%s_r1_cohort_%d_it_%d.bin" % (name, k + 1, it)))
+            assert maxrel(rb, c.r1[k][it]) < 1e-8, (it, k)
+    cg = np.array([h["cg_iters"] for h in v.history]).transpose(1, 0, 2)
+    np.testing.assert_array_equal(cg, c.cg_iters)
+    info = np.array([h["cg_info"] for h in v.history]).transpose(1, 0, 2)
+    np.testing.assert_array_equal(info, c.cg_info)
+    em = [h["em_steps"] for h in v.history if "em_steps" in h]
+    assert em == list(c.em_steps)
+    for k in range(c.K):
+        text, rows = read_tsv(tmp_path / ("%s_cohort_%d.csv" % (name, k + 1)))
+        assert text.splitlines()[0] == c.cohort_csv_text[k].splitlines()[0]
+        np.testing.assert_allclose(rows, c.cohort_csv[k], rtol=1e-5, atol=0)
+        # row 0 is written before any EM update: lam prints exactly as the reference's
+        assert text.splitlines()[1].split("\t")[-1] == c.cohort_csv_text[k].splitlines()[1].split("\t")[-1]
+    text, rows = read_tsv(tmp_path / ("%s_metrics.csv" % name))
+    assert text.splitlines()[0] == c.metrics_csv_text.splitlines()[0]
+    np.testing.assert_allclose(rows, c.metrics_csv, rtol=1e-7, atol=1e-12)
+    v.engine.close()
+
+
+def test_vamp_is_deterministic(tmp_path):
+    c = Case("k2_shared")
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    v1, x1 = run_vamp_case(c, tmp_path / "a")
+    v2, x2 = run_vamp_case(c, tmp_path / "b")
+    for a_, b_ in zip(x1, x2):
+        np.testing.assert_array_equal(a_, b_)
+    for k in range(c.K):
+        f = "%s_cohort_%d.csv" % (c.name, k + 1)
+        assert (tmp_path / "a" / f).read_text() == (tmp_path / "b" / f).read_text()
+    v1.engine.close()
+    v2.engine.close()
+
+
+# ---------------------------------------------------------------------------
+# synthetic generator vs its CPU restatement
+# ---------------------------------------------------------------------------
+def test_synth_generator_vs_oracle():
+    sizes = [50, 130, 257]
+    nsamp = 500
+    M = sum(sizes)
+    rs = np.random.RandomState(9)
+    beta = np.zeros(M)
+    idx = rs.choice(M, 40, replace=False)
+    beta[idx] = rs.normal(0, 0.1, 40)
+    w = rs.normal(0, 0.5, nsamp)
+    Rb, r, g, gb = so.synth_problem(sizes, nsamp, beta, 77, w)
+    eng = Engine(sizes, K=1)
+    g_dev = eng.synth_ld_g(0, 77, nsamp, beta)
+    for b in range(len(sizes)):
+        assert maxrel(g_dev[b], gb[b]) < 1e-12
+        Rd = eng.get_ld_block(0, b)
+        assert maxrel(Rd, Rb[b]) < 1e-12
+        np.testing.assert_array_equal(Rd, Rd.T)                  # mirrored tiles
+        np.testing.assert_allclose(np.diag(Rd), 1.0, rtol=1e-12)  # standardised markers
+    y = g_dev.sum(axis=0) + w
+    eng.synth_r(0, 77, nsamp, y)
+    assert maxrel(eng.get_vector(hb.VEC_R, 0), r) < 1e-12
+    eng.close()
+
+
+# ---------------------------------------------------------------------------
+# medium scale: HIP VAMP vs oracle on device-generated data
+# ---------------------------------------------------------------------------
+def test_vamp_medium_scale_vs_oracle(tmp_path):
+    sizes = [3000, 2500, 3500, 3000]
+    nsamp = 2000
+    M = sum(sizes)
+    rs = np.random.RandomState(5)
+    cm = M // 10
+    beta = np.zeros(M)
+    beta[rs.choice(M, cm, replace=False)] = rs.normal(0, np.sqrt(0.8 / cm), cm)
+    eng = Engine(sizes, K=1)
+    g = eng.synth_ld_g(0, 123, nsamp, beta)
+    y = g.sum(axis=0) + rs.normal(0, np.sqrt(0.2), nsamp)
+    eng.synth_r(0, 123, nsamp, y)
+    blocks = [eng.get_ld_block(0, b) for b in range(len(sizes))]
+    r = eng.get_vector(hb.VEC_R, 0)
+    prior_vars = [0.0, 0.8 / cm]
+    prior_probs = [0.9, 0.1]
+    x0 = beta * np.sqrt(nsamp)
+    v = VAMP(N=nsamp, Nt=nsamp, M=M, K=1, rho=0.5, gamw=5.0, gam1=1e-6, a=[1.0],
+             prior_vars=prior_vars, prior_probs=prior_probs, out_dir=str(tmp_path), out_name="m",
+             seed=3, write_files=False)
+    v.attach_engine(eng, x0=x0)
+    its = 6
+    xh = v.infer(None, None, its, x0=x0, lmmse_damp=False, prior_update="em")
+    L = vo.BlockLD(blocks)
+    t = vo.infer([L], [0], [r], [nsamp], its, rho=0.5, gamw=5.0, gam1=1e-6,
+                 prior_vars=prior_vars, prior_probs=prior_probs, x0=x0, seed=3,
+                 lmmse_damp=False, reducer=vo.Reducer("blocked", bounds=L.bounds))
+    for it in range(its):
+        assert maxrel(xh[it].ravel() / np.sqrt(nsamp), t["xhat"][it]) < 1e-8, it
+    assert [h["cg_iters"][0] for h in v.history] == [list(x[0]) for x in t["cg_iters"]]
+    eng.close()

@@ -1,0 +1,100 @@
+"""Pin the oracle (oracle/vamp_oracle.py) against the reference's own outputs.
+
+The fixtures in tests/golden/ were produced by running the reference
+(/root/reference/src/sgvamp.py) in the build container (make_golden.py).
+"""
+import numpy as np
+import pytest
+
+from oracle import vamp_oracle as vo
+from tests.golden import Case, case_names
+
+CASES = case_names()
+
+
+def run_oracle(c, mode="numpy"):
+    lds = [vo.BlockLD(b, s=c.flags["s"]) for b in c.ld_blocks]
+    red = vo.Reducer(mode, bounds=lds[0].bounds) if mode == "blocked" else None
+    with np.errstate(all="ignore"):
+        return vo.infer(lds, c.ld_of, list(c.r), c.N, c.flags["iterations"], x0=c.x0,
+                        reducer=red, **c.kwargs())
+
+
+def maxrel(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), 1e-300))
+
+
+def test_fixtures_present():
+    assert len(CASES) >= 7
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_matches_reference(name):
+    c = Case(name)
+    t = run_oracle(c)
+    its = c.flags["iterations"]
+    xh = np.array(t["xhat"])
+    assert xh.shape == c.xhat.shape
+    for it in range(its):
+        assert maxrel(xh[it], c.xhat[it]) < 1e-10, it
+        for k in range(c.K):
+            assert maxrel(t["r1"][it][k], c.r1[k][it]) < 1e-10, (it, k)
+    # CG iteration counts and EM steps: exact
+    cg = np.array(t["cg_iters"]).transpose(1, 0, 2)
+    np.testing.assert_array_equal(cg, c.cg_iters)
+    np.testing.assert_array_equal(np.array(t["cg_info"]).transpose(1, 0, 2), c.cg_info)
+    assert list(t["em_steps"]) == list(c.em_steps)
+    # cohort CSV rows [it, gamw, gam1, gam2, alpha1, alpha2, lam]
+    csv = np.array(t["csv"])
+    np.testing.assert_allclose(csv, c.cohort_csv, rtol=1e-6, atol=0)
+    np.testing.assert_allclose(np.array(t["metrics"]), c.metrics_csv, rtol=1e-9, atol=1e-12)
+
+
+def test_lam0_repr():
+    # the reference's lam is a Python float until the first EM update
+    c = Case("k1_dense")
+    assert repr(1 - c.flags["prior_probs"][0]) == c.lam0_repr
+
+
+@pytest.mark.parametrize("name", ["k1_dense", "k2_shared", "k1_blocks_csr_s_damp", "k1_L3"])
+def test_blocked_reduction_order_matches(name):
+    """The GPU's reduction order (per LD block, then blocks in order) keeps the
+    reference's iteration counts and trajectories."""
+    c = Case(name)
+    t = run_oracle(c, "blocked")
+    np.testing.assert_array_equal(np.array(t["cg_iters"]).transpose(1, 0, 2), c.cg_iters)
+    assert list(t["em_steps"]) == list(c.em_steps)
+    xh = np.array(t["xhat"])
+    for it in range(c.flags["iterations"]):
+        assert maxrel(xh[it], c.xhat[it]) < 1e-8
+
+
+def test_cg_restatement_matches_scipy():
+    """oracle.cg_scipy == scipy.sparse.linalg.cg (the reference's con_grad)."""
+    from scipy.sparse.linalg import cg
+
+    rs = np.random.RandomState(3)
+    X = rs.normal(size=(60, 80))
+    A = X.T @ X / 60 + 0.05 * np.eye(80)
+    b = rs.normal(size=80)
+    x0 = rs.normal(size=80) * 0.1
+    for start in (np.zeros(80), x0):
+        n = [0]
+        ref, info = cg(A, b, x0=start.copy(), maxiter=500, callback=lambda xk: n.__setitem__(0, n[0] + 1))
+        mine, info2, it, _ = vo.cg_scipy(lambda p: A @ p, b, start, 500, vo.Reducer())
+        assert info == info2 and n[0] == it
+        np.testing.assert_allclose(mine, ref, rtol=1e-12, atol=1e-14)
+    # maxiter exhaustion returns info = maxiter
+    _, info, it, _ = vo.cg_scipy(lambda p: A @ p, b, np.zeros(80), 3, vo.Reducer())
+    assert info == 3 and it == 3
+
+
+def test_probe_stream_matches_global_rng():
+    s = vo.ProbeStream(41, 2)
+    np.random.seed(42)
+    from numpy.random import binomial
+
+    first = binomial(p=1 / 2, n=1, size=500) * 2 - 1
+    s.draw(0, 500)
+    np.testing.assert_array_equal(s.draw(1, 500), first)

@@ -1,0 +1,78 @@
+"""Host logic: block partitioning, block-structure detection, LD regrouping."""
+import numpy as np
+import pytest
+import scipy.sparse
+
+from partition import (detect_blocks_csr, detect_blocks_dense, marker_offsets,
+                       partition_blocks)
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 4, 8])
+def test_equal_blocks_split_evenly(nranks):
+    r = partition_blocks([25000] * 8, nranks)
+    assert r[0][0] == 0 and r[-1][1] == 8
+    assert all(b1 - b0 == 8 // nranks for b0, b1 in r)
+    assert all(r[i][1] == r[i + 1][0] for i in range(nranks - 1))
+
+
+def test_uneven_blocks_balanced_by_bytes():
+    sizes = [100, 100, 100, 400, 50, 50, 300, 200]
+    r = partition_blocks(sizes, 3)
+    w = [sum(s * s for s in sizes[b0:b1]) for b0, b1 in r]
+    assert all(b1 > b0 for b0, b1 in r)
+    assert max(w) <= 0.6 * sum(w)
+
+
+def test_every_rank_gets_a_block():
+    r = partition_blocks([1000, 1, 1, 1], 4)
+    assert [b1 - b0 for b0, b1 in r] == [1, 1, 1, 1]
+    with pytest.raises(ValueError):
+        partition_blocks([5, 5], 3)
+
+
+def test_marker_offsets():
+    np.testing.assert_array_equal(marker_offsets([3, 4, 5]), [0, 3, 7, 12])
+
+
+def _blockdiag(sizes, seed=0):
+    rs = np.random.RandomState(seed)
+    M = sum(sizes)
+    R = np.zeros((M, M))
+    o = 0
+    for n in sizes:
+        B = rs.normal(size=(n, n))
+        R[o:o + n, o:o + n] = B + B.T
+        o += n
+    return R
+
+
+def test_detect_blocks_dense_and_csr():
+    sizes = [5, 1, 7, 3]
+    R = _blockdiag(sizes)
+    assert detect_blocks_dense(R) == sizes
+    A = scipy.sparse.csr_matrix(R)
+    assert detect_blocks_csr(A.indptr, A.indices, R.shape[0]) == sizes
+
+
+def test_detect_blocks_sparse_pattern_inside_block():
+    # a block whose first and last marker are linked only through the corner
+    R = np.eye(6)
+    R[0, 3] = R[3, 0] = 0.5
+    R[4, 5] = R[5, 4] = 0.1
+    assert detect_blocks_dense(R) == [4, 2]
+    A = scipy.sparse.csr_matrix(R)
+    assert detect_blocks_csr(A.indptr, A.indices, 6) == [4, 2]
+
+
+def test_blockld_regroup_and_common_partition():
+    from sgvamp import BlockLD, common_partition
+
+    R = _blockdiag([3, 2, 4])
+    L = BlockLD.from_dense(R)
+    assert L.block_sizes == [3, 2, 4]
+    assert common_partition([[3, 2, 4], [5, 4]]) == [5, 4]
+    G = L.regroup([5, 4])
+    np.testing.assert_array_equal(G.block(0), R[:5, :5])
+    np.testing.assert_array_equal(G.block(1), R[5:, 5:])
+    with pytest.raises(ValueError):
+        L.regroup([4, 5])
