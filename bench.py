@@ -3,8 +3,14 @@
 
 Workload (C2): K = 1 cohort, M = 200,000 markers in 8 LD blocks of 25,000,
 N = 10,000 samples, the reference CLI's default flags (gamw 5, gam1 1e-6,
-rho 0.5, prior 0,1 / 0.99,0.01, cg-maxit 500, EM prior from it 1 with <= 100
-steps, learn-gamw 1, lmmse-damp 0, s 0).  Synthetic data generated on the
+rho 0.5, cg-maxit 500, EM prior from it 1 with <= 100 steps, learn-gamw 1,
+lmmse-damp 0, s 0) except the prior: --prior matched (default) sets
+--prior-vars 0,0.8/cm --prior-probs 0.5,0.5, the simulated mixture.  With the
+CLI default prior (0,1 / 0.99,0.01: slab variance 1*Nt = 1e4 against a
+simulated effect variance of 0.08) the reference algorithm's EM drives lam to 0
+and the run turns NaN within a few iterations (tests/test_gpu_parity.py::
+test_vamp_medium_scale_vs_oracle[cli_default] shows the oracle does the same),
+after which every CG runs to cg-maxit: not a meaningful benchmark.  Synthetic data generated on the
 device following simulation/sim_gen_phen_mult.py (X ~ Bin(2, 0.4), 50 %
 causal markers, h2 = 0.8).  A "step" is one VAMP outer iteration
 (src/sgvamp.py:222-387): EM prior update, denoiser, both CG solves, gamw
@@ -50,6 +56,7 @@ def parse():
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     p.add_argument("--cpu-iters", type=int, default=3)
     p.add_argument("--no-files", action="store_true", help="skip the per-iteration output files")
+    p.add_argument("--prior", choices=["matched", "cli"], default="matched")
     return p.parse_args()
 
 
@@ -135,7 +142,12 @@ def main():
     N_list = [args.nsamp] * K
     Nt = sum(N_list)
     a = np.array(N_list) / Nt
-    flags = dict(rho=0.5, gamw=5.0, gam1=1e-6, prior_vars=[0.0, 1.0], prior_probs=[0.99, 0.01])
+    cm = int(eng.M * 0.5)
+    if args.prior == "matched":
+        prior = dict(prior_vars=[0.0, 0.8 / cm], prior_probs=[0.5, 0.5])
+    else:
+        prior = dict(prior_vars=[0.0, 1.0], prior_probs=[0.99, 0.01])
+    flags = dict(rho=0.5, gamw=5.0, gam1=1e-6, **prior)
     run = dict(cg_maxit=500, em_prior_maxit=100, learn_gamw=True, lmmse_damp=False,
                prior_update="em", update_prior_from=1)
     tmp = tempfile.mkdtemp(prefix="sgvamp_bench_")
@@ -193,11 +205,12 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: device generator following simulation/sim_gen_phen_mult.py "
-                "(Bin(2,0.4) genotypes, 50% causal, h2=0.8), seed %d" % args.seed,
+                "(Bin(2,0.4) genotypes, 50%% causal, h2=0.8), seed %d" % args.seed,
         "config": {
             "workload": "C2 (BASELINE.json configs[1]): K=%d cohort, M=%d markers in %d LD blocks "
                         "of %d, N=%d, reference CLI default flags, output files written each "
-                        "iteration" % (K, eng.M, args.blocks, args.block_size, args.nsamp),
+                        "iteration, prior %s %s" % (K, eng.M, args.blocks, args.block_size, args.nsamp,
+                                            prior["prior_vars"], prior["prior_probs"]),
             "K": K, "M": eng.M, "ld_blocks": args.blocks, "block_size": args.block_size,
             "N": args.nsamp, "parallelism": "LD blocks sharded over %d GPU rank(s)" % world,
         },

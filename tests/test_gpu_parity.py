@@ -112,7 +112,7 @@ def test_cg_solve_vs_oracle():
         A = lambda p, j=j: c1[j] * L.matvec_Rs(p) + c2[j] * p
         xr, info_r, it_r, _ = vo.cg_scipy(A, Bm[j], X0[j], 500, vo.Reducer())
         assert (it[j], info[j]) == (it_r, info_r), j
-        assert maxrel(X[j], xr) < 1e-9, j
+        assert maxrel(X[j], xr) < 1e-7, j      # CG amplifies summation-order rounding
         res = np.linalg.norm(Bm[j] - A(X[j])) / np.linalg.norm(Bm[j])
         assert res < 1e-5
     # maxiter exhaustion and a zero right-hand side
@@ -264,7 +264,11 @@ def test_synth_generator_vs_oracle():
 # ---------------------------------------------------------------------------
 # medium scale: HIP VAMP vs oracle on device-generated data
 # ---------------------------------------------------------------------------
-def test_vamp_medium_scale_vs_oracle(tmp_path):
+@pytest.mark.parametrize("prior", ["matched", "cli_default"])
+def test_vamp_medium_scale_vs_oracle(prior, tmp_path):
+    """Rank-deficient blocks (n_b > N) like C2.  With the CLI default prior
+    (slab variance 1*Nt, far above the simulated effect size) the trajectory
+    degenerates; the oracle does the same, step for step."""
     sizes = [3000, 2500, 3500, 3000]
     nsamp = 2000
     M = sum(sizes)
@@ -278,8 +282,8 @@ def test_vamp_medium_scale_vs_oracle(tmp_path):
     eng.synth_r(0, 123, nsamp, y)
     blocks = [eng.get_ld_block(0, b) for b in range(len(sizes))]
     r = eng.get_vector(hb.VEC_R, 0)
-    prior_vars = [0.0, 0.8 / cm]
-    prior_probs = [0.9, 0.1]
+    prior_vars = [0.0, 0.8 / cm] if prior == "matched" else [0.0, 1.0]
+    prior_probs = [0.9, 0.1] if prior == "matched" else [0.99, 0.01]
     x0 = beta * np.sqrt(nsamp)
     v = VAMP(N=nsamp, Nt=nsamp, M=M, K=1, rho=0.5, gamw=5.0, gam1=1e-6, a=[1.0],
              prior_vars=prior_vars, prior_probs=prior_probs, out_dir=str(tmp_path), out_name="m",
@@ -292,6 +296,12 @@ def test_vamp_medium_scale_vs_oracle(tmp_path):
                  prior_vars=prior_vars, prior_probs=prior_probs, x0=x0, seed=3,
                  lmmse_damp=False, reducer=vo.Reducer("blocked", bounds=L.bounds))
     for it in range(its):
-        assert maxrel(xh[it].ravel() / np.sqrt(nsamp), t["xhat"][it]) < 1e-8, it
+        ref = np.asarray(t["xhat"][it])
+        got = xh[it].ravel() / np.sqrt(nsamp)
+        if np.isnan(ref).any():
+            assert np.array_equal(np.isnan(ref), np.isnan(got)), it
+            continue
+        assert maxrel(got, ref) < 1e-8, it
     assert [h["cg_iters"][0] for h in v.history] == [list(x[0]) for x in t["cg_iters"]]
+    assert [h.get("em_steps") for h in v.history][1:] == list(t["em_steps"])
     eng.close()
