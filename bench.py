@@ -173,6 +173,7 @@ def main():
     recs = []
     for it in range(args.warmup, args.warmup + args.steps):
         recs.append(v.step(it))
+    v.flush()                                           # output files of the timed steps
     eng.sync()
     t1 = time.perf_counter()
     comm.barrier()
@@ -238,6 +239,7 @@ def main():
         result["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(result), flush=True)
+    v.finish()
     eng.close()
 
 

@@ -63,15 +63,20 @@ struct sgv_ctx {
   double* h_tot = nullptr;
   double* d_pq = nullptr;
   int nbmax = 0;
-  // staging
+  // staging (device) and pinned host staging: every host<->device copy goes
+  // through pinned memory and a spin wait (pageable copies block inside the
+  // runtime with its default wait policy)
   void* d_stage = nullptr;
   size_t stage_bytes = 0;
+  void* h_stage = nullptr;
+  size_t h_stage_bytes = 0;
   // comm
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   // solver state
   std::vector<int> xnz;        // x0.any() per CG column (2K)
   std::vector<int> rx0_valid;  // RX0[c] == R_s X[c]
+  hipEvent_t ev_sync = nullptr;   // host waits spin on this event
   // timers
   std::vector<hipEvent_t> evpool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
@@ -123,6 +128,20 @@ static int fail(sgv_ctx* c, int code, const char* fmt, ...) {
 
 static int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
+// Host wait for the ctx stream: record an event and spin on it.  The default
+// hipStreamSynchronize may park the thread and wake it late (measured on
+// MI355X: ~10 ms extra per wait), and the CG loop waits once per iteration.
+static int stream_wait(sgv_ctx* c) {
+  HIPCHK(hipEventRecord(c->ev_sync, c->st));
+  hipError_t e;
+  while ((e = hipEventQuery(c->ev_sync)) == hipErrorNotReady) {
+    __builtin_ia32_pause();
+  }
+  if (e != hipSuccess)
+    return fail(c, SGV_ERR_HIP, "stream wait: %s", hipGetErrorString(e));
+  return SGV_OK;
+}
+
 // ---------------------------------------------------------------------------
 // reductions
 // ---------------------------------------------------------------------------
@@ -161,7 +180,7 @@ static int reduce_dev(sgv_ctx* c, int nv, const int* d_begin, const Map16& map, 
 static int reduce_host(sgv_ctx* c, int nv, const int* d_begin, double* out) {
   CHK(reduce_dev(c, nv, d_begin, identity_map(), c->d_tot));
   HIPCHK(hipMemcpyAsync(c->h_tot, c->d_tot, sizeof(double) * nv, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));
+  CHK(stream_wait(c));
   resolve_timers(c);
   std::memcpy(out, c->h_tot, sizeof(double) * nv);
   return SGV_OK;
@@ -176,18 +195,40 @@ static int ensure_stage(sgv_ctx* c, size_t bytes) {
   return SGV_OK;
 }
 
+static int ensure_hstage(sgv_ctx* c, size_t bytes) {
+  if (bytes <= c->h_stage_bytes) return SGV_OK;
+  if (c->h_stage) HIPCHK(hipHostFree(c->h_stage));
+  c->h_stage = nullptr;
+  HIPCHK(hipHostMalloc(&c->h_stage, bytes));
+  c->h_stage_bytes = bytes;
+  return SGV_OK;
+}
+
+// host (pageable) -> pinned -> device staging buffer; returns when the copy
+// has landed (the pinned buffer may be reused right away)
+static int h2d(sgv_ctx* c, const void* host, size_t bytes) {
+  CHK(ensure_stage(c, std::max<size_t>(bytes, 8)));
+  CHK(ensure_hstage(c, std::max<size_t>(bytes, 8)));
+  std::memcpy(c->h_stage, host, bytes);
+  HIPCHK(hipMemcpyAsync(c->d_stage, c->h_stage, bytes, hipMemcpyHostToDevice, c->st));
+  return stream_wait(c);
+}
+
 static int upload_vec(sgv_ctx* c, const double* host, double* dpad) {
-  CHK(ensure_stage(c, sizeof(double) * std::max<int64_t>(c->Mloc, 1)));
-  HIPCHK(hipMemcpyAsync(c->d_stage, host, sizeof(double) * c->Mloc, hipMemcpyHostToDevice, c->st));
+  CHK(h2d(c, host, sizeof(double) * c->Mloc));
   HIPCHK(launch_unpack(c->d_ch, c->nch, c->d_ch_doff, (const double*)c->d_stage, dpad, c->st));
   return SGV_OK;
 }
 
 static int download_vec(sgv_ctx* c, const double* dpad, double* host) {
-  CHK(ensure_stage(c, sizeof(double) * std::max<int64_t>(c->Mloc, 1)));
+  const size_t bytes = sizeof(double) * std::max<int64_t>(c->Mloc, 1);
+  CHK(ensure_stage(c, bytes));
+  CHK(ensure_hstage(c, bytes));
   HIPCHK(launch_pack(c->d_ch, c->nch, c->d_ch_doff, dpad, (double*)c->d_stage, c->st));
-  HIPCHK(hipMemcpyAsync(host, c->d_stage, sizeof(double) * c->Mloc, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));
+  HIPCHK(hipMemcpyAsync(c->h_stage, c->d_stage, sizeof(double) * c->Mloc, hipMemcpyDeviceToHost,
+                        c->st));
+  CHK(stream_wait(c));
+  std::memcpy(host, c->h_stage, sizeof(double) * c->Mloc);
   return SGV_OK;
 }
 
@@ -209,7 +250,7 @@ static int ld_ensure(sgv_ctx* c, int ld, int b) {
   c->ldR[ld][b] = p;
   BlkDesc d{p, c->lda[b], c->bn[b], c->bvoff[b]};
   HIPCHK(hipMemcpyAsync(c->d_blks[ld] + b, &d, sizeof d, hipMemcpyHostToDevice, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));
+  CHK(stream_wait(c));
   return SGV_OK;
 }
 
@@ -385,6 +426,9 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
     return code;
   };
   if (hipSetDevice(device) != hipSuccess) return cleanup(fail(nullptr, SGV_ERR_HIP, "hipSetDevice"));
+  (void)hipSetDeviceFlags(hipDeviceScheduleSpin);   // best effort; waits spin anyway
+  if (hipEventCreateWithFlags(&c->ev_sync, hipEventDisableTiming) != hipSuccess)
+    return cleanup(fail(nullptr, SGV_ERR_HIP, "hipEventCreate"));
   if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail(nullptr, SGV_ERR_HIP, "hipStreamCreate"));
 
@@ -521,11 +565,13 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   (void)hipFree(c->d_pq);
   if (c->h_tot) (void)hipHostFree(c->h_tot);
   if (c->d_stage) (void)hipFree(c->d_stage);
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
   for (auto& pr : c->pending) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
   }
   for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
+  if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
 }
@@ -594,7 +640,7 @@ extern "C" int sgv_get_ld_block(sgv_ctx* c, int ld, int b, double* host, int64_t
     return fail(c, SGV_ERR_ARG, "sgv_get_ld_block: bad arguments (ld=%d b=%d)", ld, b);
   CHK(ld_ready(c, ld));
   const int64_t n = c->bn[b];
-  HIPCHK(hipStreamSynchronize(c->st));
+  CHK(stream_wait(c));
   HIPCHK(hipMemcpy2D(host, sizeof(double) * ld_host, c->ldR[ld][b], sizeof(double) * c->lda[b],
                      sizeof(double) * n, n, hipMemcpyDeviceToHost));
   return SGV_OK;
@@ -632,7 +678,7 @@ extern "C" int sgv_set_vector(sgv_ctx* c, int which, int k, const double* host) 
   double* d = vec_ptr(c, which, k);
   if (!d || !host) return fail(c, SGV_ERR_ARG, "sgv_set_vector: which=%d k=%d", which, k);
   CHK(upload_vec(c, host, d));
-  HIPCHK(hipStreamSynchronize(c->st));
+  CHK(stream_wait(c));
   if (which == SGV_VEC_XHAT2 || which == SGV_VEC_SIG2U) {
     const int col = 2 * k + (which == SGV_VEC_SIG2U);
     c->xnz[col] = host_any(host, c->Mloc);
@@ -675,7 +721,9 @@ extern "C" int sgv_synth_ld_g(sgv_ctx* c, int ld, uint64_t seed, int64_t marker0
   HIPCHK(hipMalloc(&sb.sd, sizeof(double) * nmax));
   HIPCHK(hipMalloc(&sb.vec, sizeof(double) * std::max<int64_t>(c->Mloc, 1)));
   HIPCHK(hipMalloc(&sb.g, sizeof(double) * Nsamp));
-  HIPCHK(hipMemcpy(sb.vec, beta, sizeof(double) * c->Mloc, hipMemcpyHostToDevice));
+  CHK(h2d(c, beta, sizeof(double) * c->Mloc));
+  HIPCHK(hipMemcpyAsync(sb.vec, c->d_stage, sizeof(double) * c->Mloc, hipMemcpyDeviceToDevice,
+                        c->st));
   for (int b = 0; b < c->nblk; ++b) {
     const int n = (int)c->bn[b];
     const int64_t gm0 = marker0 + c->boff[b];
@@ -686,9 +734,10 @@ extern "C" int sgv_synth_ld_g(sgv_ctx* c, int ld, uint64_t seed, int64_t marker0
       HIPCHK(launch_syrk_nt(sb.G, n, Nsamp, ldg, c->ldR[ld][b], c->lda[b], c->st));
     }
     HIPCHK(launch_g_accum(seed, gm0, n, Nsamp, sb.mean, sb.sd, sb.vec + c->boff[b], sb.g, c->st));
-    HIPCHK(hipMemcpyAsync(g_out + (size_t)b * Nsamp, sb.g, sizeof(double) * Nsamp,
-                          hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(ensure_hstage(c, sizeof(double) * Nsamp));
+    HIPCHK(hipMemcpyAsync(c->h_stage, sb.g, sizeof(double) * Nsamp, hipMemcpyDeviceToHost, c->st));
+    CHK(stream_wait(c));
+    std::memcpy(g_out + (size_t)b * Nsamp, c->h_stage, sizeof(double) * Nsamp);
   }
   std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), 0);
   return SGV_OK;
@@ -705,7 +754,8 @@ extern "C" int sgv_synth_r(sgv_ctx* c, int k, uint64_t seed, int64_t marker0, in
   HIPCHK(hipMalloc(&sb.mean, sizeof(double) * nmax));
   HIPCHK(hipMalloc(&sb.sd, sizeof(double) * nmax));
   HIPCHK(hipMalloc(&sb.g, sizeof(double) * Nsamp));
-  HIPCHK(hipMemcpy(sb.g, y, sizeof(double) * Nsamp, hipMemcpyHostToDevice));
+  CHK(h2d(c, y, sizeof(double) * Nsamp));
+  HIPCHK(hipMemcpyAsync(sb.g, c->d_stage, sizeof(double) * Nsamp, hipMemcpyDeviceToDevice, c->st));
   for (int b = 0; b < c->nblk; ++b) {
     const int n = (int)c->bn[b];
     const int64_t gm0 = marker0 + c->boff[b];
@@ -713,7 +763,7 @@ extern "C" int sgv_synth_r(sgv_ctx* c, int k, uint64_t seed, int64_t marker0, in
     HIPCHK(launch_geno_G(seed, gm0, n, Nsamp, ldg, sb.mean, sb.sd, sb.G, c->st));
     HIPCHK(launch_row_dot(sb.G, n, Nsamp, ldg, sb.g, c->r[k] + c->bvoff[b], c->st));
   }
-  HIPCHK(hipStreamSynchronize(c->st));
+  CHK(stream_wait(c));
   return SGV_OK;
 }
 
@@ -822,8 +872,7 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
   int passes = 0;
 
   // probes u_k (:326), int8 +-1 -> f64
-  CHK(ensure_stage(c, (size_t)K * std::max<int64_t>(c->Mloc, 1)));
-  HIPCHK(hipMemcpyAsync(c->d_stage, probes, (size_t)K * c->Mloc, hipMemcpyHostToDevice, c->st));
+  CHK(h2d(c, probes, (size_t)K * c->Mloc));
   for (int k = 0; k < K; ++k)
     HIPCHK(launch_unpack_i8(c->d_ch, c->nch, c->d_ch_doff,
                             (const int8_t*)c->d_stage + (size_t)k * c->Mloc, c->U[k], c->st));
@@ -969,7 +1018,7 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
       CHK(reduce_dev(c, nc, c->d_rg_begin, map, c->d_tot));
       HIPCHK(hipMemcpyAsync(c->h_tot, c->d_tot, sizeof(double) * ncol, hipMemcpyDeviceToHost,
                             c->st));
-      HIPCHK(hipStreamSynchronize(c->st));
+      CHK(stream_wait(c));
       resolve_timers(c);
       std::memcpy(gt, c->h_tot, sizeof(double) * ncol);
       for (int k = 0; k < K; ++k) {
@@ -987,7 +1036,7 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
       }
     }
   } else {
-    HIPCHK(hipStreamSynchronize(c->st));
+    CHK(stream_wait(c));
   }
   if (passes_out) *passes_out = passes;
   return SGV_OK;
@@ -1101,7 +1150,7 @@ extern "C" int sgv_cg_solve(sgv_ctx* c, int ld, int ncol, const double* c1, cons
 
 extern "C" int sgv_timers(sgv_ctx* c, double* t4, int reset) {
   ENTER(c);
-  HIPCHK(hipStreamSynchronize(c->st));
+  CHK(stream_wait(c));
   resolve_timers(c);
   if (t4) {
     double bytes = 0.0;
@@ -1121,7 +1170,7 @@ extern "C" int sgv_timers(sgv_ctx* c, double* t4, int reset) {
 
 extern "C" int sgv_sync(sgv_ctx* c) {
   ENTER(c);
-  HIPCHK(hipStreamSynchronize(c->st));
+  CHK(stream_wait(c));
   resolve_timers(c);
   return SGV_OK;
 }

@@ -21,6 +21,7 @@ import csv
 import logging
 import os
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -252,6 +253,7 @@ class VAMP:
                    update_prior_from=update_prior_from, return_xhat=return_xhat)
         for it in range(iterations):
             self.step(it)
+        self.finish()
         self.gamws = self._st["gamws"]
         return self._st["xhat1s"]
 
@@ -269,8 +271,42 @@ class VAMP:
                         em_prior_maxit=em_prior_maxit, learn_gamw=learn_gamw,
                         lmmse_damp=lmmse_damp, prior_update=prior_update,
                         update_prior_from=update_prior_from, return_xhat=return_xhat)
+        # host work that overlaps the GPU: the next iteration's probes are drawn
+        # (in stream order) while the current one runs; output files are written
+        # by a writer thread (at most one iteration in flight).
+        self._probe_pool = ThreadPoolExecutor(max_workers=1)
+        self._write_pool = ThreadPoolExecutor(max_workers=1)
+        self._next_probes = self._probe_pool.submit(self._draw_probes)
+        self._pending_write = None
         if self.rank == 0:
             logging.debug(f"a = {self.a}")
+
+    def _draw_probes(self):
+        """u_k = binomial(p=1/2, n=1, size=M)*2-1 (src/sgvamp.py:326), local slice."""
+        eng = self.engine
+        u = np.empty((self.K, eng.Mloc), dtype=np.int8)
+        for k in range(self.K):
+            u[k] = (self._st["probes"][k].binomial(p=1 / 2, n=1, size=self.M) * 2 - 1)[eng.sl]
+        return u
+
+    def _write_outputs(self, it, xhat_loc, r1_locs):
+        Nt = self.Nt
+        self.write_xhat_to_file(it, xhat_loc / np.sqrt(Nt))           # :281
+        for k, r1 in enumerate(r1_locs):
+            self.write_r1_to_file(it, r1 / np.sqrt(Nt), k + 1)        # :283
+
+    def flush(self):
+        """Wait for the output files of every finished iteration."""
+        if getattr(self, "_pending_write", None) is not None:
+            self._pending_write.result()
+            self._pending_write = None
+
+    def finish(self):
+        self.flush()
+        for pool in ("_probe_pool", "_write_pool"):
+            if getattr(self, pool, None) is not None:
+                getattr(self, pool).shutdown(wait=True)
+                setattr(self, pool, None)
 
     def step(self, it):
         """One outer iteration, src/sgvamp.py:222-387."""
@@ -313,10 +349,10 @@ class VAMP:
         if self.write_files or st["return_xhat"]:
             xhat_loc = eng.get_vector(hb.VEC_XHAT1)
             if self.write_files:
-                self.write_xhat_to_file(it, xhat_loc / np.sqrt(Nt))   # :281
-                for k in range(K):
-                    self.write_r1_to_file(it, eng.get_vector(hb.VEC_R1, k) / np.sqrt(Nt),
-                                          k + 1)                     # :283
+                r1_locs = [eng.get_vector(hb.VEC_R1, k) for k in range(K)]
+                self.flush()
+                self._pending_write = self._write_pool.submit(self._write_outputs, it, xhat_loc,
+                                                              r1_locs)
             if st["return_xhat"]:
                 full = xhat_loc
                 if self.comm.Get_size() > 1:
@@ -334,9 +370,8 @@ class VAMP:
             logging.debug(f"[rank = {rank}] gam2 = {gam2[0]}")
         for k in range(K):
             logging.info(f"...LMMSE cohort {k}")
-        u = np.empty((K, eng.Mloc), dtype=np.int8)
-        for k in range(K):
-            u[k] = (st["probes"][k].binomial(p=1 / 2, n=1, size=M) * 2 - 1)[eng.sl]   # :326
+        u = self._next_probes.result()                                # :326
+        self._next_probes = self._probe_pool.submit(self._draw_probes)
         out, cg, passes = eng.lmmse(it, gamw, gam2, alpha1, alpha2, u, st["cg_maxit"],
                                     st["lmmse_damp"], rho, st["learn_gamw"])
         rec.update(cg_iters=cg[:, [0, 2]].tolist(), cg_info=cg[:, [1, 3]].tolist(),
