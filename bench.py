@@ -57,6 +57,8 @@ def parse():
     p.add_argument("--cpu-iters", type=int, default=3)
     p.add_argument("--no-files", action="store_true", help="skip the per-iteration output files")
     p.add_argument("--prior", choices=["matched", "cli"], default="matched")
+    p.add_argument("--ld-format", choices=["packed", "dense"], default="packed",
+                   help="LD block storage: packed symmetric panels (default) or full squares")
     return p.parse_args()
 
 
@@ -138,6 +140,7 @@ def main():
     K = args.K
     t_setup = time.perf_counter()
     eng = Engine(sizes, K, ld_of=[0] * K, comm=comm, device=device)
+    eng.set_ld_packing(args.ld_format == "packed")
     beta, _ = make_problem(eng, comm, args)
     N_list = [args.nsamp] * K
     Nt = sum(N_list)
@@ -188,11 +191,13 @@ def main():
     value = steps / dt
     launches = max(tm["ld_launches"], 1)
     avg_s = tm["ld_ms"] / 1e3 / launches
-    bytes_launch = tm["ld_bytes_per_pass"] + tm["rhs_bytes"] / launches
+    ld_bytes_launch = tm["ld_bytes"] / launches            # stored LD bytes actually read
+    bytes_launch = ld_bytes_launch + tm["rhs_bytes"] / launches
     achieved = bytes_launch / avg_s / 1e9 if avg_s > 0 else None
-    traffic, traffic_src = read_traffic()
+    dense_equiv = (tm["dense_bytes"] / launches + tm["rhs_bytes"] / launches) / avg_s / 1e9
+    traffic, traffic_src = read_traffic("k_sym_pass" if args.ld_format == "packed" else "k_ld_pass")
     passes = sum(r["ld_passes"] for r in recs)
-    ld_bytes_total = tm["ld_bytes_per_pass"] * comm.Get_size()
+    ld_bytes_total = ld_bytes_launch * comm.Get_size()
     result = {
         "metric": "VAMP iterations/sec (and effective LD-matvec GB/s) at M markers, K cohorts",
         "value": value,
@@ -222,8 +227,12 @@ def main():
             "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": traffic,
-            "kernel": "sgv::k_ld_pass (LD mat-vec, per GPU)",
+            "kernel": ("sgv::k_sym_pass + k_sym_finalize (packed symmetric LD pass, per GPU)"
+                       if args.ld_format == "packed" else "sgv::k_ld_pass (dense LD pass, per GPU)"),
             "bytes_per_launch": bytes_launch,
+            "ld_format": args.ld_format,
+            "dense_equivalent_GBs": dense_equiv,
+            "aux_partial_bytes_per_launch": tm["aux_bytes"] / launches,
             "avg_launch_ms": avg_s * 1e3,
             "launches": int(launches),
             "traffic_source": traffic_src,

@@ -93,6 +93,13 @@ int sgv_comm_init(sgv_ctx* ctx, int nranks, int rank, const char* id /* 128 byte
  * Replaces the R loaders src/main.py:199-202 (dense .npy / CSR .npz blocks). */
 int sgv_set_ld_block(sgv_ctx* ctx, int ld, int blk_local, const double* rowmajor,
                      int64_t ld_host);
+/* Storage of LD blocks set or generated from now on: mode 1 (default) stores a
+ * block that is exactly symmetric as packed upper-triangle panels (about half
+ * the bytes per pass: the LD matrix of src/main.py:199-265 is symmetric by
+ * construction, R = X^T X); mode 0 always stores the full square. */
+int sgv_set_ld_packing(sgv_ctx* ctx, int mode);
+/* fmt_out: 0 dense, 1 packed symmetric, -1 not set. */
+int sgv_ld_block_format(sgv_ctx* ctx, int ld, int blk_local, int* fmt_out);
 /* Download one LD block (row-major n x n into a host array of row stride ld_host). */
 int sgv_get_ld_block(sgv_ctx* ctx, int ld, int blk_local, double* rowmajor, int64_t ld_host);
 /* R_s = (1 - s) R + s I, applied inside every LD pass (src/main.py:265). */
@@ -172,11 +179,12 @@ int sgv_cg_solve(sgv_ctx* ctx, int ld, int ncol, const double* c1, const double*
                  int* info_out);
 
 /* ---- timing -------------------------------------------------------------- */
-/* t[0] = summed LD-pass kernel time (ms, HIP events on the ctx stream),
- * t[1] = LD-pass launches, t[2] = algorithmic LD bytes per full pass (all owned
- * blocks, all LD matrices: sum n_b^2 * 8), t[3] = RHS bytes moved by those
- * launches (2 * ncol * M_local * 8 summed).  Reset with reset != 0. */
-int sgv_timers(sgv_ctx* ctx, double* t4, int reset);
+/* Summed over LD passes since the last reset (HIP events on the ctx stream):
+ * t[0] = kernel time (ms), t[1] = passes, t[2] = LD bytes read (the stored
+ * bytes: n^2*8 dense, sum over panels H*(n - r0)*8 packed), t[3] = RHS bytes
+ * (2 * ncol * M_local * 8), t[4] = dense-equivalent LD bytes (n^2*8),
+ * t[5] = packed-pass partial-buffer bytes (written + read).  reset != 0 zeroes. */
+int sgv_timers(sgv_ctx* ctx, double* t6, int reset);
 
 /* Synchronise the ctx stream. */
 int sgv_sync(sgv_ctx* ctx);

@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <utility>
@@ -23,6 +24,42 @@
 using namespace sgv;
 
 static thread_local std::string g_last_err;
+
+// one LD block of one LD matrix
+struct LdBlock {
+  double* ptr = nullptr;
+  int fmt = 0;                 // 0: dense n x lda row-major; 1: packed symmetric panels
+  std::vector<int64_t> poff, pw;   // packed: panel offsets and row strides (doubles)
+  int64_t* d_poff = nullptr;
+  int64_t* d_pw = nullptr;
+  double stored_bytes = 0.0;   // bytes a pass reads: n^2*8 dense, sum H_g (n - r0_g)*8 packed
+};
+
+// launch tables of one LD matrix (rebuilt when a block's storage changes)
+struct LdPlan {
+  bool valid = false;
+  RowGroup* d_rg = nullptr;    // dense blocks
+  int nrg = 0;
+  int* d_pbeg = nullptr;       // partial slots of block b: [pbeg[b], pbeg[b+1])
+  int nparts = 0;
+  SymItem* d_items[4] = {nullptr, nullptr, nullptr, nullptr};   // per chunk width class
+  int nitems[4] = {0, 0, 0, 0};
+  SymPanel* d_panels[4] = {nullptr, nullptr, nullptr, nullptr};
+  int npanels = 0;
+  double stored_bytes = 0.0, dense_bytes = 0.0;
+};
+
+// chunk-width class of the packed pass for nc columns (CW = 1024 >> cls);
+// SGV_SYM_WIDE=0 selects the narrower supported class (A/B tuning)
+static int sym_class(int nc) {
+  static const int narrow = [] {
+    const char* e = std::getenv("SGV_SYM_WIDE");
+    return (e && e[0] == '0') ? 1 : 0;
+  }();
+  const int base = nc <= 2 ? 0 : nc <= 4 ? 1 : nc <= 8 ? 2 : 3;
+  return std::min(3, base + (nc <= 8 ? narrow : 0));
+}
+static int sym_class_nc(int cls) { return std::min(16, 2 << (cls + 1)); }   // widest NC using cls
 
 struct sgv_ctx {
   int dev = 0;
@@ -37,18 +74,20 @@ struct sgv_ctx {
   int64_t Mtot = 0;
   double s = 0.0;
   std::vector<double> Ncoh;
-  // LD storage [ld][b]
-  std::vector<std::vector<double*>> ldR;
+  // LD storage [ld][b] and the per-LD launch plans
+  std::vector<std::vector<LdBlock>> ldb;
   std::vector<int64_t> lda;
   std::vector<BlkDesc*> d_blks;
+  std::vector<LdPlan> plan;
+  int packing = 1;               // 1: packed symmetric storage for symmetric blocks
+  double* d_rowpart = nullptr;   // k_sym_pass row partials
+  double* d_colpart = nullptr;   // k_sym_pass column partials
+  size_t rowpart_cap = 0, colpart_cap = 0, part_cap = 0;
   // chunk / row-group layouts
   int nch = 0;
   ChunkDesc* d_ch = nullptr;
   int64_t* d_ch_doff = nullptr;
   int* d_ch_begin = nullptr;
-  int nrg = 0;
-  RowGroup* d_rg = nullptr;
-  int* d_rg_begin = nullptr;
   // vectors (padded layout, zero padding)
   double* pool = nullptr;
   std::vector<double*> r, r1, r2, U, X, X0, Rr, P, Q, RX0, S;
@@ -80,7 +119,8 @@ struct sgv_ctx {
   // timers
   std::vector<hipEvent_t> evpool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
-  double ld_ms = 0.0, ld_launches = 0.0, rhs_bytes = 0.0;
+  double ld_ms = 0.0, ld_launches = 0.0, rhs_bytes = 0.0, ld_bytes = 0.0, dense_bytes = 0.0,
+         aux_bytes = 0.0;
   std::string err;
 };
 
@@ -241,14 +281,55 @@ static bool host_any(const double* v, int64_t n) {
 // ---------------------------------------------------------------------------
 // LD pass (timed with HIP events on the ctx stream)
 // ---------------------------------------------------------------------------
-static int ld_ensure(sgv_ctx* c, int ld, int b) {
-  if (c->ldR[ld][b]) return SGV_OK;
-  const size_t bytes = sizeof(double) * (size_t)c->lda[b] * (size_t)c->bn[b];
-  double* p = nullptr;
-  HIPCHK(hipMalloc(&p, bytes));
-  HIPCHK(hipMemsetAsync(p, 0, bytes, c->st));
-  c->ldR[ld][b] = p;
-  BlkDesc d{p, c->lda[b], c->bn[b], c->bvoff[b]};
+static void free_plan(LdPlan& p) {
+  if (p.d_rg) (void)hipFree(p.d_rg);
+  if (p.d_pbeg) (void)hipFree(p.d_pbeg);
+  for (int k = 0; k < 4; ++k) {
+    if (p.d_items[k]) (void)hipFree(p.d_items[k]);
+    if (p.d_panels[k]) (void)hipFree(p.d_panels[k]);
+  }
+  p = LdPlan();
+}
+
+static void free_block(LdBlock& lb) {
+  if (lb.ptr) (void)hipFree(lb.ptr);
+  if (lb.d_poff) (void)hipFree(lb.d_poff);
+  if (lb.d_pw) (void)hipFree(lb.d_pw);
+  lb = LdBlock();
+}
+
+// allocate block b of LD matrix ld in format fmt (zero filled)
+static int ld_alloc(sgv_ctx* c, int ld, int b, int fmt) {
+  LdBlock& lb = c->ldb[ld][b];
+  if (lb.ptr && lb.fmt == fmt) return SGV_OK;
+  free_block(lb);
+  c->plan[ld].valid = false;
+  const int64_t n = c->bn[b];
+  size_t elems = 0;
+  lb.fmt = fmt;
+  if (fmt == 0) {
+    elems = (size_t)c->lda[b] * (size_t)n;
+    lb.stored_bytes = (double)n * (double)n * 8.0;
+  } else {
+    double valid = 0.0;
+    for (int64_t r0 = 0; r0 < n; r0 += SYM_H) {
+      const int64_t H = std::min<int64_t>(SYM_H, n - r0);
+      const int64_t w = round_up(n - r0, PADV);
+      lb.poff.push_back((int64_t)elems);
+      lb.pw.push_back(w);
+      elems += (size_t)(H * w);
+      valid += (double)H * (double)(n - r0);
+    }
+    lb.stored_bytes = valid * 8.0;
+    HIPCHK(hipMalloc(&lb.d_poff, sizeof(int64_t) * lb.poff.size()));
+    HIPCHK(hipMalloc(&lb.d_pw, sizeof(int64_t) * lb.pw.size()));
+    HIPCHK(hipMemcpy(lb.d_poff, lb.poff.data(), sizeof(int64_t) * lb.poff.size(),
+                     hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(lb.d_pw, lb.pw.data(), sizeof(int64_t) * lb.pw.size(), hipMemcpyHostToDevice));
+  }
+  HIPCHK(hipMalloc(&lb.ptr, sizeof(double) * elems));
+  HIPCHK(hipMemsetAsync(lb.ptr, 0, sizeof(double) * elems, c->st));
+  BlkDesc d{fmt == 0 ? lb.ptr : nullptr, c->lda[b], c->bn[b], c->bvoff[b]};
   HIPCHK(hipMemcpyAsync(c->d_blks[ld] + b, &d, sizeof d, hipMemcpyHostToDevice, c->st));
   CHK(stream_wait(c));
   return SGV_OK;
@@ -256,14 +337,116 @@ static int ld_ensure(sgv_ctx* c, int ld, int b) {
 
 static int ld_ready(sgv_ctx* c, int ld) {
   for (int b = 0; b < c->nblk; ++b)
-    if (!c->ldR[ld][b])
+    if (!c->ldb[ld][b].ptr)
       return fail(c, SGV_ERR_STATE, "LD matrix %d block %d has not been set", ld, b);
   return SGV_OK;
 }
 
+template <typename T>
+static int upload_table(sgv_ctx* c, const std::vector<T>& h, T** d) {
+  if (h.empty()) return SGV_OK;
+  HIPCHK(hipMalloc(d, sizeof(T) * h.size()));
+  HIPCHK(hipMemcpy(*d, h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+  return SGV_OK;
+}
+
+static int grow(sgv_ctx* c, double** buf, size_t* cap, size_t need) {
+  if (need <= *cap) return SGV_OK;
+  if (*buf) HIPCHK(hipFree(*buf));
+  *buf = nullptr;
+  HIPCHK(hipMalloc(buf, sizeof(double) * need));
+  *cap = need;
+  return SGV_OK;
+}
+
+// launch tables of LD matrix ld: dense row groups, packed (panel, chunk) items
+// per chunk-width class, panels; unified partial slots in block order
+static int ensure_plan(sgv_ctx* c, int ld) {
+  LdPlan& pl = c->plan[ld];
+  if (pl.valid) return SGV_OK;
+  CHK(ld_ready(c, ld));
+  free_plan(pl);
+  std::vector<RowGroup> rg;
+  std::vector<int> pbeg(c->nblk + 1, 0);
+  const int rows = ld_pass_rows_per_group();
+  int nparts = 0;
+  for (int b = 0; b < c->nblk; ++b) {
+    const LdBlock& lb = c->ldb[ld][b];
+    pbeg[b] = nparts;
+    pl.stored_bytes += lb.stored_bytes;
+    pl.dense_bytes += (double)c->bn[b] * (double)c->bn[b] * 8.0;
+    if (lb.fmt == 0) {
+      for (int64_t r0 = 0; r0 < c->bn[b]; r0 += rows) rg.push_back(RowGroup{b, (int32_t)r0, nparts++, 0});
+    } else {
+      nparts += (int)lb.poff.size();   // one slot per panel
+    }
+  }
+  pbeg[c->nblk] = nparts;
+  pl.nparts = nparts;
+  pl.nrg = (int)rg.size();
+  CHK(upload_table(c, rg, &pl.d_rg));
+  CHK(upload_table(c, pbeg, &pl.d_pbeg));
+  size_t rowpart_need = 0, colpart_need = 0;
+  for (int cls = 0; cls < 4; ++cls) {
+    const int cw = 1024 >> cls;
+    std::vector<SymItem> items;
+    std::vector<SymPanel> panels;
+    for (int b = 0; b < c->nblk; ++b) {
+      const LdBlock& lb = c->ldb[ld][b];
+      if (lb.fmt != 1) continue;
+      const int64_t n = c->bn[b];
+      const int blk_panel0 = (int)panels.size();
+      for (size_t g = 0; g < lb.poff.size(); ++g) {
+        const int r0 = (int)(g * SYM_H);
+        const int H = (int)std::min<int64_t>(SYM_H, n - r0);
+        const int ib = (int)items.size();
+        for (int64_t c0 = r0; c0 < n; c0 += cw) {
+          SymItem it;
+          it.P = lb.ptr + lb.poff[g];
+          it.w = lb.pw[g];
+          it.voff = c->bvoff[b];
+          it.r0 = r0;
+          it.H = H;
+          it.c0 = (int32_t)c0;
+          it.nc = (int32_t)std::min<int64_t>(cw, n - c0);
+          it.item = (int32_t)items.size();
+          it.diag_end = r0 + H;
+          items.push_back(it);
+        }
+        SymPanel pn;
+        pn.voff = c->bvoff[b];
+        pn.r0 = r0;
+        pn.H = H;
+        pn.item_begin = ib;
+        pn.item_end = (int)items.size();
+        pn.g = (int)g;
+        pn.blk_panel0 = blk_panel0;
+        pn.part = pbeg[b] + (int)g;
+        pn.pad_ = 0;
+        panels.push_back(pn);
+      }
+    }
+    pl.nitems[cls] = (int)items.size();
+    pl.npanels = (int)panels.size();
+    CHK(upload_table(c, items, &pl.d_items[cls]));
+    CHK(upload_table(c, panels, &pl.d_panels[cls]));
+    const size_t ncmax = (size_t)sym_class_nc(cls);
+    rowpart_need = std::max(rowpart_need, items.size() * SYM_H * ncmax);
+    colpart_need = std::max(colpart_need, items.size() * ncmax * (size_t)cw);
+  }
+  CHK(grow(c, &c->d_rowpart, &c->rowpart_cap, rowpart_need));
+  CHK(grow(c, &c->d_colpart, &c->colpart_cap, colpart_need));
+  CHK(grow(c, &c->d_part, &c->part_cap, (size_t)nparts * MAXC));
+  pl.valid = true;
+  return SGV_OK;
+}
+
+static const int* ld_parts(sgv_ctx* c, int ld) { return c->plan[ld].d_pbeg; }
+
 static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa) {
   if (nc <= 0) return SGV_OK;
-  CHK(ld_ready(c, ld));
+  CHK(ensure_plan(c, ld));
+  const LdPlan& pl = c->plan[ld];
   hipEvent_t e0, e1;
   if (c->evpool.size() < 2) {
     HIPCHK(hipEventCreate(&e0));
@@ -275,10 +458,21 @@ static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa) {
     c->evpool.pop_back();
   }
   HIPCHK(hipEventRecord(e0, c->st));
-  HIPCHK(launch_ld_pass(nc, c->d_blks[ld], c->d_rg, c->nrg, pa, c->d_part, c->st));
+  if (pl.nrg) HIPCHK(launch_ld_pass(nc, c->d_blks[ld], pl.d_rg, pl.nrg, pa, c->d_part, c->st));
+  if (pl.npanels) {
+    const int cls = sym_class(nc);
+    HIPCHK(launch_sym_pass(nc, cls, pl.d_items[cls], pl.nitems[cls], pa, c->d_rowpart,
+                           c->d_colpart, c->st));
+    HIPCHK(launch_sym_finalize(nc, cls, pl.d_panels[cls], pl.npanels, pa, c->d_rowpart,
+                               c->d_colpart, c->d_part, c->st));
+    const double cw = (double)(1024 >> cls);
+    c->aux_bytes += 2.0 * 8.0 * nc * (double)pl.nitems[cls] * (SYM_H + cw);
+  }
   HIPCHK(hipEventRecord(e1, c->st));
   c->pending.emplace_back(e0, e1);
   c->ld_launches += 1.0;
+  c->ld_bytes += pl.stored_bytes;
+  c->dense_bytes += pl.dense_bytes;
   c->rhs_bytes += 2.0 * nc * (double)c->Mloc * 8.0;
   return SGV_OK;
 }
@@ -353,7 +547,7 @@ static int cg_loop(sgv_ctx* c, const CgCols& cc, double* rho, const double* atol
       }
       if (!nc) continue;
       CHK(ld_pass(c, ld, nc, pa));
-      CHK(reduce_dev(c, nc, c->d_rg_begin, map, c->d_pq));
+      CHK(reduce_dev(c, nc, ld_parts(c, ld), map, c->d_pq));
       if (passes) ++*passes;
     }
     // alpha = rho / p.q; x += alpha p; r -= alpha q; rho_new = r.r (:412-415)
@@ -449,22 +643,15 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   std::vector<ChunkDesc> ch;
   std::vector<int64_t> chdoff;
   std::vector<int> chb(nblk + 1, 0);
-  std::vector<RowGroup> rg;
-  std::vector<int> rgb(nblk + 1, 0);
-  const int rows = ld_pass_rows_per_group();
   for (int b = 0; b < nblk; ++b) {
     chb[b] = (int)ch.size();
     for (int64_t o = 0; o < c->bn[b]; o += CHUNK) {
       ch.push_back(ChunkDesc{c->bvoff[b] + o, (int32_t)std::min<int64_t>(CHUNK, c->bn[b] - o), b});
       chdoff.push_back(c->boff[b] + o);
     }
-    rgb[b] = (int)rg.size();
-    for (int64_t r0 = 0; r0 < c->bn[b]; r0 += rows) rg.push_back(RowGroup{b, (int32_t)r0});
   }
   chb[nblk] = (int)ch.size();
-  rgb[nblk] = (int)rg.size();
   c->nch = (int)ch.size();
-  c->nrg = (int)rg.size();
 
 #define CREATE_HIP(expr)                                                          \
   do {                                                                            \
@@ -480,13 +667,10 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
                        hipMemcpyHostToDevice));
   CREATE_HIP(hipMalloc(&c->d_ch_begin, sizeof(int) * chb.size()));
   CREATE_HIP(hipMemcpy(c->d_ch_begin, chb.data(), sizeof(int) * chb.size(), hipMemcpyHostToDevice));
-  CREATE_HIP(hipMalloc(&c->d_rg, sizeof(RowGroup) * rg.size()));
-  CREATE_HIP(hipMemcpy(c->d_rg, rg.data(), sizeof(RowGroup) * rg.size(), hipMemcpyHostToDevice));
-  CREATE_HIP(hipMalloc(&c->d_rg_begin, sizeof(int) * rgb.size()));
-  CREATE_HIP(hipMemcpy(c->d_rg_begin, rgb.data(), sizeof(int) * rgb.size(), hipMemcpyHostToDevice));
 
   // LD descriptors
-  c->ldR.assign(nld, std::vector<double*>(nblk, nullptr));
+  c->ldb.assign(nld, std::vector<LdBlock>(nblk));
+  c->plan.assign(nld, LdPlan());
   for (int l = 0; l < nld; ++l) {
     BlkDesc* d = nullptr;
     CREATE_HIP(hipMalloc(&d, sizeof(BlkDesc) * nblk));
@@ -525,8 +709,9 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   take(c->RX0, 2 * K);
   take(c->S, 5 * MAXC);
 
-  const size_t part_n = std::max<size_t>((size_t)c->nch * 32, (size_t)c->nrg * MAXC);
+  const size_t part_n = (size_t)c->nch * 32;
   CREATE_HIP(hipMalloc(&c->d_part, sizeof(double) * part_n));
+  c->part_cap = part_n;
   c->nbmax = nblk;
   CREATE_HIP(hipMalloc(&c->d_bsum, sizeof(double) * (size_t)nblk * 32));
   CREATE_HIP(hipMalloc(&c->d_counts, sizeof(int)));
@@ -547,15 +732,15 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   (void)hipSetDevice(c->dev);
   if (c->st) (void)hipStreamSynchronize(c->st);
   if (c->comm) (void)ncclCommDestroy(c->comm);
-  for (auto& v : c->ldR)
-    for (double* p : v)
-      if (p) (void)hipFree(p);
+  for (auto& v : c->ldb)
+    for (LdBlock& lb : v) free_block(lb);
+  for (LdPlan& pl : c->plan) free_plan(pl);
+  if (c->d_rowpart) (void)hipFree(c->d_rowpart);
+  if (c->d_colpart) (void)hipFree(c->d_colpart);
   for (BlkDesc* d : c->d_blks) (void)hipFree(d);
   (void)hipFree(c->d_ch);
   (void)hipFree(c->d_ch_doff);
   (void)hipFree(c->d_ch_begin);
-  (void)hipFree(c->d_rg);
-  (void)hipFree(c->d_rg_begin);
   (void)hipFree(c->pool);
   (void)hipFree(c->d_part);
   (void)hipFree(c->d_bsum);
@@ -622,14 +807,43 @@ extern "C" int sgv_comm_init(sgv_ctx* c, int nranks, int rank, const char* id,
 // ---------------------------------------------------------------------------
 // inputs
 // ---------------------------------------------------------------------------
+// exact symmetry test (tiled for cache locality)
+static bool host_symmetric(const double* A, int64_t n, int64_t ld) {
+  const int64_t T = 64;
+  for (int64_t i0 = 0; i0 < n; i0 += T)
+    for (int64_t j0 = i0; j0 < n; j0 += T)
+      for (int64_t i = i0; i < std::min(n, i0 + T); ++i)
+        for (int64_t j = std::max(j0, i + 1); j < std::min(n, j0 + T); ++j)
+          if (!(A[i * ld + j] == A[j * ld + i])) return false;
+  return true;
+}
+
+extern "C" int sgv_set_ld_packing(sgv_ctx* c, int mode) {
+  ENTER(c);
+  if (mode != 0 && mode != 1) return fail(c, SGV_ERR_ARG, "packing mode %d", mode);
+  c->packing = mode;
+  return SGV_OK;
+}
+
 extern "C" int sgv_set_ld_block(sgv_ctx* c, int ld, int b, const double* host, int64_t ld_host) {
   ENTER(c);
   if (ld < 0 || ld >= c->nld || b < 0 || b >= c->nblk || !host || ld_host < c->bn[b])
     return fail(c, SGV_ERR_ARG, "sgv_set_ld_block: bad arguments (ld=%d b=%d)", ld, b);
-  CHK(ld_ensure(c, ld, b));
   const int64_t n = c->bn[b];
-  HIPCHK(hipMemcpy2D(c->ldR[ld][b], sizeof(double) * c->lda[b], host, sizeof(double) * ld_host,
-                     sizeof(double) * n, n, hipMemcpyHostToDevice));
+  const int fmt = (c->packing && host_symmetric(host, n, ld_host)) ? 1 : 0;
+  CHK(ld_alloc(c, ld, b, fmt));
+  const LdBlock& lb = c->ldb[ld][b];
+  if (fmt == 0) {
+    HIPCHK(hipMemcpy2D(lb.ptr, sizeof(double) * c->lda[b], host, sizeof(double) * ld_host,
+                       sizeof(double) * n, n, hipMemcpyHostToDevice));
+  } else {
+    for (size_t g = 0; g < lb.poff.size(); ++g) {
+      const int64_t r0 = (int64_t)g * SYM_H, H = std::min<int64_t>(SYM_H, n - r0);
+      HIPCHK(hipMemcpy2D(lb.ptr + lb.poff[g], sizeof(double) * lb.pw[g], host + r0 * ld_host + r0,
+                         sizeof(double) * ld_host, sizeof(double) * (n - r0), H,
+                         hipMemcpyHostToDevice));
+    }
+  }
   std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), 0);
   return SGV_OK;
 }
@@ -640,9 +854,31 @@ extern "C" int sgv_get_ld_block(sgv_ctx* c, int ld, int b, double* host, int64_t
     return fail(c, SGV_ERR_ARG, "sgv_get_ld_block: bad arguments (ld=%d b=%d)", ld, b);
   CHK(ld_ready(c, ld));
   const int64_t n = c->bn[b];
+  const LdBlock& lb = c->ldb[ld][b];
   CHK(stream_wait(c));
-  HIPCHK(hipMemcpy2D(host, sizeof(double) * ld_host, c->ldR[ld][b], sizeof(double) * c->lda[b],
-                     sizeof(double) * n, n, hipMemcpyDeviceToHost));
+  if (lb.fmt == 0) {
+    HIPCHK(hipMemcpy2D(host, sizeof(double) * ld_host, lb.ptr, sizeof(double) * c->lda[b],
+                       sizeof(double) * n, n, hipMemcpyDeviceToHost));
+    return SGV_OK;
+  }
+  for (size_t g = 0; g < lb.poff.size(); ++g) {
+    const int64_t r0 = (int64_t)g * SYM_H, H = std::min<int64_t>(SYM_H, n - r0);
+    HIPCHK(hipMemcpy2D(host + r0 * ld_host + r0, sizeof(double) * ld_host, lb.ptr + lb.poff[g],
+                       sizeof(double) * lb.pw[g], sizeof(double) * (n - r0), H,
+                       hipMemcpyDeviceToHost));
+  }
+  for (int64_t i = 0; i < n; ++i) {          // mirror the part left of each panel
+    const int64_t r0 = (i / SYM_H) * SYM_H;
+    for (int64_t j = 0; j < r0; ++j) host[i * ld_host + j] = host[j * ld_host + i];
+  }
+  return SGV_OK;
+}
+
+extern "C" int sgv_ld_block_format(sgv_ctx* c, int ld, int b, int* fmt_out) {
+  ENTER(c);
+  if (ld < 0 || ld >= c->nld || b < 0 || b >= c->nblk || !fmt_out)
+    return fail(c, SGV_ERR_ARG, "sgv_ld_block_format: bad arguments");
+  *fmt_out = c->ldb[ld][b].ptr ? c->ldb[ld][b].fmt : -1;
   return SGV_OK;
 }
 
@@ -729,9 +965,11 @@ extern "C" int sgv_synth_ld_g(sgv_ctx* c, int ld, uint64_t seed, int64_t marker0
     const int64_t gm0 = marker0 + c->boff[b];
     HIPCHK(launch_geno_stats(seed, gm0, n, Nsamp, sb.mean, sb.sd, c->st));
     if (ld >= 0) {
-      CHK(ld_ensure(c, ld, b));
+      CHK(ld_alloc(c, ld, b, c->packing));    // R = G G^T is exactly symmetric
+      const LdBlock& lb = c->ldb[ld][b];
       HIPCHK(launch_geno_G(seed, gm0, n, Nsamp, ldg, sb.mean, sb.sd, sb.G, c->st));
-      HIPCHK(launch_syrk_nt(sb.G, n, Nsamp, ldg, c->ldR[ld][b], c->lda[b], c->st));
+      HIPCHK(launch_syrk_nt(sb.G, n, Nsamp, ldg, lb.ptr, c->lda[b], lb.fmt, lb.d_poff, lb.d_pw,
+                            c->st));
     }
     HIPCHK(launch_g_accum(seed, gm0, n, Nsamp, sb.mean, sb.sd, sb.vec + c->boff[b], sb.g, c->st));
     CHK(ensure_hstage(c, sizeof(double) * Nsamp));
@@ -1015,7 +1253,7 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
       CHK(ld_pass(c, ld, nc, pa));
       ++passes;
       double gt[MAXC];
-      CHK(reduce_dev(c, nc, c->d_rg_begin, map, c->d_tot));
+      CHK(reduce_dev(c, nc, ld_parts(c, ld), map, c->d_tot));
       HIPCHK(hipMemcpyAsync(c->h_tot, c->d_tot, sizeof(double) * ncol, hipMemcpyDeviceToHost,
                             c->st));
       CHK(stream_wait(c));
@@ -1148,22 +1386,20 @@ extern "C" int sgv_cg_solve(sgv_ctx* c, int ld, int ncol, const double* c1, cons
   return SGV_OK;
 }
 
-extern "C" int sgv_timers(sgv_ctx* c, double* t4, int reset) {
+extern "C" int sgv_timers(sgv_ctx* c, double* t6, int reset) {
   ENTER(c);
   CHK(stream_wait(c));
   resolve_timers(c);
-  if (t4) {
-    double bytes = 0.0;
-    for (int b = 0; b < c->nblk; ++b) bytes += (double)c->bn[b] * (double)c->bn[b] * 8.0;
-    t4[0] = c->ld_ms;
-    t4[1] = c->ld_launches;
-    t4[2] = bytes;
-    t4[3] = c->rhs_bytes;
+  if (t6) {
+    t6[0] = c->ld_ms;
+    t6[1] = c->ld_launches;
+    t6[2] = c->ld_bytes;
+    t6[3] = c->rhs_bytes;
+    t6[4] = c->dense_bytes;
+    t6[5] = c->aux_bytes;
   }
   if (reset) {
-    c->ld_ms = 0.0;
-    c->ld_launches = 0.0;
-    c->rhs_bytes = 0.0;
+    c->ld_ms = c->ld_launches = c->rhs_bytes = c->ld_bytes = c->dense_bytes = c->aux_bytes = 0.0;
   }
   return SGV_OK;
 }

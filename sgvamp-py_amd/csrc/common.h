@@ -35,11 +35,46 @@ struct ChunkDesc {
   int32_t blk;
 };
 
-// Row group of the LD pass: 4 waves x RW rows of block `blk` from row0.
+// Row group of the dense LD pass: 4 waves x 8 rows of block `blk` from row0;
+// its partial sums go to partial slot `part`.
 struct RowGroup {
   int32_t blk;
   int32_t row0;
+  int32_t part;
+  int32_t pad_;
 };
+
+// ---- packed symmetric LD blocks (sym_pass.hip) ----------------------------
+constexpr int SYM_H = 256;   // rows per panel
+// one (panel, column chunk) work item of k_sym_pass
+struct SymItem {
+  const double* P;   // panel base: element (r0, r0)
+  int64_t w;         // panel row stride (doubles)
+  int64_t voff;      // block's offset in the padded vector layout
+  int32_t r0, H;     // panel first row (block-relative), rows
+  int32_t c0, nc;    // chunk first column (block-relative), columns
+  int32_t item;      // rowpart/colpart slot
+  int32_t diag_end;  // r0 + H: columns >= diag_end also feed the transpose sums
+};
+// one panel of k_sym_finalize
+struct SymPanel {
+  int64_t voff;
+  int32_t r0, H;
+  int32_t item_begin, item_end;  // this panel's chunk items (in chunk order)
+  int32_t g;                     // panel index inside its block
+  int32_t blk_panel0;            // index (in the panel table) of the block's first panel
+  int32_t part;                  // partial slot
+  int32_t pad_;
+};
+
+// element (i, j) of a packed block is stored iff j >= 256 * floor(i / 256)
+__device__ __forceinline__ double* sym_addr(double* base, const int64_t* poff, const int64_t* pw,
+                                            int i, int j) {
+  const int g = i / SYM_H;
+  const int r0 = g * SYM_H;
+  if (j < r0) return nullptr;
+  return base + poff[g] + (int64_t)(i - r0) * pw[g] + (j - r0);
+}
 
 // Columns of one LD pass: out[c] = c1[c] * (R in[c]) + c2[c] * in[c];
 // partial[c] = sum_rows dot[c] * out[c] (dot[c] may be null).
@@ -64,6 +99,40 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// Wave-reduce P values at once (P a power of two <= 64) by halving: each step
+// a lane keeps one half of its values and adds its partner's copy of that half
+// (log2 P steps, P-1 shuffles in all, instead of 6 P for P butterflies), then
+// butterflies over the remaining lane bits.  Lane l ends with the total of
+// value index (l >> (6 - log2 P)) & (P - 1); fixed order, deterministic.
+template <int P>
+__device__ __forceinline__ double wave_reduce_many(double (&v)[P]) {
+  constexpr int LOGP = (P >= 64) ? 6 : (P >= 32) ? 5 : (P >= 16) ? 4 : (P >= 8) ? 3
+                     : (P >= 4) ? 2 : (P >= 2) ? 1 : 0;
+  static_assert((1 << LOGP) == P, "P must be a power of two <= 64");
+  const int lane = threadIdx.x & (WAVE - 1);
+#pragma unroll
+  for (int step = 0; step < LOGP; ++step) {
+    const int o = 32 >> step;
+    const int h = P >> (step + 1);
+    const bool up = (lane & o) != 0;
+#pragma unroll
+    for (int k = 0; k < h; ++k) {
+      const double send = up ? v[k] : v[k + h];
+      const double keep = up ? v[k + h] : v[k];
+      v[k] = keep + __shfl_xor(send, o, WAVE);
+    }
+  }
+#pragma unroll
+  for (int o = 32 >> LOGP; o > 0; o >>= 1) v[0] += __shfl_xor(v[0], o, WAVE);
+  return v[0];
+}
+
+template <int N>
+struct Pow2Ceil {
+  static constexpr int value = N <= 1 ? 1 : N <= 2 ? 2 : N <= 4 ? 4 : N <= 8 ? 8 : N <= 16 ? 16
+                             : N <= 32 ? 32 : 64;
+};
+
 // Sum NV per-thread values over a 256-thread workgroup and store NV results
 // at out[0..NV) (fixed order: wave butterfly, then waves 0..3 in order).
 template <int NV>
@@ -84,10 +153,17 @@ __device__ __forceinline__ void block_reduce_store(double (&v)[NV], double* __re
 }
 
 // ---- launchers (defined in the .hip files) ------------------------------
-// LD pass: one workgroup per row group; partials[g * nc + c].
+// LD pass: one workgroup per row group; partials[rg.part * nc + c].
 hipError_t launch_ld_pass(int nc, const BlkDesc* d_blks, const RowGroup* d_rg, int nrg,
                           const PassArgs& pa, double* d_partials, hipStream_t st);
 int ld_pass_rows_per_group();
+// symmetric pass over packed blocks, then per-panel finalize (partials[panel.part * nc + c])
+// chunk-width class cls: CW = 1024 >> cls columns per work item
+hipError_t launch_sym_pass(int nc, int cls, const SymItem* d_items, int nitems,
+                           const PassArgs& pa, double* rowpart, double* colpart, hipStream_t st);
+hipError_t launch_sym_finalize(int nc, int cls, const SymPanel* d_panels, int npanels,
+                               const PassArgs& pa, const double* rowpart, const double* colpart,
+                               double* partials, hipStream_t st);
 
 // Reductions: partials[part * nv + v] with parts of local block b in
 // [begin[b], begin[b+1]) -> bsum[b * nv + v] (fixed order), then
@@ -233,8 +309,9 @@ hipError_t launch_geno_stats(uint64_t seed, int64_t gmarker0, int n, int nsamp, 
 hipError_t launch_geno_G(uint64_t seed, int64_t gmarker0, int n, int nsamp, int ldg,
                          const double* d_mean, const double* d_std, double* d_G,
                          hipStream_t st);
+// R = G G^T; packed != 0: write the packed symmetric layout (poff/pw per panel)
 hipError_t launch_syrk_nt(const double* d_G, int n, int nsamp, int ldg, double* d_R, int64_t lda,
-                          hipStream_t st);
+                          int packed, const int64_t* d_poff, const int64_t* d_pw, hipStream_t st);
 hipError_t launch_g_accum(uint64_t seed, int64_t gmarker0, int n, int nsamp, const double* d_mean,
                           const double* d_std, const double* d_beta, double* d_g, hipStream_t st);
 hipError_t launch_row_dot(const double* d_G, int n, int nsamp, int ldg, const double* d_y,

@@ -33,7 +33,7 @@ __global__ __launch_bounds__(256) void k_ld_pass(const BlkDesc* __restrict__ blk
   const RowGroup rg = rgs[blockIdx.x];
   const BlkDesc bd = blks[rg.blk];
   const int lane = threadIdx.x & (WAVE - 1);
-  const int wid = threadIdx.x / WAVE;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // provably wave-uniform
   const int64_t n = bd.n;
   const int64_t nfull = n & ~(int64_t)127;
 
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void k_ld_pass(const BlkDesc* __restrict__ blk
     for (int w = 0; w < 4; ++w)
 #pragma unroll
       for (int r = 0; r < LD_RW; ++r) s += red[w][r * NC + c];
-    partials[(int64_t)blockIdx.x * NC + c] = s;
+    partials[(int64_t)rg.part * NC + c] = s;
   }
 }
 

@@ -1,0 +1,206 @@
+// Symmetric (packed upper-triangle) LD pass: Y = R_b P reading each stored
+// element of a symmetric LD block once -- about half the bytes of the dense
+// pass (ld_pass.hip).  Same fused epilogue and partial dots.
+//
+// Packed layout of an n x n block: panels of SYM_H = 256 rows; panel g
+// (rows r0 = 256 g .. r0 + H - 1) stores columns r0 .. n-1 (its 256 x 256
+// diagonal block in full, everything right of it), row-major with row stride
+// w_g = round_up(n - r0, 128) doubles (rows 1 KiB aligned).
+//
+// k_sym_pass: one workgroup per (panel, chunk of NSEG*128 columns).  Every
+// element R_ij read feeds the row sum y_i += R_ij p_j and, right of the
+// diagonal block (j >= r0 + H), the transpose contribution y_j += R_ij p_i.
+// Row sums are written per (item, row); column sums per (item, column), each
+// combined over the 4 waves in a fixed order through LDS.
+// k_sym_finalize: one workgroup per panel; row i sums its panel's row parts
+// (chunk order) and the column parts of every earlier panel of the block
+// (panel order), then applies out = c1*y + c2*in and the partial dot.
+// All orders are fixed: bitwise reproducible, no atomics.
+#include "common.h"
+
+namespace sgv {
+
+template <int NC, int RWI, int NSEG>
+__global__ __launch_bounds__(256) void k_sym_pass(const SymItem* __restrict__ items, PassArgs pa,
+                                                  double* __restrict__ rowpart,
+                                                  double* __restrict__ colpart) {
+  constexpr int CW = NSEG * 128;
+  static_assert(RWI * NC <= 16, "row results per sub-sweep");
+  // per-wave column partials: lane l owns columns 2l, 2l+1 of every segment,
+  // so read-modify-writes are private; waves are summed in order at the end
+  __shared__ d2 cbw[4][NC][CW / 2];
+
+  const SymItem it = items[blockIdx.x];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // provably wave-uniform
+  const double* pp[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) pp[c] = pa.in[c] + it.voff;
+  const bool has_cols = it.c0 + it.nc > it.diag_end;   // uniform
+  if (has_cols) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      for (int s = 0; s < NSEG; ++s) cbw[wid][c][s * 64 + lane] = d2{0.0, 0.0};
+  }
+
+  constexpr int NSUB = SYM_H / (4 * RWI);
+#pragma unroll 1
+  for (int sub = 0; sub < NSUB; ++sub) {
+    const int rbase = sub * 4 * RWI + wid * RWI;   // panel-relative first row of this wave
+    if (rbase >= it.H) break;                      // wave-uniform
+    const double* rp[RWI];
+    double prow[RWI][NC];
+#pragma unroll
+    for (int r = 0; r < RWI; ++r) {
+      const int rr = rbase + r;
+      const bool ok = rr < it.H;
+      rp[r] = it.P + (int64_t)(ok ? rr : it.H - 1) * it.w + (it.c0 - it.r0);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) prow[r][c] = ok ? pp[c][it.r0 + rr] : 0.0;
+    }
+    double racc[RWI][NC];
+#pragma unroll
+    for (int r = 0; r < RWI; ++r)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) racc[r][c] = 0.0;
+
+#pragma unroll 2
+    for (int s = 0; s < NSEG; ++s) {
+      const int jl = s * 128 + 2 * lane;            // chunk-relative column
+      const bool valid = jl < it.nc;
+      d2 rv[RWI];
+      d2 pv[NC];
+#pragma unroll
+      for (int r = 0; r < RWI; ++r)
+        rv[r] = valid ? __builtin_nontemporal_load((const d2*)(rp[r] + jl)) : d2{0.0, 0.0};
+#pragma unroll
+      for (int c = 0; c < NC; ++c) pv[c] = valid ? *(const d2*)(pp[c] + it.c0 + jl) : d2{0.0, 0.0};
+#pragma unroll
+      for (int r = 0; r < RWI; ++r)
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          racc[r][c] = __builtin_fma(rv[r].x, pv[c].x, racc[r][c]);
+          racc[r][c] = __builtin_fma(rv[r].y, pv[c].y, racc[r][c]);
+        }
+      if (it.c0 + s * 128 >= it.diag_end) {         // wave-uniform: right of the diagonal block
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          d2 cv = cbw[wid][c][s * 64 + lane];
+#pragma unroll
+          for (int r = 0; r < RWI; ++r) {
+            cv.x = __builtin_fma(rv[r].x, prow[r][c], cv.x);
+            cv.y = __builtin_fma(rv[r].y, prow[r][c], cv.y);
+          }
+          cbw[wid][c][s * 64 + lane] = cv;
+        }
+      }
+    }
+    // all RWI x NC row sums at once (halving reduction)
+    constexpr int P = Pow2Ceil<RWI * NC>::value;
+    constexpr int SH = (P >= 64) ? 0 : (P >= 32) ? 1 : (P >= 16) ? 2 : (P >= 8) ? 3
+                     : (P >= 4) ? 4 : (P >= 2) ? 5 : 6;
+    double v[P];
+#pragma unroll
+    for (int k = 0; k < P; ++k) v[k] = (k < RWI * NC) ? racc[k / NC][k % NC] : 0.0;
+    const double y = wave_reduce_many<P>(v);
+    const int idx = (lane >> SH) & (P - 1);
+    const int rr = idx / NC, cc = idx % NC;
+    if ((lane & ((1 << SH) - 1)) == 0 && idx < RWI * NC && rbase + rr < it.H)
+      rowpart[((int64_t)it.item * SYM_H + rbase + rr) * NC + cc] = y;
+  }
+
+  // column parts: waves 0..3 in order
+  if (has_cols) {
+    __syncthreads();
+    double* out = colpart + (int64_t)it.item * NC * CW;
+    for (int t = threadIdx.x; t < NC * CW / 2; t += 256) {
+      const int c = t / (CW / 2), q = t % (CW / 2);
+      const int jl = 2 * q;
+      const d2 a = cbw[0][c][q], b = cbw[1][c][q], e = cbw[2][c][q], f = cbw[3][c][q];
+      const double s0 = ((a.x + b.x) + e.x) + f.x;
+      const double s1 = ((a.y + b.y) + e.y) + f.y;
+      if (jl < it.nc && it.c0 + jl >= it.diag_end) out[c * CW + jl] = s0;
+      if (jl + 1 < it.nc && it.c0 + jl + 1 >= it.diag_end) out[c * CW + jl + 1] = s1;
+    }
+  }
+}
+
+// one workgroup per panel; thread t = panel row r0 + t
+__global__ __launch_bounds__(256) void k_sym_finalize(const SymPanel* __restrict__ panels,
+                                                      int ncol, int cw, PassArgs pa,
+                                                      const double* __restrict__ rowpart,
+                                                      const double* __restrict__ colpart,
+                                                      double* __restrict__ partials) {
+  const SymPanel pn = panels[blockIdx.x];
+  const int t = threadIdx.x;
+  double acc[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) acc[c] = 0.0;
+  if (t < pn.H) {
+    const int i = pn.r0 + t;  // block-relative row
+    double y[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) y[c] = 0.0;
+    // this panel's row parts, chunk order
+    for (int itm = pn.item_begin; itm < pn.item_end; ++itm) {
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+        if (c < ncol) y[c] += rowpart[((int64_t)itm * SYM_H + t) * ncol + c];
+    }
+    // column parts of the earlier panels of this block, panel order
+    for (int g = pn.blk_panel0; g < pn.blk_panel0 + pn.g; ++g) {
+      const SymPanel q = panels[g];
+      const int ch = (i - q.r0) / cw;
+      const int itm = q.item_begin + ch;
+      const int jl = i - q.r0 - ch * cw;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+        if (c < ncol) y[c] += colpart[((int64_t)itm * ncol + c) * cw + jl];
+    }
+    const int64_t idx = pn.voff + i;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      if (c < ncol) {
+        const double o = pa.c1[c] * y[c] + pa.c2[c] * pa.in[c][idx];
+        pa.out[c][idx] = o;
+        if (pa.dot[c]) acc[c] = pa.dot[c][idx] * o;
+      }
+  }
+  block_reduce_store<MAXC>(acc, partials + (int64_t)pn.part * ncol, ncol);
+}
+
+template <int NC, int NSEG>
+static hipError_t launch_sym_nc(const SymItem* d_items, int nitems, const PassArgs& pa,
+                                double* rowpart, double* colpart, hipStream_t st) {
+  constexpr int RWI = (NC <= 2) ? 8 : (NC <= 4) ? 4 : (NC <= 8) ? 2 : 1;   // RWI*NC <= 16
+  hipLaunchKernelGGL((k_sym_pass<NC, RWI, NSEG>), dim3(nitems), dim3(256), 0, st, d_items, pa,
+                     rowpart, colpart);
+  return hipGetLastError();
+}
+
+// (nc, class) -> instantiation; NSEG = 8 >> cls.  Supported classes per nc:
+// nc <= 2: 0, 1;  nc <= 4: 1, 2;  nc <= 8: 2, 3;  nc <= 16: 3.
+hipError_t launch_sym_pass(int nc, int cls, const SymItem* d_items, int nitems,
+                           const PassArgs& pa, double* rowpart, double* colpart, hipStream_t st) {
+#define SYM_CASE(N, C)                                                                       \
+  if (nc == N && cls == C)                                                                   \
+    return launch_sym_nc<N, (8 >> C)>(d_items, nitems, pa, rowpart, colpart, st);
+  SYM_CASE(1, 0) SYM_CASE(1, 1) SYM_CASE(2, 0) SYM_CASE(2, 1)
+  SYM_CASE(3, 1) SYM_CASE(3, 2) SYM_CASE(4, 1) SYM_CASE(4, 2)
+  SYM_CASE(5, 2) SYM_CASE(5, 3) SYM_CASE(6, 2) SYM_CASE(6, 3) SYM_CASE(7, 2) SYM_CASE(7, 3)
+  SYM_CASE(8, 2) SYM_CASE(8, 3)
+  SYM_CASE(9, 3) SYM_CASE(10, 3) SYM_CASE(11, 3) SYM_CASE(12, 3) SYM_CASE(13, 3) SYM_CASE(14, 3)
+  SYM_CASE(15, 3) SYM_CASE(16, 3)
+#undef SYM_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_sym_finalize(int nc, int cls, const SymPanel* d_panels, int npanels,
+                               const PassArgs& pa, const double* rowpart, const double* colpart,
+                               double* partials, hipStream_t st) {
+  hipLaunchKernelGGL(k_sym_finalize, dim3(npanels), dim3(256), 0, st, d_panels, nc, 1024 >> cls,
+                     pa, rowpart, colpart, partials);
+  return hipGetLastError();
+}
+
+}  // namespace sgv

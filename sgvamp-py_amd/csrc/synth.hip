@@ -88,7 +88,9 @@ hipError_t launch_geno_G(uint64_t seed, int64_t gm0, int n, int nsamp, int ldg,
 // R = G G^T (n x n, symmetric; upper tiles computed, mirrored).  64x64 tiles,
 // 256 threads x (4 x 4) outputs, K-steps of 16 staged through LDS.
 __global__ __launch_bounds__(256) void k_syrk_nt(const double* __restrict__ G, int n, int kpad,
-                                                 int ldg, double* __restrict__ R, int64_t lda) {
+                                                 int ldg, double* __restrict__ R, int64_t lda,
+                                                 int packed, const int64_t* __restrict__ poff,
+                                                 const int64_t* __restrict__ pw) {
   const int tj = blockIdx.x, ti = blockIdx.y;
   if (ti > tj) return;
   const int i0 = ti * 64, j0 = tj * 64;
@@ -129,17 +131,25 @@ __global__ __launch_bounds__(256) void k_syrk_nt(const double* __restrict__ G, i
     for (int b = 0; b < 4; ++b) {
       const int i = i0 + ty + 16 * a, j = j0 + tx + 16 * b;
       if (i < n && j < n) {
-        R[(int64_t)i * lda + j] = acc[a][b];
-        R[(int64_t)j * lda + i] = acc[a][b];
+        if (packed) {
+          double* p = sym_addr(R, poff, pw, i, j);
+          if (p) *p = acc[a][b];
+          p = sym_addr(R, poff, pw, j, i);
+          if (p) *p = acc[a][b];
+        } else {
+          R[(int64_t)i * lda + j] = acc[a][b];
+          R[(int64_t)j * lda + i] = acc[a][b];
+        }
       }
     }
 }
 
 hipError_t launch_syrk_nt(const double* d_G, int n, int nsamp, int ldg, double* d_R, int64_t lda,
-                          hipStream_t st) {
+                          int packed, const int64_t* d_poff, const int64_t* d_pw, hipStream_t st) {
   const int nt = (n + 63) / 64;
   const int kpad = (nsamp + 15) / 16 * 16;  // <= ldg, zero padded
-  hipLaunchKernelGGL(k_syrk_nt, dim3(nt, nt), dim3(256), 0, st, d_G, n, kpad, ldg, d_R, lda);
+  hipLaunchKernelGGL(k_syrk_nt, dim3(nt, nt), dim3(256), 0, st, d_G, n, kpad, ldg, d_R, lda,
+                     packed, d_poff, d_pw);
   return hipGetLastError();
 }
 

@@ -156,9 +156,19 @@ class Engine:
         return X, it, info
 
     def timers(self, reset=False):
-        t = np.zeros(4)
+        t = np.zeros(6)
         self.ctx.sgv_timers(hb.dptr(t), int(bool(reset)))
-        return dict(ld_ms=t[0], ld_launches=int(t[1]), ld_bytes_per_pass=t[2], rhs_bytes=t[3])
+        return dict(ld_ms=t[0], ld_launches=int(t[1]), ld_bytes=t[2], rhs_bytes=t[3],
+                    dense_bytes=t[4], aux_bytes=t[5])
+
+    def set_ld_packing(self, packed):
+        """True: symmetric blocks set/generated from now on are stored packed."""
+        self.ctx.sgv_set_ld_packing(int(bool(packed)))
+
+    def ld_block_format(self, ld, b_global):
+        f = np.zeros(1, dtype=np.int32)
+        self.ctx.sgv_ld_block_format(int(ld), b_global - self.b0, hb.iptr(f))
+        return int(f[0])
 
     def sync(self):
         self.ctx.sgv_sync()

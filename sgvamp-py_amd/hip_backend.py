@@ -35,6 +35,8 @@ _SIGS = {
     "sgv_comm_init": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _c_int_p],
     "sgv_set_ld_block": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, ctypes.c_int64],
     "sgv_get_ld_block": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, ctypes.c_int64],
+    "sgv_set_ld_packing": [_vp, ctypes.c_int],
+    "sgv_ld_block_format": [_vp, ctypes.c_int, ctypes.c_int, _c_int_p],
     "sgv_set_ridge": [_vp, ctypes.c_double],
     "sgv_set_cohort_n": [_vp, ctypes.c_int, ctypes.c_double],
     "sgv_set_vector": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p],
