@@ -54,8 +54,11 @@ def parse():
     p.add_argument("--K", type=int, default=1)
     p.add_argument("--seed", type=int, default=2025)
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    p.add_argument("--cpu-iters", type=int, default=3)
+    p.add_argument("--cpu-iters", type=int, default=30)   # ~10 s of CPU work on the box
     p.add_argument("--no-files", action="store_true", help="skip the per-iteration output files")
+    p.add_argument("--share-device", action="store_true",
+                   help="rehearsal: every rank on device 0 with the host exchange (RCCL refuses "
+                        "two ranks on one device); timings are then not a multi-GPU result")
     p.add_argument("--prior", choices=["matched", "cli"], default="matched")
     p.add_argument("--ld-format", choices=["packed", "dense"], default="packed",
                    help="LD block storage: packed symmetric panels (default) or full squares")
@@ -135,11 +138,12 @@ def main():
 
     comm = world_from_env()
     rank = comm.Get_rank()
-    device = int(os.environ.get("LOCAL_RANK", "0"))
+    device = 0 if args.share_device else int(os.environ.get("LOCAL_RANK", "0"))
     sizes = [args.block_size] * args.blocks
     K = args.K
     t_setup = time.perf_counter()
-    eng = Engine(sizes, K, ld_of=[0] * K, comm=comm, device=device)
+    eng = Engine(sizes, K, ld_of=[0] * K, comm=comm, device=device,
+                 exchange="host" if args.share_device else None)
     eng.set_ld_packing(args.ld_format == "packed")
     beta, _ = make_problem(eng, comm, args)
     N_list = [args.nsamp] * K

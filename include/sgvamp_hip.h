@@ -86,6 +86,15 @@ const char* sgv_last_error(const sgv_ctx* ctx);
 int sgv_comm_unique_id(char* id_out /* 128 bytes */);
 int sgv_comm_init(sgv_ctx* ctx, int nranks, int rank, const char* id /* 128 bytes */,
                   const int* nblk_per_rank /* [nranks] */);
+/* Host-side exchange instead of RCCL (same ordered reductions, bitwise the same
+ * results): the library copies its per-block partials to host memory and calls
+ * fn(user, send, recv, count) which must all-gather `count` doubles from every
+ * rank into recv[nranks][count] in rank order and return 0.  For ranks that
+ * RCCL cannot connect (several ranks on one device, hosts without xGMI peers)
+ * and for testing the sharded path with a host communicator. */
+typedef int (*sgv_allgather_fn)(void* user, const double* send, double* recv, int64_t count);
+int sgv_comm_init_host(sgv_ctx* ctx, int nranks, int rank, const int* nblk_per_rank,
+                       sgv_allgather_fn fn, void* user);
 
 /* ---- inputs -------------------------------------------------------------- */
 

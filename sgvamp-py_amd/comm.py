@@ -1,8 +1,10 @@
-"""Host-side communicators (bootstrap, barriers, timing) -- never on the data path.
+"""Host-side communicators (bootstrap, barriers, timing).
 
 The data-path reductions of the solver run inside libsgvamp_hip.so over RCCL.
-These objects only exchange the RCCL unique id, synchronise ranks and
-combine scalars for logging/benchmarking.  They mirror the subset of the
+These objects exchange the RCCL unique id, synchronise ranks and combine
+scalars for logging/benchmarking; ``allgather_f64`` also serves as the
+library's host exchange (``sgv_comm_init_host``) when RCCL cannot connect the
+ranks (e.g. several ranks on one device).  They mirror the subset of the
 mpi4py API the reference uses (src/main.py:16-18; src/sgvamp.py:202,232-233):
 Get_rank, Get_size, bcast -- plus allgather and barrier.
 """
@@ -23,6 +25,9 @@ class SingleComm:
 
     def allgather(self, obj):
         return [obj]
+
+    def allgather_f64(self, arr):
+        return arr.copy()
 
     def barrier(self):
         pass
@@ -58,6 +63,16 @@ class TorchGlooComm:
         out = [None] * self.size
         self.dist.all_gather_object(out, obj)
         return out
+
+    def allgather_f64(self, arr):
+        """All-gather a float64 array of the same length from every rank, in rank
+        order (size * len(arr) doubles)."""
+        import torch
+
+        t = torch.from_numpy(arr)
+        out = [torch.empty_like(t) for _ in range(self.size)]
+        self.dist.all_gather(out, t)
+        return torch.cat(out).numpy()
 
     def barrier(self):
         self.dist.barrier()

@@ -111,6 +111,10 @@ struct sgv_ctx {
   size_t h_stage_bytes = 0;
   // comm
   ncclComm_t comm = nullptr;
+  sgv_allgather_fn host_ag = nullptr;   // host exchange (sgv_comm_init_host)
+  void* host_ag_user = nullptr;
+  double* h_bsum = nullptr;             // pinned [nbmax * 32] and [nranks][nbmax * 32]
+  double* h_bsum_all = nullptr;
   int nranks = 1, rank = 0;
   // solver state
   std::vector<int> xnz;        // x0.any() per CG column (2K)
@@ -209,6 +213,17 @@ static int reduce_dev(sgv_ctx* c, int nv, const int* d_begin, const Map16& map, 
   if (c->comm) {
     NCCLCHK(ncclAllGather(c->d_bsum, c->d_bsum_all, (size_t)c->nbmax * nv, ncclDouble, c->comm,
                           c->st));
+  } else if (c->host_ag) {
+    const size_t cnt = (size_t)c->nbmax * nv;
+    HIPCHK(hipMemcpyAsync(c->h_bsum, c->d_bsum, sizeof(double) * cnt, hipMemcpyDeviceToHost,
+                          c->st));
+    CHK(stream_wait(c));
+    if (c->host_ag(c->host_ag_user, c->h_bsum, c->h_bsum_all, (int64_t)cnt) != 0)
+      return fail(c, SGV_ERR_RCCL, "host all-gather callback failed");
+    HIPCHK(hipMemcpyAsync(c->d_bsum_all, c->h_bsum_all, sizeof(double) * cnt * c->nranks,
+                          hipMemcpyHostToDevice, c->st));
+  }
+  if (c->nranks > 1) {
     src = c->d_bsum_all;
     nr = c->nranks;
     nbm = c->nbmax;
@@ -732,6 +747,8 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   (void)hipSetDevice(c->dev);
   if (c->st) (void)hipStreamSynchronize(c->st);
   if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->h_bsum) (void)hipHostFree(c->h_bsum);
+  if (c->h_bsum_all) (void)hipHostFree(c->h_bsum_all);
   for (auto& v : c->ldb)
     for (LdBlock& lb : v) free_block(lb);
   for (LdPlan& pl : c->plan) free_plan(pl);
@@ -778,29 +795,57 @@ extern "C" int sgv_comm_unique_id(char* id_out) {
   return SGV_OK;
 }
 
-extern "C" int sgv_comm_init(sgv_ctx* c, int nranks, int rank, const char* id,
-                             const int* nblk_per_rank) {
-  ENTER(c);
-  if (nranks < 1 || rank < 0 || rank >= nranks || !id || !nblk_per_rank)
-    return fail(c, SGV_ERR_ARG, "bad comm arguments");
-  if (nblk_per_rank[rank] != c->nblk)
-    return fail(c, SGV_ERR_ARG, "nblk_per_rank[%d]=%d != %d", rank, nblk_per_rank[rank], c->nblk);
-  if (nranks == 1) return SGV_OK;
-  ncclUniqueId uid;
-  std::memcpy(&uid, id, sizeof uid);
-  NCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
+// buffers of the ordered cross-rank reduction (per-block partials of every rank)
+static int comm_buffers(sgv_ctx* c, int nranks, int rank, const int* nblk_per_rank) {
   c->nranks = nranks;
   c->rank = rank;
   c->nbmax = *std::max_element(nblk_per_rank, nblk_per_rank + nranks);
+  const size_t per = (size_t)c->nbmax * 32;
   HIPCHK(hipFree(c->d_bsum));
   c->d_bsum = nullptr;
-  HIPCHK(hipMalloc(&c->d_bsum, sizeof(double) * (size_t)c->nbmax * 32));
-  HIPCHK(hipMemset(c->d_bsum, 0, sizeof(double) * (size_t)c->nbmax * 32));
-  HIPCHK(hipMalloc(&c->d_bsum_all, sizeof(double) * (size_t)c->nbmax * 32 * nranks));
+  HIPCHK(hipMalloc(&c->d_bsum, sizeof(double) * per));
+  HIPCHK(hipMemset(c->d_bsum, 0, sizeof(double) * per));
+  HIPCHK(hipMalloc(&c->d_bsum_all, sizeof(double) * per * nranks));
   HIPCHK(hipFree(c->d_counts));
   c->d_counts = nullptr;
   HIPCHK(hipMalloc(&c->d_counts, sizeof(int) * nranks));
   HIPCHK(hipMemcpy(c->d_counts, nblk_per_rank, sizeof(int) * nranks, hipMemcpyHostToDevice));
+  return SGV_OK;
+}
+
+static int comm_args(sgv_ctx* c, int nranks, int rank, const int* nblk_per_rank) {
+  if (nranks < 1 || rank < 0 || rank >= nranks || !nblk_per_rank)
+    return fail(c, SGV_ERR_ARG, "bad comm arguments");
+  if (nblk_per_rank[rank] != c->nblk)
+    return fail(c, SGV_ERR_ARG, "nblk_per_rank[%d]=%d != %d", rank, nblk_per_rank[rank], c->nblk);
+  if (c->comm || c->host_ag) return fail(c, SGV_ERR_ARG, "communicator already initialised");
+  return SGV_OK;
+}
+
+extern "C" int sgv_comm_init(sgv_ctx* c, int nranks, int rank, const char* id,
+                             const int* nblk_per_rank) {
+  ENTER(c);
+  if (!id) return fail(c, SGV_ERR_ARG, "bad comm arguments");
+  CHK(comm_args(c, nranks, rank, nblk_per_rank));
+  if (nranks == 1) return SGV_OK;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof uid);
+  NCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
+  return comm_buffers(c, nranks, rank, nblk_per_rank);
+}
+
+extern "C" int sgv_comm_init_host(sgv_ctx* c, int nranks, int rank, const int* nblk_per_rank,
+                                  sgv_allgather_fn fn, void* user) {
+  ENTER(c);
+  if (!fn) return fail(c, SGV_ERR_ARG, "allgather callback is null");
+  CHK(comm_args(c, nranks, rank, nblk_per_rank));
+  if (nranks == 1) return SGV_OK;
+  CHK(comm_buffers(c, nranks, rank, nblk_per_rank));
+  const size_t per = (size_t)c->nbmax * 32;
+  HIPCHK(hipHostMalloc(&c->h_bsum, sizeof(double) * per));
+  HIPCHK(hipHostMalloc(&c->h_bsum_all, sizeof(double) * per * nranks));
+  c->host_ag = fn;
+  c->host_ag_user = user;
   return SGV_OK;
 }
 

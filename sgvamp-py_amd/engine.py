@@ -5,6 +5,9 @@ marker-length vector; every M-length reduction inside the library is ordered
 by global LD block, so the scalars it returns are identical on every rank and
 for any number of ranks.
 """
+import ctypes
+import os
+
 import numpy as np
 
 import hip_backend as hb
@@ -12,9 +15,11 @@ from partition import marker_offsets, partition_blocks
 
 
 class Engine:
-    def __init__(self, block_sizes, K, ld_of=None, comm=None, device=None):
+    def __init__(self, block_sizes, K, ld_of=None, comm=None, device=None, exchange=None):
         """block_sizes: global LD block sizes (marker order).  ld_of[k]: index of
-        the LD matrix cohort k uses (cohorts sharing an LD share LD passes)."""
+        the LD matrix cohort k uses (cohorts sharing an LD share LD passes).
+        exchange: "rccl" (default) or "host" (the communicator's allgather_f64
+        carries the per-block partials; env SGV_EXCHANGE overrides the default)."""
         from comm import SingleComm
 
         self.comm = comm or SingleComm()
@@ -39,15 +44,24 @@ class Engine:
         self.Mloc = int(offs[self.b1] - offs[self.b0])
         self.local_sizes = self.block_sizes[self.b0:self.b1]
         self.sl = slice(self.marker0, self.marker0 + self.Mloc)
-        if device is None:
-            device = self.rank if self.nranks > 1 else 0
+        if device is None:   # one process per GPU: the node-local rank (torchrun LOCAL_RANK)
+            device = int(os.environ.get("LOCAL_RANK", "0")) if self.nranks > 1 else 0
         self.ctx = hb.Context(device, self.K, self.ld_of, self.local_sizes, self.b0,
                               len(self.block_sizes), self.M)
+        self.exchange = exchange or os.environ.get("SGV_EXCHANGE", "rccl")
+        if self.exchange not in ("rccl", "host"):
+            raise ValueError("exchange must be 'rccl' or 'host', got %r" % self.exchange)
+        self._ag_cb = None
         if self.nranks > 1:
-            uid = hb.unique_id() if self.rank == 0 else None
-            uid = self.comm.bcast(uid, root=0)
             counts = np.array([r1 - r0 for r0, r1 in self.ranges], dtype=np.int32)
-            self.ctx.sgv_comm_init(self.nranks, self.rank, uid, hb.iptr(counts))
+            if self.exchange == "host":
+                self._ag_cb = hb.make_allgather(self.comm, self.nranks)
+                self.ctx.sgv_comm_init_host(self.nranks, self.rank, hb.iptr(counts),
+                                            ctypes.cast(self._ag_cb, ctypes.c_void_p), None)
+            else:
+                uid = hb.unique_id() if self.rank == 0 else None
+                uid = self.comm.bcast(uid, root=0)
+                self.ctx.sgv_comm_init(self.nranks, self.rank, uid, hb.iptr(counts))
 
     # ---- inputs ----------------------------------------------------------
     def set_ld_block(self, ld, b_global, block):

@@ -33,6 +33,7 @@ _SIGS = {
     "sgv_last_error": [_vp],
     "sgv_comm_unique_id": [ctypes.c_char_p],
     "sgv_comm_init": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_char_p, _c_int_p],
+    "sgv_comm_init_host": [_vp, ctypes.c_int, ctypes.c_int, _c_int_p, ctypes.c_void_p, _vp],
     "sgv_set_ld_block": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, ctypes.c_int64],
     "sgv_get_ld_block": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, ctypes.c_int64],
     "sgv_set_ld_packing": [_vp, ctypes.c_int],
@@ -142,6 +143,31 @@ class Context:
             self.check(fn(self.h, *args), name)
 
         return call
+
+
+# int fn(void* user, const double* send, double* recv, int64_t count)
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
+                                ctypes.POINTER(ctypes.c_double), ctypes.c_int64)
+
+
+def make_allgather(comm, nranks):
+    """Wrap comm.allgather_f64 as the library's host all-gather callback.  Keep
+    the returned object alive for as long as the context uses it."""
+    import numpy as np
+
+    def cb(_user, send, recv, count):
+        try:
+            a = np.ctypeslib.as_array(send, shape=(count,)).copy()
+            out = np.ctypeslib.as_array(recv, shape=(count * nranks,))
+            out[:] = comm.allgather_f64(a)
+            return 0
+        except Exception:  # noqa: BLE001 -- reported as a nonzero status by the library
+            import traceback
+
+            traceback.print_exc()
+            return 1
+
+    return ALLGATHER_FN(cb)
 
 
 def unique_id():

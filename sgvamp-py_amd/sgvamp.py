@@ -111,7 +111,8 @@ def common_partition(size_lists):
 
 class VAMP:
     def __init__(self, N, Nt, M, K, rho, gamw, gam1, a, prior_vars, prior_probs, out_dir,
-                 out_name, comm=None, seed=None, device=None, write_files=True, ld_packing=True):
+                 out_name, comm=None, seed=None, device=None, write_files=True, ld_packing=True,
+                 exchange=None):
         # src/sgvamp.py:15-31
         self.eps = 1e-32
         self.K = int(K)
@@ -141,6 +142,7 @@ class VAMP:
         self.rank = self.comm.Get_rank()
         self.seed = seed
         self.device = device
+        self.exchange = exchange
         self.write_files = write_files
         self.ld_packing = ld_packing   # packed symmetric LD storage for symmetric blocks
         self.gam = None
@@ -212,7 +214,8 @@ class VAMP:
         if sum(sizes) != self.M:
             raise ValueError("LD matrices cover %d markers, M = %d" % (sum(sizes), self.M))
         uniq = [L.regroup(sizes) for L in uniq]
-        self.engine = eng = Engine(sizes, K, ld_of, comm=self.comm, device=self.device)
+        self.engine = eng = Engine(sizes, K, ld_of, comm=self.comm, device=self.device,
+                                          exchange=self.exchange)
         eng.set_ld_packing(self.ld_packing)
         eng.set_ridge(s_vals.pop())
         for l, L in enumerate(uniq):
