@@ -102,6 +102,10 @@ int sgv_comm_init_host(sgv_ctx* ctx, int nranks, int rank, const int* nblk_per_r
  * Replaces the R loaders src/main.py:199-202 (dense .npy / CSR .npz blocks). */
 int sgv_set_ld_block(sgv_ctx* ctx, int ld, int blk_local, const double* rowmajor,
                      int64_t ld_host);
+/* Packed passes with at least nc_min right-hand sides run on the f64 matrix
+ * cores (v_mfma_f64_16x16x4f64); fewer run on the VALU.  0 = never.  Default 3
+ * (env SGV_MFMA_MIN).  Results agree to rounding, not bitwise, across the two. */
+int sgv_set_mfma_min(sgv_ctx* ctx, int nc_min);
 /* Storage of LD blocks set or generated from now on: mode 1 (default) stores a
  * block that is exactly symmetric as packed upper-triangle panels (about half
  * the bytes per pass: the LD matrix of src/main.py:199-265 is symmetric by

@@ -59,6 +59,16 @@ static int sym_class(int nc) {
   const int base = nc <= 2 ? 0 : nc <= 4 ? 1 : nc <= 8 ? 2 : 3;
   return std::min(3, base + (nc <= 8 ? narrow : 0));
 }
+// default number of right-hand sides from which packed passes run on the f64
+// matrix cores (sym_mfma.hip, class-1 items); env SGV_MFMA_MIN overrides,
+// 0 disables; per context: sgv_set_mfma_min
+static int mfma_min_default() {
+  static const int v = [] {
+    const char* e = std::getenv("SGV_MFMA_MIN");
+    return e ? std::atoi(e) : 3;
+  }();
+  return v;
+}
 static int sym_class_nc(int cls) { return std::min(16, 2 << (cls + 1)); }   // widest NC using cls
 
 struct sgv_ctx {
@@ -83,6 +93,9 @@ struct sgv_ctx {
   double* d_rowpart = nullptr;   // k_sym_pass row partials
   double* d_colpart = nullptr;   // k_sym_pass column partials
   size_t rowpart_cap = 0, colpart_cap = 0, part_cap = 0;
+  int mfma_min = 3;              // see mfma_min_default
+  double* d_pk = nullptr;        // RHS interleaved [Mpad][16] for the MFMA pass
+  size_t pk_cap = 0;
   // chunk / row-group layouts
   int nch = 0;
   ChunkDesc* d_ch = nullptr;
@@ -449,6 +462,11 @@ static int ensure_plan(sgv_ctx* c, int ld) {
     rowpart_need = std::max(rowpart_need, items.size() * SYM_H * ncmax);
     colpart_need = std::max(colpart_need, items.size() * ncmax * (size_t)cw);
   }
+  if (pl.npanels) {   // the MFMA pass: class-1 items with up to 16 columns
+    rowpart_need = std::max(rowpart_need, (size_t)pl.nitems[1] * SYM_H * MAXC);
+    colpart_need = std::max(colpart_need, (size_t)pl.nitems[1] * MAXC * 512);
+    CHK(grow(c, &c->d_pk, &c->pk_cap, (size_t)c->Mpad * 16));
+  }
   CHK(grow(c, &c->d_rowpart, &c->rowpart_cap, rowpart_need));
   CHK(grow(c, &c->d_colpart, &c->colpart_cap, colpart_need));
   CHK(grow(c, &c->d_part, &c->part_cap, (size_t)nparts * MAXC));
@@ -475,13 +493,19 @@ static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa) {
   HIPCHK(hipEventRecord(e0, c->st));
   if (pl.nrg) HIPCHK(launch_ld_pass(nc, c->d_blks[ld], pl.d_rg, pl.nrg, pa, c->d_part, c->st));
   if (pl.npanels) {
-    const int cls = sym_class(nc);
-    HIPCHK(launch_sym_pass(nc, cls, pl.d_items[cls], pl.nitems[cls], pa, c->d_rowpart,
-                           c->d_colpart, c->st));
+    const bool mf = c->mfma_min > 0 && nc >= c->mfma_min;
+    const int cls = mf ? 1 : sym_class(nc);
+    if (mf)
+      HIPCHK(launch_sym_mfma(nc, pl.d_items[cls], pl.nitems[cls], pa, c->Mpad, c->d_pk,
+                             c->d_rowpart, c->d_colpart, c->st));
+    else
+      HIPCHK(launch_sym_pass(nc, cls, pl.d_items[cls], pl.nitems[cls], pa, c->d_rowpart,
+                             c->d_colpart, c->st));
     HIPCHK(launch_sym_finalize(nc, cls, pl.d_panels[cls], pl.npanels, pa, c->d_rowpart,
                                c->d_colpart, c->d_part, c->st));
     const double cw = (double)(1024 >> cls);
     c->aux_bytes += 2.0 * 8.0 * nc * (double)pl.nitems[cls] * (SYM_H + cw);
+    if (mf) c->aux_bytes += 8.0 * (double)c->Mpad * (16 + nc);   // Pk pack
   }
   HIPCHK(hipEventRecord(e1, c->st));
   c->pending.emplace_back(e0, e1);
@@ -620,6 +644,7 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
     return fail(nullptr, SGV_ERR_ARG, "device %d outside [0,%d)", device, ndev);
 
   c = new sgv_ctx();
+  c->mfma_min = mfma_min_default();
   c->dev = device;
   c->K = K;
   c->nld = nld;
@@ -754,6 +779,7 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   for (LdPlan& pl : c->plan) free_plan(pl);
   if (c->d_rowpart) (void)hipFree(c->d_rowpart);
   if (c->d_colpart) (void)hipFree(c->d_colpart);
+  if (c->d_pk) (void)hipFree(c->d_pk);
   for (BlkDesc* d : c->d_blks) (void)hipFree(d);
   (void)hipFree(c->d_ch);
   (void)hipFree(c->d_ch_doff);
@@ -861,6 +887,13 @@ static bool host_symmetric(const double* A, int64_t n, int64_t ld) {
         for (int64_t j = std::max(j0, i + 1); j < std::min(n, j0 + T); ++j)
           if (!(A[i * ld + j] == A[j * ld + i])) return false;
   return true;
+}
+
+extern "C" int sgv_set_mfma_min(sgv_ctx* c, int nc_min) {
+  ENTER(c);
+  if (nc_min < 0) return fail(c, SGV_ERR_ARG, "nc_min must be >= 0");
+  c->mfma_min = nc_min;
+  return SGV_OK;
 }
 
 extern "C" int sgv_set_ld_packing(sgv_ctx* c, int mode) {

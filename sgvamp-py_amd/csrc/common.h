@@ -16,6 +16,20 @@ constexpr int MAXL = 8;         // slab components (L - 1)
 
 typedef double d2 __attribute__((ext_vector_type(2)));
 
+// Loads through the global address space.  Pointers read out of descriptor
+// structs are generic to the compiler, which then emits FLAT loads: those
+// count against lgkmcnt as well as vmcnt, so every wait for an LDS access
+// also drains the in-flight HBM stream.  global_load keeps the counters apart.
+#define SGV_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ T ldg(const T* p) {
+  return *(const SGV_GLOBAL T*)p;
+}
+template <class T>
+__device__ __forceinline__ T ldg_nt(const T* p) {   // streaming (read-once) data
+  return __builtin_nontemporal_load((const SGV_GLOBAL T*)p);
+}
+
 // One LD block of one LD matrix: n x n dense f64, row-major, row stride lda
 // (multiple of PADV, zero padded); voff = offset of the block's first marker
 // in the padded device vector layout.
@@ -161,6 +175,9 @@ int ld_pass_rows_per_group();
 // chunk-width class cls: CW = 1024 >> cls columns per work item
 hipError_t launch_sym_pass(int nc, int cls, const SymItem* d_items, int nitems,
                            const PassArgs& pa, double* rowpart, double* colpart, hipStream_t st);
+hipError_t launch_sym_mfma(int nc, const SymItem* d_items, int nitems, const PassArgs& pa,
+                           int64_t mpad, double* d_pk, double* rowpart, double* colpart,
+                           hipStream_t st);
 hipError_t launch_sym_finalize(int nc, int cls, const SymPanel* d_panels, int npanels,
                                const PassArgs& pa, const double* rowpart, const double* colpart,
                                double* partials, hipStream_t st);

@@ -77,10 +77,10 @@ __global__ __launch_bounds__(256) void k_ld_pass(const BlkDesc* __restrict__ blk
     for (int64_t j = 2 * lane; j < nfull; j += 128) {
       d2 rv[RWI];
 #pragma unroll
-      for (int r = 0; r < RWI; ++r) rv[r] = __builtin_nontemporal_load((const d2*)(rp[r] + j));
+      for (int r = 0; r < RWI; ++r) rv[r] = ldg_nt((const d2*)(rp[r] + j));
       d2 pv[NC];
 #pragma unroll
-      for (int c = 0; c < NC; ++c) pv[c] = *(const d2*)(pp[c] + j);
+      for (int c = 0; c < NC; ++c) pv[c] = ldg((const d2*)(pp[c] + j));
 #pragma unroll
       for (int r = 0; r < RWI; ++r)
 #pragma unroll
@@ -95,10 +95,10 @@ __global__ __launch_bounds__(256) void k_ld_pass(const BlkDesc* __restrict__ blk
       if (j < n) {
         d2 rv[RWI];
 #pragma unroll
-        for (int r = 0; r < RWI; ++r) rv[r] = __builtin_nontemporal_load((const d2*)(rp[r] + j));
+        for (int r = 0; r < RWI; ++r) rv[r] = ldg_nt((const d2*)(rp[r] + j));
         d2 pv[NC];
 #pragma unroll
-        for (int c = 0; c < NC; ++c) pv[c] = *(const d2*)(pp[c] + j);
+        for (int c = 0; c < NC; ++c) pv[c] = ldg((const d2*)(pp[c] + j));
 #pragma unroll
         for (int r = 0; r < RWI; ++r)
 #pragma unroll

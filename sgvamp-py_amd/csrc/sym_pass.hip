@@ -72,9 +72,14 @@ __global__ __launch_bounds__(256) void k_sym_pass(const SymItem* __restrict__ it
       d2 pv[NC];
 #pragma unroll
       for (int r = 0; r < RWI; ++r)
-        rv[r] = valid ? __builtin_nontemporal_load((const d2*)(rp[r] + jl)) : d2{0.0, 0.0};
+        rv[r] = ldg_nt((const d2*)(rp[r] + (valid ? jl : 0)));
+      // branch-free: an invalid column loads column 0 of its row (finite) and
+      // meets a zero P; its column sums are never stored
 #pragma unroll
-      for (int c = 0; c < NC; ++c) pv[c] = valid ? *(const d2*)(pp[c] + it.c0 + jl) : d2{0.0, 0.0};
+      for (int c = 0; c < NC; ++c) {
+        const d2 v = ldg((const d2*)(pp[c] + it.c0 + (valid ? jl : 0)));
+        pv[c] = valid ? v : d2{0.0, 0.0};
+      }
 #pragma unroll
       for (int r = 0; r < RWI; ++r)
 #pragma unroll

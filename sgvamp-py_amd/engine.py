@@ -80,6 +80,10 @@ class Engine:
         self.ctx.sgv_get_ld_block(ld, b_global - self.b0, hb.dptr(out), n)
         return out
 
+    def set_mfma_min(self, nc_min):
+        """Packed LD passes with >= nc_min right-hand sides use the f64 MFMA kernel."""
+        self.ctx.sgv_set_mfma_min(int(nc_min))
+
     def set_ridge(self, s):
         self.ctx.sgv_set_ridge(float(s))
 

@@ -51,14 +51,18 @@ def rand_blocks(sizes, seed=0, nsamp=None, symmetric=True):
                                    [256, 257, 513], [1500, 2600]])
 @pytest.mark.parametrize("ncol", [1, 2, 3, 5, 8, 12, 16])
 @pytest.mark.parametrize("s", [0.0, 0.1])
-@pytest.mark.parametrize("fmt", ["packed", "dense", "nonsym"])
+@pytest.mark.parametrize("fmt", ["packed", "packed_valu", "dense", "nonsym"])
 def test_ld_matvec_vs_numpy(sizes, ncol, s, fmt):
+    """packed: f64 MFMA pass from 3 columns (sym_mfma.hip); packed_valu: VALU pass
+    for every column count; dense/nonsym: full-square storage."""
     blocks = rand_blocks(sizes, seed=len(sizes) + ncol, symmetric=fmt != "nonsym")
     eng = Engine(sizes, K=1)
-    eng.set_ld_packing(fmt == "packed")
+    eng.set_ld_packing(fmt.startswith("packed"))
+    if fmt == "packed_valu":
+        eng.set_mfma_min(0)
     for b, B in enumerate(blocks):
         eng.set_ld_block(0, b, B)
-        assert eng.ld_block_format(0, b) == (1 if fmt == "packed" else 0)
+        assert eng.ld_block_format(0, b) == (1 if fmt.startswith("packed") else 0)
     eng.set_ridge(s)
     M = sum(sizes)
     V = np.random.RandomState(ncol).normal(size=(ncol, M))
@@ -93,10 +97,17 @@ def test_ld_matvec_symmetry_and_linearity_large():
     rs = np.random.RandomState(1)
     U = rs.normal(size=(3, 25000))
     U[2] = 0.3 * U[0] - 1.7 * U[1]
-    Y = eng.ld_matvec(0, U)
+    Y = eng.ld_matvec(0, U)                 # 3 columns: the MFMA pass
     assert eng.ld_block_format(0, 0) == 1
     assert abs(U[0] @ Y[1] - U[1] @ Y[0]) <= 1e-11 * abs(U[0] @ Y[1])
     assert maxrel(Y[2], 0.3 * Y[0] - 1.7 * Y[1]) < 1e-11
+    # 16 columns on the MFMA pass vs one column at a time on the VALU pass
+    U16 = rs.normal(size=(16, 25000))
+    Y16 = eng.ld_matvec(0, U16)
+    eng.set_mfma_min(0)
+    for j in (0, 7, 15):
+        assert maxrel(Y16[j], eng.ld_matvec(0, U16[j:j + 1])[0]) < 1e-12
+    eng.set_mfma_min(3)
     # the same block stored dense gives the same products
     B = eng.get_ld_block(0, 0)
     eng.close()
@@ -192,7 +203,7 @@ def test_denoise_and_em_vs_oracle(K, nslab):
 # ---------------------------------------------------------------------------
 # full VAMP vs the reference's golden outputs
 # ---------------------------------------------------------------------------
-def run_vamp_case(c, out_dir, device=None, ld_packing=True):
+def run_vamp_case(c, out_dir, device=None, ld_packing=True, mfma_min=None):
     f = c.flags
     lds = [BlockLD(blocks, s=f["s"]) for blocks in c.ld_blocks]
     R = lds[0] if len(lds) == 1 else [lds[c.ld_of[k]] for k in range(c.K)]
@@ -200,7 +211,8 @@ def run_vamp_case(c, out_dir, device=None, ld_packing=True):
     a = np.array(c.N) / Nt
     v = VAMP(N=c.N, Nt=Nt, M=c.M, K=c.K, rho=f["rho"], gamw=f["gamw"], gam1=f["gam1"], a=a,
              prior_vars=f["prior_vars"], prior_probs=f["prior_probs"], out_dir=str(out_dir),
-             out_name=c.name, seed=f["seed"], device=device, ld_packing=ld_packing)
+             out_name=c.name, seed=f["seed"], device=device, ld_packing=ld_packing,
+             mfma_min=mfma_min)
     xh = v.infer(R, c.r, f["iterations"], x0=c.x0, cg_maxit=f["cg_maxit"],
                  em_prior_maxit=f["em_prior_maxit"], learn_gamw=f["learn_gamw"],
                  lmmse_damp=f["lmmse_damp"], prior_update=f["prior_update"],
@@ -215,11 +227,16 @@ def read_tsv(path):
     return text, np.array(rows)
 
 
-@pytest.mark.parametrize("packing", [True, False])
+@pytest.mark.parametrize("packing", [True, False, "valu"])
 @pytest.mark.parametrize("name", case_names())
 def test_vamp_matches_reference_golden(name, packing, tmp_path):
+    """packing True: packed storage (MFMA pass for K >= 2, i.e. >= 3 CG columns);
+    "valu": packed storage, VALU pass only; False: dense storage."""
     c = Case(name)
-    v, xh = run_vamp_case(c, tmp_path, ld_packing=packing)
+    if packing == "valu" and c.K == 1:
+        pytest.skip("K = 1 never reaches 3 columns: same as packing=True")
+    v, xh = run_vamp_case(c, tmp_path, ld_packing=bool(packing),
+                          mfma_min=0 if packing == "valu" else None)
     fmts = {v.engine.ld_block_format(l, b) for l in range(v.engine.nld)
             for b in range(len(v.engine.block_sizes))}
     assert fmts == {1 if packing else 0}

@@ -23,14 +23,17 @@ def main():
     ap.add_argument("--block-size", type=int, default=25000)
     ap.add_argument("--nsamp", type=int, default=2000)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--ncols", default="1,2,4,8,16")
-    ap.add_argument("--formats", default="packed,dense")
+    ap.add_argument("--ncols", default="1,2,3,4,8,12,16")
+    ap.add_argument("--formats", default="packed,packed_valu,dense",
+                    help="packed (f64 MFMA pass from 3 columns), packed_valu, dense")
     a = ap.parse_args()
     sizes = [a.block_size] * a.blocks
     M = sum(sizes)
     for fmt in a.formats.split(","):
         eng = Engine(sizes, K=1)
-        eng.set_ld_packing(fmt == "packed")
+        eng.set_ld_packing(fmt.startswith("packed"))
+        if fmt == "packed_valu":
+            eng.set_mfma_min(0)
         eng.synth_ld_g(0, 11, a.nsamp, np.zeros(M))
         rs = np.random.RandomState(0)
         for nc in [int(x) for x in a.ncols.split(",")]:
