@@ -1,40 +1,41 @@
-// Multi-RHS symmetric LD pass on the f64 matrix cores (v_mfma_f64_16x16x4f64).
+// Multi-RHS symmetric LD pass on the f64 matrix cores.
 //
-// For 3..16 right-hand sides a VALU pass runs out of operands before HBM
-// runs out of bytes: each stored R_ij feeds 2*NC FMAs whose P operands must
-// be in registers, so the VALU kernels (sym_pass.hip) re-read P or spill
-// column partials through LDS at a multiple of the HBM traffic.  A 16x16x4
-// MFMA takes ONE f64 of R and ONE f64 of P per lane and does 16 FMAs per lane:
-// the matrix core does the register blocking.  On gfx950 the f64 MFMA rate
-// is about the f64 VALU rate (tools/mfma_probe.hip: ~47 TF at 2 waves/SIMD),
-// so with the RHS padded to 16 columns the pass costs ~16 MFMAs per 4 KiB of
-// stored R for any NC <= 16 -- close to the HBM time of the same bytes.
+// For 3..16 right-hand sides a VALU pass runs out of operands before HBM runs
+// out of bytes: each stored R_ij feeds 2*NC FMAs whose P operands must sit in
+// registers, so the VALU kernels (sym_pass.hip) re-read P or spill column
+// partials through LDS at a multiple of the HBM traffic.  An MFMA takes ONE
+// f64 of R and ONE f64 of P per lane and lets the matrix core do the register
+// blocking.  Of the two f64 shapes, v_mfma_f64_4x4x4f64 (4 blocks of 4x4x4)
+// costs 17 cycles for 256 MACs (~71 TF) and v_mfma_f64_16x16x4f64 140 cycles
+// for 1024 (~47 TF) (tools/mfma_probe.hip); the 4x4x4 form also needs only
+// ceil(NC/4) column groups instead of padding to 16.  Per 16x32 sub-tile
+// (4 KiB of R) the pass issues 16 * ceil(NC/4) of them (~270 cycles per group),
+// under the ~1300-1500 cycles the same bytes take to arrive from HBM.
+//
+// 4x4x4 f64 lane maps (probed): block b = (l>>2)&3;
+//   A_b[m][k] at lane 16k + 4b + m,  B_b[k][n] at lane 16k + 4b + n,
+//   D_b[m][n] at lane 16m + 4b + n.
 //
 // Same items (panel x 512-column chunk), partial layout and finalize as the
 // VALU pass (class 1): rowpart[item][256][NC], colpart[item][NC][512].
 //
-// One 256-thread workgroup per item; wave w owns chunk columns
-// [128 w, 128 w + 128) and sweeps the panel's rows in 16-row groups.  Each
-// 16 x 32 sub-tile (4 KiB) is loaded from HBM once, 16 B per lane:
-//   col fragment  lane l: R[row 4a + (l>>4)][col 2(l&15) + e]  (a = 0..3)
-//       -> A operand (m = column, k = row) of  Dcol[col][c] += R[j][col] P[j][c]
-// and written to a per-wave LDS tile (rows padded to 34 doubles), from which
-// the transposed fragment is read back without bank conflicts:
-//   row fragment  lane l: R[row (l&15)][col 8s + 2(l>>4) + e]  (s = 0..3)
-//       -> A operand (m = row, k = column) of  Drow[row][c] += R[row][i] P[i][c]
-// The row-part B operands (P at the wave's 128 columns) stay in registers for
-// the whole item.
-// Dcol accumulates over all 256 rows in registers and is complete per item;
-// Drow is summed over the 4 waves through LDS once per 16-row group, in wave
-// order.  The B operands come from Pk, the RHS interleaved as Pk[i][16].
-// f64 C/D layout (cdna_hip_programming.md): D[(l>>4) + 4r][l & 15], r = 0..3.
+// One workgroup per item, NW waves; wave w owns chunk columns
+// [w*512/NW, (w+1)*512/NW) and sweeps the panel's rows in 16-row groups.
+// Each 16 x 32 sub-tile is loaded from HBM once, 16 B per lane:
+//   col fragment  lane l: R[row 4a + (l>>4)][col pair (l&15), + e]   (a = 0..3)
+//       A_b[m][k] = R[row k][pair 4b+m]: Dcol[pair][c] += R[j][i] P[j][c]
+// and written to a per-wave LDS tile (rows padded to 34 doubles) from which
+//   row fragment  lane l: R[row 4q + (l&3)][col pair (l>>4) + 4b, + e] (q = 0..3)
+//       A_b[m][k] = R[row m][pair k+4b]: Drow[row][c] += R[j][i] P[i][c]
+// is read back without bank conflicts.  Each 4x4x4 block contracts its own 4
+// column pairs, so the 4 blocks' row partials are summed by two xor-shuffles
+// per row group (fixed order), then over the waves through LDS (wave order).
+// Dcol accumulates over all 256 rows in registers; every order is fixed.
 #include "common.h"
 
 namespace sgv {
 
-typedef double d4 __attribute__((ext_vector_type(4)));
-
-#define MFMA64(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
+#define MFMA4(a, b, c) __builtin_amdgcn_mfma_f64_4x4x4f64((a), (b), (c), 0, 0, 0)
 
 // wave-local LDS ordering point: lanes of one wave exchange data through the
 // tile.  The LDS executes a wave's DS instructions in order, so the write ->
@@ -46,15 +47,182 @@ __device__ __forceinline__ void lds_order() {
   __builtin_amdgcn_wave_barrier();
 }
 
-constexpr int MF_CW = 512;            // chunk width (class 1 items)
-constexpr int MF_WC = MF_CW / 4;      // columns per wave
-constexpr int MF_NT = MF_WC / 32;     // 32-column steps per wave
+constexpr int MF_CW = 512;   // chunk width (class 1 items)
+constexpr int MF_LDP = 34;   // staging row pitch (doubles): conflict-free both ways
 
-__global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymItem* __restrict__ items,
+template <int NG, int NW>
+__global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restrict__ items,
+                                                         const double* __restrict__ pk, int ncol,
+                                                         double* __restrict__ rowpart,
+                                                         double* __restrict__ colpart) {
+  constexpr int WC = MF_CW / NW;   // columns per wave
+  constexpr int NT = WC / 32;      // 32-column steps per wave
+  static_assert(NT >= 1, "at least one step per wave");
+  __shared__ double red[2][NW][256];
+  __shared__ __attribute__((aligned(16))) double stg[NW][16 * MF_LDP];
+  const SymItem it = items[blockIdx.x];
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+  const int lo = lane & 15, hi = lane >> 4, bq = (lane >> 2) & 3, n4 = lane & 3;
+  const int pc = hi + 4 * bq;                          // this lane's column pair in a fragment
+  const double* base = it.P + (it.c0 - it.r0);        // panel row 0, chunk column 0
+  const int64_t w = it.w;
+  const double* pkb = pk + (int64_t)it.voff * 16;     // Pk of this block (block-relative index)
+  const int cw0 = wid * WC;                            // first chunk column of this wave
+  double* sb = stg[wid];
+
+  // row-part B operands: P at this wave's columns, reused by every row group
+  double brow[NT][2][NG];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int col = cw0 + 32 * t + 2 * pc + e;
+#pragma unroll
+      for (int q = 0; q < NG; ++q) {
+        const double v = ldg(pkb + (int64_t)(it.c0 + (col < it.nc ? col : 0)) * 16 + 4 * q + n4);
+        brow[t][e][q] = col < it.nc ? v : 0.0;
+      }
+    }
+  double dcol[NT][2][NG];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int q = 0; q < NG; ++q) dcol[t][e][q] = 0.0;
+
+  // fragment loads of step (g, t), 16 B per lane, branch-free: a row past H
+  // clamps (its P is 0), a column past the chunk loads column 0 (finite; it
+  // meets a zero B in the row part and is never stored by the column part)
+  auto load_cf = [&](int g, int t, d2* cf) {
+    const int xc = cw0 + 32 * t + 2 * lo;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int rB = 16 * g + 4 * a + hi;
+      const double* row = base + (int64_t)(rB < it.H ? rB : it.H - 1) * w;
+      cf[a] = ldg_nt((const d2*)(row + (xc < it.nc ? xc : 0)));
+    }
+  };
+  auto load_bcol = [&](int g, double (*bc)[NG]) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int rB = 16 * g + 4 * a + hi;
+#pragma unroll
+      for (int q = 0; q < NG; ++q) {
+        const double v = ldg(pkb + (int64_t)(it.r0 + (rB < it.H ? rB : 0)) * 16 + 4 * q + n4);
+        bc[a][q] = rB < it.H ? v : 0.0;
+      }
+    }
+  };
+  const int ng = (it.H + 15) / 16;
+  d2 cfn[4];
+  double bcn[4][NG];
+  load_cf(0, 0, cfn);
+  load_bcol(0, bcn);
+
+#pragma unroll 1
+  for (int g = 0; g < ng; ++g) {                      // ng is uniform over the workgroup
+    double bcol[4][NG];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int q = 0; q < NG; ++q) bcol[a][q] = bcn[a][q];
+    double drow[4][NG];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < NG; ++q) drow[r][q] = 0.0;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      d2 cf[4], rf[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) cf[a] = cfn[a];
+      // the next step's loads go out here, ahead of this step's LDS and MFMA work
+      if (t + 1 < NT) {
+        load_cf(g, t + 1, cfn);
+      } else if (g + 1 < ng) {
+        load_cf(g + 1, 0, cfn);
+        load_bcol(g + 1, bcn);
+      }
+      lds_order();                                     // previous step's tile reads issued
+#pragma unroll
+      for (int a = 0; a < 4; ++a) *(d2*)(sb + (4 * a + hi) * MF_LDP + 2 * lo) = cf[a];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+          dcol[t][0][q] = MFMA4(cf[a].x, bcol[a][q], dcol[t][0][q]);
+          dcol[t][1][q] = MFMA4(cf[a].y, bcol[a][q], dcol[t][1][q]);
+        }
+      lds_order();                                     // tile written
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + (4 * r + n4) * MF_LDP + 2 * pc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < NG; ++q) {
+          drow[r][q] = MFMA4(rf[r].x, brow[t][0][q], drow[r][q]);
+          drow[r][q] = MFMA4(rf[r].y, brow[t][1][q], drow[r][q]);
+        }
+    }
+    // row sums: the 4 blocks (lanes differing in bits 2,3), then the waves in order
+    double* rb = red[g & 1][wid];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int q = 0; q < NG; ++q) {
+        double v = drow[r][q];
+        v = v + __shfl_xor(v, 4);
+        v = v + __shfl_xor(v, 8);
+        if (bq == 0) rb[((4 * r + hi) << 4) + 4 * q + n4] = v;   // D row 4r + m (m = hi)
+      }
+    __syncthreads();
+    if (threadIdx.x < 256) {
+      const int t = threadIdx.x, row = t >> 4, cc = t & 15;
+      if (16 * g + row < it.H && cc < ncol) {
+        double s = red[g & 1][0][t];
+#pragma unroll
+        for (int v = 1; v < NW; ++v) s += red[g & 1][v][t];
+        rowpart[((int64_t)it.item * SYM_H + 16 * g + row) * ncol + cc] = s;
+      }
+    }
+  }
+
+  // column sums (complete over the panel's rows), right of the diagonal block only:
+  // D_b[m][n] at lane 16m + 4b + n holds column pair 4b + m = pc, column c = 4q + n
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    const int cc = 4 * q + n4;
+    if (cc < ncol) {
+      double* out = colpart + ((int64_t)it.item * ncol + cc) * MF_CW;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int jl = cw0 + 32 * t + 2 * pc + e;
+          if (jl < it.nc && it.c0 + jl >= it.diag_end) out[jl] = dcol[t][e][q];
+        }
+    }
+  }
+}
+
+// 13..16 right-hand sides: v_mfma_f64_16x16x4f64 (one 16-column group, 140
+// cycles per 16x16x4) keeps fewer accumulators and B operands in registers
+// than four 4x4x4 groups, which spill at 4 waves.  Same structure as above:
+//   col fragment -> A (m = column, k = row); LDS tile -> row fragment
+//   lane l: R[row (l&15)][col 8s + 2(l>>4) + e] -> A (m = row, k = column);
+//   16x16x4 f64 C/D layout (cdna_hip_programming.md): D[(l>>4) + 4r][l & 15].
+typedef double d4 __attribute__((ext_vector_type(4)));
+#define MFMA16(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
+constexpr int MF_WC = MF_CW / 4;
+constexpr int MF_NT = MF_WC / 32;
+
+__global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymItem* __restrict__ items,
                                                      const double* __restrict__ pk, int ncol,
                                                      double* __restrict__ rowpart,
                                                      double* __restrict__ colpart) {
-  constexpr int LDP = 34;                     // staging row pitch (doubles): conflict-free
+  constexpr int LDP = MF_LDP;
   __shared__ double red[2][4][256];
   __shared__ __attribute__((aligned(16))) double stg[4][16 * LDP];
   const SymItem it = items[blockIdx.x];
@@ -132,16 +300,16 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymItem* __restrict__
       for (int a = 0; a < 4; ++a) *(d2*)(sb + (4 * a + hi) * LDP + 2 * lo) = cf[a];
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        dcol[t][0] = MFMA64(cf[a].x, bcol[a], dcol[t][0]);
-        dcol[t][1] = MFMA64(cf[a].y, bcol[a], dcol[t][1]);
+        dcol[t][0] = MFMA16(cf[a].x, bcol[a], dcol[t][0]);
+        dcol[t][1] = MFMA16(cf[a].y, bcol[a], dcol[t][1]);
       }
       lds_order();                                     // tile written
 #pragma unroll
       for (int s = 0; s < 4; ++s) rf[s] = *(const d2*)(sb + lo * LDP + 8 * s + 2 * hi);
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        drow0 = MFMA64(rf[s].x, brow[t][s][0], drow0);
-        drow1 = MFMA64(rf[s].y, brow[t][s][1], drow1);
+        drow0 = MFMA16(rf[s].x, brow[t][s][0], drow0);
+        drow1 = MFMA16(rf[s].y, brow[t][s][1], drow1);
       }
     }
     // row sums of this 16-row group: waves 0..3 in order
@@ -182,6 +350,13 @@ __global__ __launch_bounds__(256) void k_pack16(PassArgs pa, int ncol, int64_t m
   pk[t] = c < ncol ? pa.in[c][i] : 0.0;
 }
 
+template <int NG, int NW>
+static void launch_mf(const SymItem* d_items, int nitems, const double* d_pk, int nc,
+                      double* rowpart, double* colpart, hipStream_t st) {
+  hipLaunchKernelGGL((k_sym_mfma<NG, NW>), dim3(nitems), dim3(NW * 64), 0, st, d_items, d_pk, nc,
+                     rowpart, colpart);
+}
+
 hipError_t launch_sym_mfma(int nc, const SymItem* d_items, int nitems, const PassArgs& pa,
                            int64_t mpad, double* d_pk, double* rowpart, double* colpart,
                            hipStream_t st) {
@@ -189,8 +364,15 @@ hipError_t launch_sym_mfma(int nc, const SymItem* d_items, int nitems, const Pas
   const int64_t n16 = mpad * 16;
   hipLaunchKernelGGL(k_pack16, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, st, pa, nc,
                      mpad, d_pk);
-  hipLaunchKernelGGL(k_sym_mfma, dim3(nitems), dim3(256), 0, st, d_items, d_pk, nc, rowpart,
-                     colpart);
+  switch ((nc + 3) / 4) {
+    case 1: launch_mf<1, 4>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
+    case 2: launch_mf<2, 4>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
+    case 3: launch_mf<3, 4>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
+    default:
+      hipLaunchKernelGGL(k_sym_mfma16, dim3(nitems), dim3(256), 0, st, d_items, d_pk, nc, rowpart,
+                         colpart);
+      break;
+  }
   return hipGetLastError();
 }
 

@@ -45,6 +45,23 @@ __global__ __launch_bounds__(256) void k_mfma_rate(double* out, int iters, long 
 }
 
 template <int NACC>
+__global__ __launch_bounds__(256) void k_mfma4_rate(double* out, int iters, long long* cyc) {
+  double a = threadIdx.x * 1e-3, b = 1.0 + threadIdx.x * 1e-4;
+  double c[NACC];
+  for (int i = 0; i < NACC; ++i) c[i] = 0;
+  long long t0 = clock64();
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) c[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c[i], 0, 0, 0);
+  }
+  long long t1 = clock64();
+  double s = 0;
+  for (int i = 0; i < NACC; ++i) s += c[i];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  if (threadIdx.x == 0 && blockIdx.x == 0) *cyc = t1 - t0;
+}
+
+template <int NACC>
 __global__ __launch_bounds__(256) void k_fma_rate(double* out, int iters, long long* cyc) {
   double a = threadIdx.x * 1e-3, b = 1.0 + threadIdx.x * 1e-4;
   double c[NACC];
@@ -90,7 +107,7 @@ int main() {
   printf("layout16x16x4 (row=(l>>4)+4r, col=l&15): %s (%d bad)\n", bad ? "MISMATCH" : "ok", bad);
   // ---- 4x4x4 (4 blocks?) probe: print raw result for A = onehot patterns
   for (int l = 0; l < 64; ++l) A[l] = l + 1;
-  for (int trial = 0; trial < 64; trial += 1) {
+  for (int trial = 0; trial < 0; trial += 1) {
     std::vector<double> Bv(64, 0.0);
     Bv[trial] = 1.0;
     CK(hipMemcpy(dA, A.data(), 512, hipMemcpyHostToDevice));
@@ -123,6 +140,22 @@ int main() {
     const double flops = 2.0 * 16 * 16 * 4 * 8.0 * iters * nblk * 4;
     printf("mfma_f64_16x16x4 waves/SIMD=%d: %.3f ms  %.1f TF  cycles/mfma(clock64)=%.1f\n", wps, ms,
            flops / ms / 1e9, (double)cyc / (iters * 8.0));
+  }
+  for (int wps = 1; wps <= 2; ++wps) {
+    const int nblk = 256 * wps;
+    for (int rep = 0; rep < 2; ++rep) {
+      CK(hipEventRecord(e0));
+      k_mfma4_rate<8><<<nblk, 256>>>(dout, iters, dcyc);
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+    }
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    long long cyc;
+    CK(hipMemcpy(&cyc, dcyc, 8, hipMemcpyDeviceToHost));
+    const double flops = 2.0 * 4 * 4 * 4 * 4 * 8.0 * iters * nblk * 4;
+    printf("mfma_f64_4x4x4 (4 blocks) waves/SIMD=%d: %.3f ms  %.1f TF  cycles/mfma(clock64)=%.1f\n", wps,
+           ms, flops / ms / 1e9, (double)cyc / (iters * 8.0));
   }
   for (int wps = 1; wps <= 4; wps *= 2) {
     const int nblk = 256 * wps;
