@@ -199,7 +199,12 @@ def main():
     bytes_launch = ld_bytes_launch + tm["rhs_bytes"] / launches
     achieved = bytes_launch / avg_s / 1e9 if avg_s > 0 else None
     dense_equiv = (tm["dense_bytes"] / launches + tm["rhs_bytes"] / launches) / avg_s / 1e9
-    traffic, traffic_src = read_traffic("k_sym_pass" if args.ld_format == "packed" else "k_ld_pass")
+    mfma = args.ld_format == "packed" and 2 * K >= 3     # NC >= 3: the f64 MFMA pass
+    traffic, traffic_src = read_traffic(("k_sym_mfma" if mfma else "k_sym_pass")
+                                        if args.ld_format == "packed" else "k_ld_pass")
+    cname = {1: "C2 (BASELINE.json configs[1])", 4: "C3 (BASELINE.json configs[2])"}.get(K, "C2-like")
+    if eng.M != 200000:
+        cname = "custom"
     passes = sum(r["ld_passes"] for r in recs)
     ld_bytes_total = ld_bytes_launch * comm.Get_size()
     result = {
@@ -217,10 +222,11 @@ def main():
         "data": "synthetic: device generator following simulation/sim_gen_phen_mult.py "
                 "(Bin(2,0.4) genotypes, 50%% causal, h2=0.8), seed %d" % args.seed,
         "config": {
-            "workload": "C2 (BASELINE.json configs[1]): K=%d cohort, M=%d markers in %d LD blocks "
-                        "of %d, N=%d, reference CLI default flags, output files written each "
-                        "iteration, prior %s %s" % (K, eng.M, args.blocks, args.block_size, args.nsamp,
-                                            prior["prior_vars"], prior["prior_probs"]),
+            "workload": "%s: K=%d cohort(s) sharing one LD, M=%d markers in %d LD blocks "
+                        "of %d, N=%d per cohort, reference CLI default flags, output files written "
+                        "each iteration, prior %s %s" % (cname, K, eng.M, args.blocks,
+                                                         args.block_size, args.nsamp,
+                                                         prior["prior_vars"], prior["prior_probs"]),
             "K": K, "M": eng.M, "ld_blocks": args.blocks, "block_size": args.block_size,
             "N": args.nsamp, "parallelism": "LD blocks sharded over %d GPU rank(s)" % world,
         },
@@ -231,7 +237,8 @@ def main():
             "unit": "GB/s",
             "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
             "traffic": traffic,
-            "kernel": ("sgv::k_sym_pass + k_sym_finalize (packed symmetric LD pass, per GPU)"
+            "kernel": (("sgv::k_sym_mfma (f64 MFMA, >= 3 RHS)" if mfma else "sgv::k_sym_pass")
+                       + " + k_sym_finalize (packed symmetric LD pass, per GPU)"
                        if args.ld_format == "packed" else "sgv::k_ld_pass (dense LD pass, per GPU)"),
             "bytes_per_launch": bytes_launch,
             "ld_format": args.ld_format,

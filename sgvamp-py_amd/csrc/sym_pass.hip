@@ -130,38 +130,49 @@ __global__ __launch_bounds__(256) void k_sym_pass(const SymItem* __restrict__ it
   }
 }
 
-// one workgroup per panel; thread t = panel row r0 + t
+// one workgroup per panel; thread t = panel row r0 + t.  The item offsets of
+// the block's earlier panels are staged in LDS first, so the column-partial
+// loads of the panel loop are independent of each other (no descriptor load
+// in the chain) and can be kept in flight together.
 __global__ __launch_bounds__(256) void k_sym_finalize(const SymPanel* __restrict__ panels,
                                                       int ncol, int cw, PassArgs pa,
                                                       const double* __restrict__ rowpart,
                                                       const double* __restrict__ colpart,
                                                       double* __restrict__ partials) {
+  constexpr int PCH = 1024;   // panels staged per round
+  __shared__ int s_ib[PCH];
   const SymPanel pn = panels[blockIdx.x];
   const int t = threadIdx.x;
   double acc[MAXC];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) acc[c] = 0.0;
+  double y[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) y[c] = 0.0;
+  const int i = pn.r0 + (t < pn.H ? t : 0);   // block-relative row
+  // this panel's row parts, chunk order
+  for (int itm = pn.item_begin; itm < pn.item_end; ++itm) {
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      if (c < ncol) y[c] += ldg(rowpart + ((int64_t)itm * SYM_H + t) * ncol + c);
+  }
+  // column parts of the earlier panels of this block, panel order
+  for (int g0 = 0; g0 < pn.g; g0 += PCH) {
+    const int gn = min(PCH, pn.g - g0);
+    __syncthreads();
+    for (int k = t; k < gn; k += 256) s_ib[k] = panels[pn.blk_panel0 + g0 + k].item_begin;
+    __syncthreads();
+#pragma unroll 4
+    for (int k = 0; k < gn; ++k) {
+      const int rel = i - (g0 + k) * SYM_H;      // column relative to that panel's first row
+      const int ch = rel / cw;
+      const int64_t base = ((int64_t)(s_ib[k] + ch) * ncol) * cw + (rel - ch * cw);
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+        if (c < ncol) y[c] += ldg(colpart + base + (int64_t)c * cw);
+    }
+  }
   if (t < pn.H) {
-    const int i = pn.r0 + t;  // block-relative row
-    double y[MAXC];
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c) y[c] = 0.0;
-    // this panel's row parts, chunk order
-    for (int itm = pn.item_begin; itm < pn.item_end; ++itm) {
-#pragma unroll
-      for (int c = 0; c < MAXC; ++c)
-        if (c < ncol) y[c] += rowpart[((int64_t)itm * SYM_H + t) * ncol + c];
-    }
-    // column parts of the earlier panels of this block, panel order
-    for (int g = pn.blk_panel0; g < pn.blk_panel0 + pn.g; ++g) {
-      const SymPanel q = panels[g];
-      const int ch = (i - q.r0) / cw;
-      const int itm = q.item_begin + ch;
-      const int jl = i - q.r0 - ch * cw;
-#pragma unroll
-      for (int c = 0; c < MAXC; ++c)
-        if (c < ncol) y[c] += colpart[((int64_t)itm * ncol + c) * cw + jl];
-    }
     const int64_t idx = pn.voff + i;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c)
