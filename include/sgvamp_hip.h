@@ -102,6 +102,14 @@ int sgv_comm_init_host(sgv_ctx* ctx, int nranks, int rank, const int* nblk_per_r
  * Replaces the R loaders src/main.py:199-202 (dense .npy / CSR .npz blocks). */
 int sgv_set_ld_block(sgv_ctx* ctx, int ld, int blk_local, const double* rowmajor,
                      int64_t ld_host);
+/* R_s xhat2 and R_s Sigma2_u for gamw learning (src/sgvamp.py:352,359) and the
+ * next warm start's R_s x0 (scipy iterative.py:392): on (default), carried
+ * through both CG solves -- x_k = x_0 + sum a_i p_i, so R_s x_k = R_s x_0 +
+ * sum a_i R_s p_i with R_s p_i written by the pass the CG makes anyway -- which
+ * saves one LD pass per outer iteration; off, computed by a separate pass as
+ * the reference does.  Same values in exact arithmetic; measured against the
+ * reference fixtures the carried form agrees as closely (tests/). */
+int sgv_set_rs_recurrence(sgv_ctx* ctx, int on);
 /* Packed passes with at least nc_min right-hand sides run on the f64 matrix
  * cores (v_mfma_f64_16x16x4f64); fewer run on the VALU.  0 = never.  Default 3
  * (env SGV_MFMA_MIN).  Results agree to rounding, not bitwise, across the two. */

@@ -221,6 +221,47 @@ def cg_scipy(matvec, b, x0, maxiter, red, rtol=1e-5):
     return x, maxiter, maxiter, nmv
 
 
+def cg_track(matvec_rs, gw, gam2, b, x0, rsx0, maxiter, red, rtol=1e-5):
+    """cg_scipy with A = gw*R_s + gam2*I that also carries R_s x along the
+    iterates: x_k = x_0 + sum alpha_i p_i  =>  R_s x_k = R_s x_0 + sum alpha_i (R_s p_i),
+    and every iteration's pass computes R_s p_i anyway.  The warm-start residual
+    uses the carried R_s x_0 (no extra pass).  Same iterates as cg_scipy in exact
+    arithmetic; rounding differs from a direct product.  Returns
+    (x, rsx, info, n_iter, n_matvec)."""
+    x = np.array(x0, dtype=np.float64).ravel().copy()
+    rsx = np.array(rsx0, dtype=np.float64).ravel().copy()
+    b = np.asarray(b, dtype=np.float64).ravel()
+    bnrm2 = red.norm(b)
+    atol = max(0.0, rtol * bnrm2)
+    if bnrm2 == 0:
+        return b.copy(), np.zeros_like(b), 0, 0, 0
+    nmv = 0
+    if x.any():
+        r = b - (gw * rsx + gam2 * x)
+    else:
+        r = b.copy()
+    rho_prev, p = None, None
+    for it in range(maxiter):
+        if red.norm(r) < atol:
+            return x, rsx, 0, it, nmv
+        rho_cur = red.dot(r, r)
+        if it > 0:
+            beta = rho_cur / rho_prev
+            p *= beta
+            p += r
+        else:
+            p = r.copy()
+        y = matvec_rs(p)
+        q = gw * y + gam2 * p
+        nmv += 1
+        alpha = rho_cur / red.dot(p, q)
+        x += alpha * p
+        rsx += alpha * y
+        r -= alpha * q
+        rho_prev = rho_cur
+    return x, rsx, maxiter, maxiter, nmv
+
+
 # ----------------------------------------------------------------------------
 # probe vectors (the reference's global RNG, seeded per cohort rank)
 # ----------------------------------------------------------------------------
@@ -241,8 +282,13 @@ class ProbeStream:
 def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-6,
           prior_vars=(0.0, 1.0), prior_probs=(0.99, 0.01), x0=None, cg_maxit=500,
           em_prior_maxit=100, learn_gamw=True, lmmse_damp=False, prior_update="em",
-          update_prior_from=1, seed=0, reducer=None, M_total=None, probe=None):
+          update_prior_from=1, seed=0, reducer=None, M_total=None, probe=None,
+          rs_recurrence=False):
     """All K cohorts of src/sgvamp.py:196-389 in one process.
+
+    rs_recurrence: carry R_s x through both CG solves (cg_track) instead of the
+    direct products of the warm start and gamw learning (:352, :359) -- the
+    build's pass-saving variant; exact in exact arithmetic.
 
     lds: list of BlockLD; ld_of[k]: which LD cohort k uses; r_list[k]: (M,)
     x0: true signal in reference scale (beta*sqrt(N_0)) or None.
@@ -265,6 +311,8 @@ def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-
     xhat1 = np.zeros(M)
     xhat2 = [np.zeros(M) for _ in range(K)]
     sig2u_prev = [np.zeros(M) for _ in range(K)]
+    rs_x2 = [np.zeros(M) for _ in range(K)]       # R_s xhat2 (rs_recurrence)
+    rs_s2u = [np.zeros(M) for _ in range(K)]      # R_s Sigma2_u
     gam1_k = [gam1] * K
     gamw_k = [gamw] * K
     alpha1_k = [0] * K
@@ -309,12 +357,24 @@ def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-
                 return gw * L.matvec_Rs(p) + gam2 * p
             mu2 = gw * r[k] + gam2 * r2                                 # :313
             x2_prev = xhat2[k]
-            x2, info1, n1, m1 = cg_scipy(A, mu2, x2_prev, cg_maxit, red)    # :316
+            if rs_recurrence:
+                x2, rx2, info1, n1, m1 = cg_track(L.matvec_Rs, gw, gam2, mu2, x2_prev, rs_x2[k],
+                                                  cg_maxit, red)
+                if lmmse_damp:
+                    rx2 = rho * rx2 + (1 - rho) * rs_x2[k]
+                rs_x2[k] = rx2
+            else:
+                x2, info1, n1, m1 = cg_scipy(A, mu2, x2_prev, cg_maxit, red)    # :316
             if lmmse_damp:
                 x2 = rho * x2 + (1 - rho) * x2_prev                     # :322-323
             xhat2[k] = x2
             u = probes(k, it)                                           # :326
-            s2u, info2, n2, m2 = cg_scipy(A, u, sig2u_prev[k], cg_maxit, red)   # :332
+            if rs_recurrence:
+                s2u, rs2, info2, n2, m2 = cg_track(L.matvec_Rs, gw, gam2, u, sig2u_prev[k],
+                                                   rs_s2u[k], cg_maxit, red)
+                rs_s2u[k] = rs2
+            else:
+                s2u, info2, n2, m2 = cg_scipy(A, u, sig2u_prev[k], cg_maxit, red)   # :332
             sig2u_prev[k] = s2u
             uf = u.astype(np.float64)
             TrSigma2 = red.dot(uf, s2u)                                 # :338
@@ -326,10 +386,11 @@ def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-
             r1[k] = (x2 - alpha2 * r2) / (1 - alpha2)                   # :348
             if learn_gamw:                                              # :350-364
                 N = N_list[k]
-                z = N - 2 * red.dot(x2, r[k]) + red.dot(x2, L.matvec_Rs(x2))
+                rx = rs_x2[k] if rs_recurrence else L.matvec_Rs(x2)
+                z = N - 2 * red.dot(x2, r[k]) + red.dot(x2, rx)
                 if z < 0:
                     z = 0
-                TrRSigma2 = red.dot(uf, L.matvec_Rs(s2u))
+                TrRSigma2 = red.dot(uf, rs_s2u[k] if rs_recurrence else L.matvec_Rs(s2u))
                 gw = 1 / (z / N + TrRSigma2 / N)
             traj["gamws"][k].append(gw)                                 # :373
             gamw_k[k] = max(gw, 1.0)                                    # :374

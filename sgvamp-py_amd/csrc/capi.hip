@@ -103,7 +103,7 @@ struct sgv_ctx {
   int* d_ch_begin = nullptr;
   // vectors (padded layout, zero padding)
   double* pool = nullptr;
-  std::vector<double*> r, r1, r2, U, X, X0, Rr, P, Q, RX0, S;
+  std::vector<double*> r, r1, r2, U, X, X0, Rr, P, Q, RX0, Y, RXp, S;
   double* xhat1 = nullptr;
   double* x0 = nullptr;
   // reductions
@@ -126,12 +126,13 @@ struct sgv_ctx {
   ncclComm_t comm = nullptr;
   sgv_allgather_fn host_ag = nullptr;   // host exchange (sgv_comm_init_host)
   void* host_ag_user = nullptr;
-  double* h_bsum = nullptr;             // pinned [nbmax * 32] and [nranks][nbmax * 32]
+  double* h_bsum = nullptr;             // pinned [nbmax * MAXNV] and [nranks][nbmax * MAXNV]
   double* h_bsum_all = nullptr;
   int nranks = 1, rank = 0;
   // solver state
   std::vector<int> xnz;        // x0.any() per CG column (2K)
   std::vector<int> rx0_valid;  // RX0[c] == R_s X[c]
+  int rs_rec = 1;              // carry R_s x through the CG (sgv_set_rs_recurrence)
   hipEvent_t ev_sync = nullptr;   // host waits spin on this event
   // timers
   std::vector<hipEvent_t> evpool;
@@ -204,7 +205,7 @@ static int stream_wait(sgv_ctx* c) {
 // ---------------------------------------------------------------------------
 static Map16 identity_map() {
   Map16 m;
-  for (int i = 0; i < MAXC * 2; ++i) m.d[i] = i;
+  for (int i = 0; i < MAXNV; ++i) m.d[i] = i;
   return m;
 }
 
@@ -530,6 +531,9 @@ struct CgCols {
   double* Rr[MAXC];
   double* P[MAXC];
   double* Q[MAXC];
+  double* RX[MAXC] = {};   // non-null: carry R_s x (RX += alpha R_s p), Y = R_s p scratch
+  double* Y[MAXC] = {};
+  double s = 0.0;          // ridge of R_s
 };
 
 static int cg_loop(sgv_ctx* c, const CgCols& cc, double* rho, const double* atol, int maxiter,
@@ -579,12 +583,15 @@ static int cg_loop(sgv_ctx* c, const CgCols& cc, double* rho, const double* atol
         pa.in[nc] = cc.P[j];
         pa.out[nc] = cc.Q[j];
         pa.dot[nc] = cc.P[j];
+        pa.yout[nc] = cc.RX[j] ? cc.Y[j] : nullptr;
         pa.c1[nc] = cc.c1[j];
         pa.c2[nc] = cc.c2[j];
         map.d[nc] = j;
         ++nc;
       }
       if (!nc) continue;
+      pa.ys1 = 1.0 - cc.s;   // Y = R_s p = (1-s) R p + s p
+      pa.ys0 = cc.s;
       CHK(ld_pass(c, ld, nc, pa));
       CHK(reduce_dev(c, nc, ld_parts(c, ld), map, c->d_pq));
       if (passes) ++*passes;
@@ -599,6 +606,8 @@ static int cg_loop(sgv_ctx* c, const CgCols& cc, double* rho, const double* atol
       xa.Rr[j] = cc.Rr[j];
       xa.P[j] = cc.P[j];
       xa.Q[j] = cc.Q[j];
+      xa.RX[j] = cc.RX[j];
+      xa.Y[j] = cc.Y[j];
       xa.rho[j] = rho[j];
     }
     HIPCHK(launch_cg_xr(c->d_ch, c->nch, xa, c->d_part, c->st));
@@ -720,9 +729,9 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
     c->d_blks.push_back(d);
   }
 
-  // vectors: r, r1, r2, U (K each); xhat1, x0; X, X0, Rr, P, Q, RX0 (2K each);
+  // vectors: r, r1, r2, U (K each); xhat1, x0; X, X0, Rr, P, Q, RX0, Y, RXp (2K each);
   // S: 5 * MAXC scratch columns for the operator-seam entry points
-  const int nvec = 4 * K + 2 + 12 * K + 5 * MAXC;
+  const int nvec = 4 * K + 2 + 16 * K + 5 * MAXC;
   const size_t vbytes = sizeof(double) * (size_t)c->Mpad * nvec;
   CREATE_HIP(hipMalloc(&c->pool, vbytes));
   CREATE_HIP(hipMemset(c->pool, 0, vbytes));
@@ -747,13 +756,15 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   take(c->P, 2 * K);
   take(c->Q, 2 * K);
   take(c->RX0, 2 * K);
+  take(c->Y, 2 * K);
+  take(c->RXp, 2 * K);
   take(c->S, 5 * MAXC);
 
-  const size_t part_n = (size_t)c->nch * 32;
+  const size_t part_n = (size_t)c->nch * MAXNV;
   CREATE_HIP(hipMalloc(&c->d_part, sizeof(double) * part_n));
   c->part_cap = part_n;
   c->nbmax = nblk;
-  CREATE_HIP(hipMalloc(&c->d_bsum, sizeof(double) * (size_t)nblk * 32));
+  CREATE_HIP(hipMalloc(&c->d_bsum, sizeof(double) * (size_t)nblk * MAXNV));
   CREATE_HIP(hipMalloc(&c->d_counts, sizeof(int)));
   CREATE_HIP(hipMemcpy(c->d_counts, &nblk, sizeof(int), hipMemcpyHostToDevice));
   CREATE_HIP(hipMalloc(&c->d_tot, sizeof(double) * 64));
@@ -826,7 +837,7 @@ static int comm_buffers(sgv_ctx* c, int nranks, int rank, const int* nblk_per_ra
   c->nranks = nranks;
   c->rank = rank;
   c->nbmax = *std::max_element(nblk_per_rank, nblk_per_rank + nranks);
-  const size_t per = (size_t)c->nbmax * 32;
+  const size_t per = (size_t)c->nbmax * MAXNV;
   HIPCHK(hipFree(c->d_bsum));
   c->d_bsum = nullptr;
   HIPCHK(hipMalloc(&c->d_bsum, sizeof(double) * per));
@@ -867,7 +878,7 @@ extern "C" int sgv_comm_init_host(sgv_ctx* c, int nranks, int rank, const int* n
   CHK(comm_args(c, nranks, rank, nblk_per_rank));
   if (nranks == 1) return SGV_OK;
   CHK(comm_buffers(c, nranks, rank, nblk_per_rank));
-  const size_t per = (size_t)c->nbmax * 32;
+  const size_t per = (size_t)c->nbmax * MAXNV;
   HIPCHK(hipHostMalloc(&c->h_bsum, sizeof(double) * per));
   HIPCHK(hipHostMalloc(&c->h_bsum_all, sizeof(double) * per * nranks));
   c->host_ag = fn;
@@ -887,6 +898,13 @@ static bool host_symmetric(const double* A, int64_t n, int64_t ld) {
         for (int64_t j = std::max(j0, i + 1); j < std::min(n, j0 + T); ++j)
           if (!(A[i * ld + j] == A[j * ld + i])) return false;
   return true;
+}
+
+extern "C" int sgv_set_rs_recurrence(sgv_ctx* c, int on) {
+  ENTER(c);
+  c->rs_rec = on ? 1 : 0;
+  std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), 0);   // re-derive R_s x0 once
+  return SGV_OK;
 }
 
 extern "C" int sgv_set_mfma_min(sgv_ctx* c, int nc_min) {
@@ -1193,7 +1211,8 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
     HIPCHK(launch_unpack_i8(c->d_ch, c->nch, c->d_ch_doff,
                             (const int8_t*)c->d_stage + (size_t)k * c->Mloc, c->U[k], c->st));
 
-  // warm start needs R_s x0 (reused from the previous gamw pass when valid)
+  // warm start needs R_s x0: carried from the previous iteration (rs_rec), or the
+  // previous gamw pass; a pass only when X was set from outside
   for (int ld = 0; ld < c->nld; ++ld) {
     PassArgs pa{};
     int nc = 0;
@@ -1234,12 +1253,14 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
     ia.col.P[j] = c->P[j];
     ia.col.Q[j] = c->Q[j];
     ia.col.RX0[j] = c->RX0[j];
+    ia.col.RXp[j] = c->rs_rec ? c->RXp[j] : nullptr;
     ia.warm[j] = c->xnz[j];
   }
   HIPCHK(launch_lmmse_init(c->d_ch, c->nch, ia, c->d_part, c->st));
   double tot[2 * MAXC];
   CHK(reduce_host(c, 2 * MAXC, c->d_ch_begin, tot));
-  std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), 0);
+  // carried: RX0 follows X through the CG; otherwise the gamw pass refreshes it
+  std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), c->rs_rec ? 1 : 0);
 
   CgCols cc;
   cc.ncol = ncol;
@@ -1254,33 +1275,42 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
     cc.Rr[j] = c->Rr[j];
     cc.P[j] = c->P[j];
     cc.Q[j] = c->Q[j];
+    if (c->rs_rec) {
+      cc.RX[j] = c->RX0[j];
+      cc.Y[j] = c->Y[j];
+    }
     const double bn = std::sqrt(tot[j]);      // bnrm2 (iterative.py:376)
     atol[j] = std::max(0.0, rtol * bn);
     rhov[j] = tot[MAXC + j];
     active[j] = 1;
     if (bn == 0.0) {                          // iterative.py:380-381: return b
       HIPCHK(hipMemsetAsync(c->X[j], 0, sizeof(double) * c->Mpad, c->st));
+      HIPCHK(hipMemsetAsync(c->RX0[j], 0, sizeof(double) * c->Mpad, c->st));   // R_s 0
       active[j] = 0;
     }
   }
+  cc.s = s;
   CHK(cg_loop(c, cc, rhov, atol, cg_maxit, active, iters, info, &passes));
 
   // damping, u.Sigma2_u, xhat2.r, x.any() (:322-323, 338, 352)
   PostArgs po{};
   po.K = K;
   po.damp = lmmse_damp;
+  po.rs = c->rs_rec;
   po.rho = rho;
   for (int j = 0; j < ncol; ++j) {
     po.X[j] = c->X[j];
     po.X0[j] = c->X0[j];
+    po.RX[j] = c->RX0[j];
+    po.RXp[j] = c->RXp[j];
   }
   for (int k = 0; k < K; ++k) {
     po.u[k] = c->U[k];
     po.r[k] = c->r[k];
   }
   HIPCHK(launch_lmmse_post(c->d_ch, c->nch, po, c->d_part, c->st));
-  double pt[2 * MAXK + MAXC];
-  CHK(reduce_host(c, 2 * MAXK + MAXC, c->d_ch_begin, pt));
+  double pt[4 * MAXK + MAXC];
+  CHK(reduce_host(c, 4 * MAXK + MAXC, c->d_ch_begin, pt));
   for (int j = 0; j < ncol; ++j) c->xnz[j] = pt[2 * MAXK + j] > 0.0;
 
   R1Args ra{};
@@ -1310,7 +1340,20 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
   }
   HIPCHK(launch_r1_update(c->d_ch, c->nch, ra, c->st));   // :348
 
-  if (learn_gamw) {  // :350-363; R_s [xhat2, Sigma2_u] is also the next warm start's R_s x0
+  if (learn_gamw && c->rs_rec) {  // :350-363 from the carried products: no pass
+    for (int k = 0; k < K; ++k) {
+      const double N = c->Ncoh[k];
+      double* o = out + (size_t)k * SGV_LMMSE_NOUT;
+      const double xRx = pt[2 * MAXK + MAXC + k];
+      const double TrRSigma2 = pt[3 * MAXK + MAXC + k];
+      double z = N - 2 * o[SGV_O_XR] + xRx;                        // :352
+      if (z < 0) z = 0;                                            // :353-354
+      o[SGV_O_Z] = z;
+      o[SGV_O_XRX] = xRx;
+      o[SGV_O_TRRSIGMA2] = TrRSigma2;
+      o[SGV_O_GAMW] = 1 / (z / N + TrRSigma2 / N);                 // :363
+    }
+  } else if (learn_gamw) {  // :350-363; R_s [xhat2, Sigma2_u] is also the next warm start's R_s x0
     for (int ld = 0; ld < c->nld; ++ld) {
       PassArgs pa{};
       Map16 map = identity_map();

@@ -92,16 +92,23 @@ __device__ __forceinline__ double* sym_addr(double* base, const int64_t* poff, c
 
 // Columns of one LD pass: out[c] = c1[c] * (R in[c]) + c2[c] * in[c];
 // partial[c] = sum_rows dot[c] * out[c] (dot[c] may be null).
+// out = c1 * (R in) + c2 * in; optionally also yout = ys1 * (R in) + ys0 * in
+// (R_s in: the CG carries R_s x along its iterates, see sgv_lmmse)
 struct PassArgs {
   const double* in[MAXC];
   double* out[MAXC];
   const double* dot[MAXC];
+  double* yout[MAXC];
   double c1[MAXC];
   double c2[MAXC];
+  double ys1, ys0;
 };
 
+// most values one ordered reduction carries
+constexpr int MAXNV = 4 * MAXK + MAXC;
+
 struct Map16 {
-  int d[MAXC * 2];
+  int d[MAXNV];
 };
 
 // ---- deterministic reductions --------------------------------------------
@@ -235,7 +242,8 @@ struct ColPtrs {
   double* Rr[MAXC];
   double* P[MAXC];
   double* Q[MAXC];
-  const double* RX0[MAXC];
+  double* RX0[MAXC];        // R_s X (the carried products)
+  double* RXp[MAXC];        // copy of RX0 at the start (damping of xhat2)
 };
 struct InitArgs {
   CohortPtrs cp;
@@ -244,7 +252,7 @@ struct InitArgs {
   int K;
   double alpha1[MAXK], gamw[MAXK], gam2[MAXK];
   int warm[MAXC];           // residual r = b - A x0 (x0.any()); else r = b
-  int save_x0;              // copy X[2k] to X0[2k] (LMMSE damping)
+  int save_x0;              // copy X[2k] to X0[2k] (and RX0 to RXp) for LMMSE damping
 };
 hipError_t launch_lmmse_init(const ChunkDesc* d_ch, int nch, const InitArgs& a, double* d_part,
                              hipStream_t st);
@@ -254,6 +262,8 @@ struct XrArgs {
   double* Rr[MAXC];
   const double* P[MAXC];
   const double* Q[MAXC];
+  double* RX[MAXC];         // RX += alpha Y (R_s x carried), if non-null
+  const double* Y[MAXC];    // R_s p from the pass
   double rho[MAXC];
   const double* pq;         // device, indexed by column
   unsigned mask;
@@ -274,10 +284,13 @@ hipError_t launch_cg_p(const ChunkDesc* d_ch, int nch, const PArgs& a, hipStream
 struct PostArgs {
   double* X[MAXC];
   const double* X0[MAXC];
+  double* RX[MAXC];         // carried R_s X (rs != 0): damped with X, dotted for gamw
+  const double* RXp[MAXC];
   const double* u[MAXK];
   const double* r[MAXK];
   int K;
   int damp;
+  int rs;
   double rho;
 };
 hipError_t launch_lmmse_post(const ChunkDesc* d_ch, int nch, const PostArgs& a, double* d_part,

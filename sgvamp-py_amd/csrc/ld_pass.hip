@@ -46,6 +46,7 @@ __global__ __launch_bounds__(256) void k_ld_pass(const BlkDesc* __restrict__ blk
   const double* ip = pa.in[0];
   double* op = pa.out[0];
   const double* dp = pa.dot[0];
+  double* yp = pa.yout[0];
   double c1 = pa.c1[0], c2 = pa.c2[0];
 #pragma unroll
   for (int c = 1; c < NC; ++c)
@@ -53,6 +54,7 @@ __global__ __launch_bounds__(256) void k_ld_pass(const BlkDesc* __restrict__ blk
       ip = pa.in[c];
       op = pa.out[c];
       dp = pa.dot[c];
+      yp = pa.yout[c];
       c1 = pa.c1[c];
       c2 = pa.c2[c];
     }
@@ -124,8 +126,10 @@ __global__ __launch_bounds__(256) void k_ld_pass(const BlkDesc* __restrict__ blk
     double contrib = 0.0;
     if (lane < RWI * NC && row < n) {
       const int64_t idx = bd.voff + row;
-      const double o = c1 * y + c2 * ip[idx];
+      const double in = ip[idx];
+      const double o = c1 * y + c2 * in;
       op[idx] = o;
+      if (yp) yp[idx] = pa.ys1 * y + pa.ys0 * in;
       if (dp) contrib = dp[idx] * o;
     }
     if (lane < RWI * NC) red[wid][h * RWI * NC + lane] = contrib;

@@ -177,8 +177,10 @@ __global__ __launch_bounds__(256) void k_sym_finalize(const SymPanel* __restrict
 #pragma unroll
     for (int c = 0; c < MAXC; ++c)
       if (c < ncol) {
-        const double o = pa.c1[c] * y[c] + pa.c2[c] * pa.in[c][idx];
+        const double in = pa.in[c][idx];
+        const double o = pa.c1[c] * y[c] + pa.c2[c] * in;
         pa.out[c][idx] = o;
+        if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * y[c] + pa.ys0 * in;
         if (pa.dot[c]) acc[c] = pa.dot[c][idx] * o;
       }
   }

@@ -185,7 +185,10 @@ __global__ __launch_bounds__(VTHREADS) void k_lmmse_init(const ChunkDesc* __rest
           acc[c] += b * b;
           acc[MAXC + c] += r * r;
         }
-        if (a.save_x0) a.col.X0[2 * k][i] = a.col.X[2 * k][i];
+        if (a.save_x0) {
+          a.col.X0[2 * k][i] = a.col.X[2 * k][i];
+          if (a.col.RXp[2 * k]) a.col.RXp[2 * k][i] = a.col.RX0[2 * k][i];
+        }
       }
   }
   block_reduce_store<INIT_NV>(acc, part + (int64_t)blockIdx.x * INIT_NV, INIT_NV);
@@ -217,6 +220,7 @@ __global__ __launch_bounds__(VTHREADS) void k_cg_xr(const ChunkDesc* __restrict_
     for (int c = 0; c < MAXC; ++c)
       if (c < a.ncol && ((a.mask >> c) & 1u)) {
         a.X[c][i] = a.X[c][i] + alpha[c] * a.P[c][i];
+        if (a.RX[c]) a.RX[c][i] = a.RX[c][i] + alpha[c] * a.Y[c][i];   // R_s x carried
         const double r = a.Rr[c][i] - alpha[c] * a.Q[c][i];
         a.Rr[c][i] = r;
         acc[c] += r * r;
@@ -248,11 +252,14 @@ hipError_t launch_cg_p(const ChunkDesc* d_ch, int nch, const PArgs& a, hipStream
 }
 
 // ---------------------------------------------------------------------------
-// after both CG solves (src/sgvamp.py:322-338,352):
+// after both CG solves (src/sgvamp.py:322-338,352,359):
 //   xhat2 damping; partials [k] = u.Sigma2_u, [MAXK + k] = xhat2.r,
-//   [2 MAXK + c] = count(x_c != 0)  (next iteration's x0.any())
+//   [2 MAXK + c] = count(x_c != 0)  (next iteration's x0.any()),
+//   with the carried products (rs): [2 MAXK + MAXC + k] = xhat2.R_s xhat2,
+//   [3 MAXK + MAXC + k] = u.R_s Sigma2_u
 // ---------------------------------------------------------------------------
-constexpr int POST_NV = 2 * MAXK + MAXC;
+constexpr int POST_NV = 4 * MAXK + MAXC;
+static_assert(POST_NV <= MAXNV, "post partials");
 __global__ __launch_bounds__(VTHREADS) void k_lmmse_post(const ChunkDesc* __restrict__ chs,
                                                          PostArgs a,
                                                          double* __restrict__ part) {
@@ -271,8 +278,18 @@ __global__ __launch_bounds__(VTHREADS) void k_lmmse_post(const ChunkDesc* __rest
           a.X[2 * k][i] = x2;
         }
         const double s2u = a.X[2 * k + 1][i];
-        acc[k] += a.u[k][i] * s2u;                          // :338
+        const double uk = a.u[k][i];
+        acc[k] += uk * s2u;                                 // :338
         acc[MAXK + k] += x2 * a.r[k][i];                    // :352
+        if (a.rs) {
+          double rx = a.RX[2 * k][i];
+          if (a.damp) {                                     // R_s is linear: damp with x
+            rx = a.rho * rx + (1 - a.rho) * a.RXp[2 * k][i];
+            a.RX[2 * k][i] = rx;
+          }
+          acc[2 * MAXK + MAXC + k] += x2 * rx;              // :352 xhat2^T R_s xhat2
+          acc[3 * MAXK + MAXC + k] += uk * a.RX[2 * k + 1][i];   // :359 u^T R_s Sigma2_u
+        }
         acc[2 * MAXK + 2 * k] += (x2 != 0.0) ? 1.0 : 0.0;
         acc[2 * MAXK + 2 * k + 1] += (s2u != 0.0) ? 1.0 : 0.0;
       }

@@ -84,6 +84,10 @@ class Engine:
         """Packed LD passes with >= nc_min right-hand sides use the f64 MFMA kernel."""
         self.ctx.sgv_set_mfma_min(int(nc_min))
 
+    def set_rs_recurrence(self, on):
+        """Carry R_s x through the CG (default) instead of a gamw LD pass."""
+        self.ctx.sgv_set_rs_recurrence(1 if on else 0)
+
     def set_ridge(self, s):
         self.ctx.sgv_set_ridge(float(s))
 

@@ -112,7 +112,7 @@ def common_partition(size_lists):
 class VAMP:
     def __init__(self, N, Nt, M, K, rho, gamw, gam1, a, prior_vars, prior_probs, out_dir,
                  out_name, comm=None, seed=None, device=None, write_files=True, ld_packing=True,
-                 exchange=None, mfma_min=None):
+                 exchange=None, mfma_min=None, rs_recurrence=None):
         # src/sgvamp.py:15-31
         self.eps = 1e-32
         self.K = int(K)
@@ -146,6 +146,7 @@ class VAMP:
         self.write_files = write_files
         self.ld_packing = ld_packing   # packed symmetric LD storage for symmetric blocks
         self.mfma_min = mfma_min       # None: library default (f64 MFMA pass from 3 RHS)
+        self.rs_recurrence = rs_recurrence   # None: library default (R_s x carried, no gamw pass)
         self.gam = None
         self.engine = None
         self.history = []
@@ -220,6 +221,8 @@ class VAMP:
         eng.set_ld_packing(self.ld_packing)
         if self.mfma_min is not None:
             eng.set_mfma_min(self.mfma_min)
+        if self.rs_recurrence is not None:
+            eng.set_rs_recurrence(self.rs_recurrence)
         eng.set_ridge(s_vals.pop())
         for l, L in enumerate(uniq):
             for b in range(eng.b0, eng.b1):

@@ -203,7 +203,7 @@ def test_denoise_and_em_vs_oracle(K, nslab):
 # ---------------------------------------------------------------------------
 # full VAMP vs the reference's golden outputs
 # ---------------------------------------------------------------------------
-def run_vamp_case(c, out_dir, device=None, ld_packing=True, mfma_min=None):
+def run_vamp_case(c, out_dir, device=None, ld_packing=True, mfma_min=None, rs_recurrence=None):
     f = c.flags
     lds = [BlockLD(blocks, s=f["s"]) for blocks in c.ld_blocks]
     R = lds[0] if len(lds) == 1 else [lds[c.ld_of[k]] for k in range(c.K)]
@@ -212,7 +212,7 @@ def run_vamp_case(c, out_dir, device=None, ld_packing=True, mfma_min=None):
     v = VAMP(N=c.N, Nt=Nt, M=c.M, K=c.K, rho=f["rho"], gamw=f["gamw"], gam1=f["gam1"], a=a,
              prior_vars=f["prior_vars"], prior_probs=f["prior_probs"], out_dir=str(out_dir),
              out_name=c.name, seed=f["seed"], device=device, ld_packing=ld_packing,
-             mfma_min=mfma_min)
+             mfma_min=mfma_min, rs_recurrence=rs_recurrence)
     xh = v.infer(R, c.r, f["iterations"], x0=c.x0, cg_maxit=f["cg_maxit"],
                  em_prior_maxit=f["em_prior_maxit"], learn_gamw=f["learn_gamw"],
                  lmmse_damp=f["lmmse_damp"], prior_update=f["prior_update"],
@@ -227,16 +227,19 @@ def read_tsv(path):
     return text, np.array(rows)
 
 
-@pytest.mark.parametrize("packing", [True, False, "valu"])
+@pytest.mark.parametrize("packing", [True, False, "valu", "direct"])
 @pytest.mark.parametrize("name", case_names())
 def test_vamp_matches_reference_golden(name, packing, tmp_path):
-    """packing True: packed storage (MFMA pass for K >= 2, i.e. >= 3 CG columns);
-    "valu": packed storage, VALU pass only; False: dense storage."""
+    """packing True: packed storage (MFMA pass for K >= 2, i.e. >= 3 CG columns),
+    R_s x carried through the CG (default); "valu": packed storage, VALU pass
+    only; False: dense storage; "direct": R_s xhat2 / R_s Sigma2_u by a separate
+    LD pass, as the reference computes them (src/sgvamp.py:352,359)."""
     c = Case(name)
     if packing == "valu" and c.K == 1:
         pytest.skip("K = 1 never reaches 3 columns: same as packing=True")
     v, xh = run_vamp_case(c, tmp_path, ld_packing=bool(packing),
-                          mfma_min=0 if packing == "valu" else None)
+                          mfma_min=0 if packing == "valu" else None,
+                          rs_recurrence=False if packing == "direct" else None)
     fmts = {v.engine.ld_block_format(l, b) for l in range(v.engine.nld)
             for b in range(len(v.engine.block_sizes))}
     assert fmts == {1 if packing else 0}
@@ -316,11 +319,13 @@ def test_synth_generator_vs_oracle(packed):
 # ---------------------------------------------------------------------------
 # medium scale: HIP VAMP vs oracle on device-generated data
 # ---------------------------------------------------------------------------
+@pytest.mark.parametrize("rs", [True, False])
 @pytest.mark.parametrize("prior", ["matched", "cli_default"])
-def test_vamp_medium_scale_vs_oracle(prior, tmp_path):
+def test_vamp_medium_scale_vs_oracle(prior, rs, tmp_path):
     """Rank-deficient blocks (n_b > N) like C2.  With the CLI default prior
     (slab variance 1*Nt, far above the simulated effect size) the trajectory
-    degenerates; the oracle does the same, step for step."""
+    degenerates; the oracle does the same, step for step.  rs: R_s x carried
+    through the CG (oracle cg_track) or by direct products."""
     sizes = [3000, 2500, 3500, 3000]
     nsamp = 2000
     M = sum(sizes)
@@ -341,12 +346,14 @@ def test_vamp_medium_scale_vs_oracle(prior, tmp_path):
              prior_vars=prior_vars, prior_probs=prior_probs, out_dir=str(tmp_path), out_name="m",
              seed=3, write_files=False)
     v.attach_engine(eng, x0=x0)
+    eng.set_rs_recurrence(rs)
     its = 6
     xh = v.infer(None, None, its, x0=x0, lmmse_damp=False, prior_update="em")
     L = vo.BlockLD(blocks)
     t = vo.infer([L], [0], [r], [nsamp], its, rho=0.5, gamw=5.0, gam1=1e-6,
                  prior_vars=prior_vars, prior_probs=prior_probs, x0=x0, seed=3,
-                 lmmse_damp=False, reducer=vo.Reducer("blocked", bounds=L.bounds))
+                 lmmse_damp=False, reducer=vo.Reducer("blocked", bounds=L.bounds),
+                 rs_recurrence=rs)
     for it in range(its):
         ref = np.asarray(t["xhat"][it])
         got = xh[it].ravel() / np.sqrt(nsamp)

@@ -12,12 +12,12 @@ from tests.golden import Case, case_names
 CASES = case_names()
 
 
-def run_oracle(c, mode="numpy"):
+def run_oracle(c, mode="numpy", rs_recurrence=False):
     lds = [vo.BlockLD(b, s=c.flags["s"]) for b in c.ld_blocks]
     red = vo.Reducer(mode, bounds=lds[0].bounds) if mode == "blocked" else None
     with np.errstate(all="ignore"):
         return vo.infer(lds, c.ld_of, list(c.r), c.N, c.flags["iterations"], x0=c.x0,
-                        reducer=red, **c.kwargs())
+                        reducer=red, rs_recurrence=rs_recurrence, **c.kwargs())
 
 
 def maxrel(a, b):
@@ -29,10 +29,13 @@ def test_fixtures_present():
     assert len(CASES) >= 7
 
 
+@pytest.mark.parametrize("rs", [False, True])
 @pytest.mark.parametrize("name", CASES)
-def test_oracle_matches_reference(name):
+def test_oracle_matches_reference(name, rs):
+    """rs=True: R_s x carried through the CG (cg_track, the build's default)
+    instead of the reference's direct products -- held to the same bar."""
     c = Case(name)
-    t = run_oracle(c)
+    t = run_oracle(c, rs_recurrence=rs)
     its = c.flags["iterations"]
     xh = np.array(t["xhat"])
     assert xh.shape == c.xhat.shape
@@ -45,9 +48,12 @@ def test_oracle_matches_reference(name):
     np.testing.assert_array_equal(cg, c.cg_iters)
     np.testing.assert_array_equal(np.array(t["cg_info"]).transpose(1, 0, 2), c.cg_info)
     assert list(t["em_steps"]) == list(c.em_steps)
-    # cohort CSV rows [it, gamw, gam1, gam2, alpha1, alpha2, lam]
+    # cohort CSV rows [it, gamw, gam1, gam2, alpha1, alpha2, lam].  gam2 =
+    # gam1 (1 - alpha1) / alpha1 amplifies rounding as alpha1 -> 0: the direct
+    # products stay within 1e-6 (observed 6e-7); the carried products differ
+    # from them by rounding and are held to the north star's 1e-5 (observed 1.1e-6)
     csv = np.array(t["csv"])
-    np.testing.assert_allclose(csv, c.cohort_csv, rtol=1e-6, atol=0)
+    np.testing.assert_allclose(csv, c.cohort_csv, rtol=1e-5 if rs else 1e-6, atol=0)
     np.testing.assert_allclose(np.array(t["metrics"]), c.metrics_csv, rtol=1e-9, atol=1e-12)
 
 
