@@ -133,9 +133,12 @@ __global__ __launch_bounds__(256) void k_sym_pass(const SymItem* __restrict__ it
 // one workgroup per panel; thread t = panel row r0 + t.  The item offsets of
 // the block's earlier panels are staged in LDS first, so the column-partial
 // loads of the panel loop are independent of each other (no descriptor load
-// in the chain) and can be kept in flight together.
-__global__ __launch_bounds__(256) void k_sym_finalize(const SymPanel* __restrict__ panels,
-                                                      int ncol, int cw, PassArgs pa,
+// in the chain) and, with NC a compile-time constant, unconditional: the
+// compiler keeps them in flight together instead of draining vmcnt at every
+// per-column branch.
+template <int NC>
+__global__ __launch_bounds__(256) void k_sym_finalize(const SymPanel* __restrict__ panels, int cw,
+                                                      PassArgs pa,
                                                       const double* __restrict__ rowpart,
                                                       const double* __restrict__ colpart,
                                                       double* __restrict__ partials) {
@@ -143,18 +146,15 @@ __global__ __launch_bounds__(256) void k_sym_finalize(const SymPanel* __restrict
   __shared__ int s_ib[PCH];
   const SymPanel pn = panels[blockIdx.x];
   const int t = threadIdx.x;
-  double acc[MAXC];
+  double y[NC];
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) acc[c] = 0.0;
-  double y[MAXC];
-#pragma unroll
-  for (int c = 0; c < MAXC; ++c) y[c] = 0.0;
+  for (int c = 0; c < NC; ++c) y[c] = 0.0;
   const int i = pn.r0 + (t < pn.H ? t : 0);   // block-relative row
   // this panel's row parts, chunk order
   for (int itm = pn.item_begin; itm < pn.item_end; ++itm) {
+    const double* rp = rowpart + ((int64_t)itm * SYM_H + t) * NC;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-      if (c < ncol) y[c] += ldg(rowpart + ((int64_t)itm * SYM_H + t) * ncol + c);
+    for (int c = 0; c < NC; ++c) y[c] += ldg(rp + c);
   }
   // column parts of the earlier panels of this block, panel order
   for (int g0 = 0; g0 < pn.g; g0 += PCH) {
@@ -166,25 +166,26 @@ __global__ __launch_bounds__(256) void k_sym_finalize(const SymPanel* __restrict
     for (int k = 0; k < gn; ++k) {
       const int rel = i - (g0 + k) * SYM_H;      // column relative to that panel's first row
       const int ch = rel / cw;
-      const int64_t base = ((int64_t)(s_ib[k] + ch) * ncol) * cw + (rel - ch * cw);
+      const double* cp = colpart + ((int64_t)(s_ib[k] + ch) * NC) * cw + (rel - ch * cw);
 #pragma unroll
-      for (int c = 0; c < MAXC; ++c)
-        if (c < ncol) y[c] += ldg(colpart + base + (int64_t)c * cw);
+      for (int c = 0; c < NC; ++c) y[c] += ldg(cp + (int64_t)c * cw);
     }
   }
+  double acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = 0.0;
   if (t < pn.H) {
     const int64_t idx = pn.voff + i;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-      if (c < ncol) {
-        const double in = pa.in[c][idx];
-        const double o = pa.c1[c] * y[c] + pa.c2[c] * in;
-        pa.out[c][idx] = o;
-        if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * y[c] + pa.ys0 * in;
-        if (pa.dot[c]) acc[c] = pa.dot[c][idx] * o;
-      }
+    for (int c = 0; c < NC; ++c) {
+      const double in = pa.in[c][idx];
+      const double o = pa.c1[c] * y[c] + pa.c2[c] * in;
+      pa.out[c][idx] = o;
+      if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * y[c] + pa.ys0 * in;
+      if (pa.dot[c]) acc[c] = pa.dot[c][idx] * o;
+    }
   }
-  block_reduce_store<MAXC>(acc, partials + (int64_t)pn.part * ncol, ncol);
+  block_reduce_store<NC>(acc, partials + (int64_t)pn.part * NC, NC);
 }
 
 template <int NC, int NSEG>
@@ -216,8 +217,19 @@ hipError_t launch_sym_pass(int nc, int cls, const SymItem* d_items, int nitems,
 hipError_t launch_sym_finalize(int nc, int cls, const SymPanel* d_panels, int npanels,
                                const PassArgs& pa, const double* rowpart, const double* colpart,
                                double* partials, hipStream_t st) {
-  hipLaunchKernelGGL(k_sym_finalize, dim3(npanels), dim3(256), 0, st, d_panels, nc, 1024 >> cls,
-                     pa, rowpart, colpart, partials);
+  const int cw = 1024 >> cls;
+#define FIN_CASE(N)                                                                              \
+  case N:                                                                                        \
+    hipLaunchKernelGGL(k_sym_finalize<N>, dim3(npanels), dim3(256), 0, st, d_panels, cw, pa,     \
+                       rowpart, colpart, partials);                                              \
+    break;
+  switch (nc) {
+    FIN_CASE(1) FIN_CASE(2) FIN_CASE(3) FIN_CASE(4) FIN_CASE(5) FIN_CASE(6) FIN_CASE(7) FIN_CASE(8)
+    FIN_CASE(9) FIN_CASE(10) FIN_CASE(11) FIN_CASE(12) FIN_CASE(13) FIN_CASE(14) FIN_CASE(15)
+    FIN_CASE(16)
+    default: return hipErrorInvalidValue;
+  }
+#undef FIN_CASE
   return hipGetLastError();
 }
 
