@@ -176,6 +176,20 @@ int sgv_em(sgv_ctx* ctx, const double* gam1s, const double* a, int nslab,
  *   probes: [K][M_local] int8 of +-1 (the host draws u, :326)
  *   out: [K][SGV_LMMSE_NOUT]; cg_out: [K][4] = iters1, info1, iters2, info2
  *   ld_passes_out: LD passes (full sweeps over all owned LD bytes) performed */
+/* MLE prior update (--prior-update mle, src/sgvamp.py:139-194).  The host runs
+ * the reference's scipy.optimize.fsolve on Lagrangian_der; these two calls
+ * compute its device-side parts over all markers and cohorts (the current r1
+ * vectors).  L = mixture components including the spike, sigma2[L] the
+ * component variances (sigma2[0] = 1e-16, :169-171).
+ * exp_max (:152): max over (k, m, l) of (-r1_km^2 / 2) / (sigma2_l + 1/gam1_k).
+ * sums[l] (:155-158): sum over k, m of a_k p_kml / sum_l' p_kml' omega_l', with
+ * p_kml = exp((-r1_km^2 / 2) / v_kl - exp_max) / sqrt(v_kl). */
+int sgv_mle_exp_max(sgv_ctx* ctx, const double* gam1s /* K */, int L, const double* sigma2,
+                    double* exp_max);
+int sgv_mle_terms(sgv_ctx* ctx, const double* a /* K */, const double* gam1s /* K */, int L,
+                  const double* sigma2 /* L */, const double* omega /* L */, double exp_max,
+                  double* sums /* L */);
+
 int sgv_lmmse(sgv_ctx* ctx, int it, const double* gamw, const double* gam2,
               const double* alpha1, const double* alpha2_prev, const int8_t* probes,
               int cg_maxit, double rtol, int lmmse_damp, double rho, int learn_gamw,

@@ -18,6 +18,8 @@ What it restates (reference file:line)
 * ``denoiser_meta``  src/sgvamp.py:93-102    vectorised over markers
 * ``der_denoiser_meta`` src/sgvamp.py:104-114 vectorised, all K cohorts at once
 * ``prior_update_em`` src/sgvamp.py:116-136  + driver loop :247-259
+* ``Lagrangian_der`` / ``prior_update_mle`` src/sgvamp.py:139-194 (scipy
+  ``optimize.fsolve``, MINPACK hybrd, as the reference calls it)
 * ``VAMP.infer``      src/sgvamp.py:196-389  all K cohort ranks in one process
 * scipy 1.15.3 ``cg`` scipy/sparse/linalg/_isolve/iterative.py:305-422 (the
   reference's ``con_grad``, src/sgvamp.py:7,316,332): rtol 1e-5, atol 0,
@@ -130,6 +132,74 @@ def prior_update_em(r1s, gam1s, a, lam, omegas, sigmas, red=None, M_total=None):
     den = (pi * a.reshape(K, 1, 1)).sum(axis=0).ravel()
     omegas_new = np.array([red.dot(num[:, l], ones) for l in range(Lm1)]) / red.dot(den, ones)
     return lam_new, omegas_new
+
+
+def lagrangian_der(x, omega0, sigma2, r1s, gam1s, a, exp_max, red=None):
+    """src/sgvamp.py:139-160 (Lagrangian_der).  ``exp_max`` (:152) depends only
+    on r1s, gam1s and sigma2, so it is computed once per update (mle_exp_max).
+    With a "blocked" reducer the marker sums go through it (sharded runs)."""
+    K, M = r1s.shape
+    L = len(sigma2)
+    y = np.zeros(L + 1)
+    omega = x[:L]
+    gam = x[L]
+    prior_vars0 = sigma2.reshape(1, 1, L)
+    gam1invs = 1.0 / gam1s.reshape(K, 1, 1)
+    r1s_rs = r1s.reshape(K, M, 1)
+    probs = np.exp(-np.power(r1s_rs, 2) / 2 / (prior_vars0 + gam1invs) - exp_max) \
+        / np.sqrt(prior_vars0 + gam1invs)                                        # :153
+    Num = a.reshape(K, 1, 1) * probs                                             # :154
+    Den = np.sum(probs * omega.reshape(1, 1, L), axis=2).reshape(K, M, 1)        # :155
+    if red is None or red.mode == "numpy":
+        S = np.sum(Num / Den, axis=(0, 1))                                       # :157
+    else:
+        T = Num / Den
+        t = T[0]
+        for k in range(1, K):
+            t = t + T[k]
+        ones = np.ones(M)
+        S = np.array([red.dot(t[:, l], ones) for l in range(L)])
+    y[:L] = S + (omega0 - 1) / omega + gam                                       # :157
+    y[L] = sum(omega) - 1.0                                                      # :158
+    return y
+
+
+def mle_exp_max(r1s, gam1s, sigma2, red=None):
+    """src/sgvamp.py:152: max over (k, m, l) of (-r1^2 / 2) / (sigma2_l + 1/gam1_k)."""
+    K, M = r1s.shape
+    L = len(sigma2)
+    v = sigma2.reshape(1, 1, L) + 1.0 / gam1s.reshape(K, 1, 1)
+    local = (-np.power(r1s.reshape(K, M, 1), 2) / 2 / v).max()
+    if red is not None and red.comm is not None:
+        return float(np.max(red.comm.allgather_blocks(np.array([local]))))
+    return local
+
+
+def prior_update_mle(r1s, gam1s, a, lam, omegas, sigmas, gam, red=None):
+    """src/sgvamp.py:162-194.  Returns (lam, omegas, gam, warning or None)."""
+    from scipy import optimize
+
+    L = len(sigmas) + 1
+    omega0 = np.zeros(L)
+    omega0[0] = 1 - lam
+    omega0[1:] = lam * omegas
+    sigma2 = np.zeros(L)
+    sigma2[0] = 1e-16
+    sigma2[1:] = sigmas
+    x0 = np.zeros(L + 1)
+    x0[:-1] = omega0
+    x0[-1] = 1 if gam is None else gam
+    em = mle_exp_max(r1s, gam1s, sigma2, red)
+    x, _, ier, _ = optimize.fsolve(func=lagrangian_der, x0=x0,
+                                   args=(omega0, sigma2, r1s, gam1s, a, em, red), full_output=True)
+    if ier != 1:                                                                 # :183-186
+        return lam, omegas, gam, "WARNING: fsolve not converged. No prior update!"
+    if any(s <= 0 for s in x[:-1]):                                              # :187-190
+        return lam, omegas, gam, "WARNING: Negative values in MLE. No prior update!"
+    x[:-1] /= sum(x[:-1])                                                        # :191
+    lam = 1 - x[0]
+    omegas = np.array([w / sum(x[1:-1]) for w in x[1:-1]])
+    return lam, omegas, x[L], None
 
 
 # ----------------------------------------------------------------------------
@@ -318,7 +388,9 @@ def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-
     alpha1_k = [0] * K
     alpha2_k = [0] * K
     traj = dict(xhat=[], r1=[], csv=[[] for _ in range(K)], metrics=[], cg_iters=[],
-                cg_info=[], em_steps=[], gamws=[[] for _ in range(K)], ld_passes=[])
+                cg_info=[], em_steps=[], gamws=[[] for _ in range(K)], ld_passes=[],
+                mle_warnings=[])
+    gam_mle = None                                                       # :31 self.gam
 
     for it in range(iterations):
         gam1s = np.array(gam1_k, dtype=np.float64)                      # :228-233
@@ -332,8 +404,11 @@ def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-
                 if om_err < 1e-6 and lam_err < 1e-6:
                     break
             traj["em_steps"].append(em_it + 1)
-        elif it >= update_prior_from and prior_update == "mle":
-            raise NotImplementedError("MLE prior update is outside the oracle's scope")
+        elif it >= update_prior_from and prior_update == "mle":          # :244-246
+            lam, omegas, gam_mle, warn = prior_update_mle(r1s, gam1s, a, lam, omegas, sigmas,
+                                                          gam_mle, red)
+            if warn:
+                traj["mle_warnings"].append(warn)
 
         xhat1_prev = xhat1
         xhat1 = denoiser_meta(r1s, gam1s, a, lam, omegas, sigmas)       # :273

@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <limits>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -220,8 +221,9 @@ static void resolve_timers(sgv_ctx* c) {
 }
 
 // partials [nparts][nv] -> d_dst[map.d[v]] (global, ordered); stays on device
-static int reduce_dev(sgv_ctx* c, int nv, const int* d_begin, const Map16& map, double* d_dst) {
-  HIPCHK(launch_reduce_blocks(c->d_part, nv, d_begin, c->nblk, c->d_bsum, c->st));
+static int reduce_dev(sgv_ctx* c, int nv, const int* d_begin, const Map16& map, double* d_dst,
+                      int op = 0) {
+  HIPCHK(launch_reduce_blocks(c->d_part, nv, d_begin, c->nblk, c->d_bsum, c->st, op));
   const double* src = c->d_bsum;
   int nr = 1, nbm = c->nblk;
   if (c->comm) {
@@ -242,12 +244,12 @@ static int reduce_dev(sgv_ctx* c, int nv, const int* d_begin, const Map16& map, 
     nr = c->nranks;
     nbm = c->nbmax;
   }
-  HIPCHK(launch_reduce_total(src, nr, nbm, nv, c->d_counts, map, d_dst, c->st));
+  HIPCHK(launch_reduce_total(src, nr, nbm, nv, c->d_counts, map, d_dst, c->st, op));
   return SGV_OK;
 }
 
-static int reduce_host(sgv_ctx* c, int nv, const int* d_begin, double* out) {
-  CHK(reduce_dev(c, nv, d_begin, identity_map(), c->d_tot));
+static int reduce_host(sgv_ctx* c, int nv, const int* d_begin, double* out, int op = 0) {
+  CHK(reduce_dev(c, nv, d_begin, identity_map(), c->d_tot, op));
   HIPCHK(hipMemcpyAsync(c->h_tot, c->d_tot, sizeof(double) * nv, hipMemcpyDeviceToHost, c->st));
   CHK(stream_wait(c));
   resolve_timers(c);
@@ -1193,6 +1195,60 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
 // ---------------------------------------------------------------------------
 // LMMSE (src/sgvamp.py:301-364)
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// MLE prior update (src/sgvamp.py:139-194): the K x M x L sums of
+// Lagrangian_der on the device; fsolve (MINPACK hybrd) stays on the host
+// ---------------------------------------------------------------------------
+static int mle_args(sgv_ctx* c, const double* gam1s, int L, const double* sigma2, MleArgs* m) {
+  if (!gam1s || !sigma2 || L < 1 || L > MAXL + 1) return fail(c, SGV_ERR_ARG, "bad MLE arguments");
+  *m = MleArgs{};
+  m->K = c->K;
+  m->L = L;
+  for (int k = 0; k < c->K; ++k) {
+    m->r1[k] = c->r1[k];
+    const double ginv = 1.0 / gam1s[k];                       // :146
+    for (int l = 0; l < L; ++l) {
+      m->v[k][l] = sigma2[l] + ginv;                          // prior_vars0 + gam1invs
+      m->sv[k][l] = std::sqrt(m->v[k][l]);
+    }
+  }
+  return SGV_OK;
+}
+
+extern "C" int sgv_mle_exp_max(sgv_ctx* c, const double* gam1s, int L, const double* sigma2,
+                               double* exp_max) {
+  ENTER(c);
+  if (!exp_max) return fail(c, SGV_ERR_ARG, "exp_max is null");
+  MleArgs m;
+  CHK(mle_args(c, gam1s, L, sigma2, &m));
+  HIPCHK(launch_mle_minsq(c->d_ch, c->nch, m, c->d_part, c->st));
+  double mn[MAXK];
+  CHK(reduce_host(c, MAXK, c->d_ch_begin, mn, /*op=min*/ 1));
+  // :152: max over (k, m, l) of (-r1^2 / 2) / v_kl, attained at min_m r1_km^2
+  double best = -std::numeric_limits<double>::infinity();
+  for (int k = 0; k < c->K; ++k)
+    for (int l = 0; l < L; ++l) best = std::max(best, -mn[k] / 2.0 / m.v[k][l]);
+  *exp_max = best;
+  return SGV_OK;
+}
+
+extern "C" int sgv_mle_terms(sgv_ctx* c, const double* a, const double* gam1s, int L,
+                             const double* sigma2, const double* omega, double exp_max,
+                             double* sums) {
+  ENTER(c);
+  if (!a || !omega || !sums) return fail(c, SGV_ERR_ARG, "bad MLE arguments");
+  MleArgs m;
+  CHK(mle_args(c, gam1s, L, sigma2, &m));
+  for (int k = 0; k < c->K; ++k) m.a[k] = a[k];
+  for (int l = 0; l < L; ++l) m.omega[l] = omega[l];
+  m.exp_max = exp_max;
+  HIPCHK(launch_mle_terms(c->d_ch, c->nch, m, c->d_part, c->st));
+  double tot[MAXL + 1];
+  CHK(reduce_host(c, MAXL + 1, c->d_ch_begin, tot));
+  for (int l = 0; l < L; ++l) sums[l] = tot[l];
+  return SGV_OK;
+}
+
 extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* gam2,
                          const double* alpha1, const double* alpha2_prev, const int8_t* probes,
                          int cg_maxit, double rtol, int lmmse_damp, double rho, int learn_gamw,

@@ -193,11 +193,12 @@ hipError_t launch_sym_finalize(int nc, int cls, const SymPanel* d_panels, int np
 // [begin[b], begin[b+1]) -> bsum[b * nv + v] (fixed order), then
 // total[v] = sum over all ranks' blocks in global block order, written to
 // dst[map.d[v]].
+// op 0: ordered sum; op 1: min (exact in any order)
 hipError_t launch_reduce_blocks(const double* d_part, int nv, const int* d_begin, int nblk,
-                                double* d_bsum, hipStream_t st);
+                                double* d_bsum, hipStream_t st, int op = 0);
 hipError_t launch_reduce_total(const double* d_bsum_all, int nranks, int nbmax, int nv,
                                const int* d_counts, const Map16& map, double* d_dst,
-                               hipStream_t st);
+                               hipStream_t st, int op = 0);
 
 // Vector kernels (vec.hip) ------------------------------------------------
 struct DenoiseArgs {
@@ -216,6 +217,20 @@ struct DenoiseArgs {
 };
 hipError_t launch_denoise(const ChunkDesc* d_ch, int nch, const DenoiseArgs& a, double* d_part,
                           hipStream_t st);
+
+struct MleArgs {
+  const double* r1[MAXK];
+  double a[MAXK];
+  double v[MAXK][MAXL + 1];    // prior_vars0 + 1/gam1_k (:148-155), spike first
+  double sv[MAXK][MAXL + 1];   // sqrt(v)
+  double omega[MAXL + 1];
+  double exp_max;
+  int K, L;                    // L = components incl. the spike (reference self.L)
+};
+hipError_t launch_mle_minsq(const ChunkDesc* d_ch, int nch, const MleArgs& a, double* d_part,
+                            hipStream_t st);
+hipError_t launch_mle_terms(const ChunkDesc* d_ch, int nch, const MleArgs& a, double* d_part,
+                            hipStream_t st);
 
 struct EmArgs {
   const double* r1[MAXK];

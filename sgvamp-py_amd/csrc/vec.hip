@@ -426,29 +426,37 @@ hipError_t launch_pack(const ChunkDesc* d_ch, int nch, const int64_t* d_doff, co
 // ---------------------------------------------------------------------------
 // ordered reductions
 // ---------------------------------------------------------------------------
-// grid (nblk, nv), one wave: bsum[b * nv + v] = sum of parts [begin[b], begin[b+1])
+// grid (nblk, nv), one wave: bsum[b * nv + v] = sum (op 0) or min (op 1) of parts
+// [begin[b], begin[b+1])
 __global__ __launch_bounds__(WAVE) void k_reduce_blocks(const double* __restrict__ part, int nv,
                                                         const int* __restrict__ begin,
-                                                        double* __restrict__ bsum) {
+                                                        double* __restrict__ bsum, int op) {
   const int b = blockIdx.x, v = blockIdx.y, lane = threadIdx.x;
   const int p0 = begin[b], p1 = begin[b + 1];
-  double s = 0.0;
-  for (int p = p0 + lane; p < p1; p += WAVE) s += part[(int64_t)p * nv + v];
-  s = wave_sum(s);
-  if (lane == 0) bsum[(int64_t)b * nv + v] = s;
+  if (op == 0) {
+    double s = 0.0;
+    for (int p = p0 + lane; p < p1; p += WAVE) s += part[(int64_t)p * nv + v];
+    s = wave_sum(s);
+    if (lane == 0) bsum[(int64_t)b * nv + v] = s;
+  } else {
+    double s = __builtin_inf();
+    for (int p = p0 + lane; p < p1; p += WAVE) s = fmin(s, part[(int64_t)p * nv + v]);
+    for (int o = 32; o > 0; o >>= 1) s = fmin(s, __shfl_xor(s, o, WAVE));
+    if (lane == 0) bsum[(int64_t)b * nv + v] = s;
+  }
 }
 
 hipError_t launch_reduce_blocks(const double* d_part, int nv, const int* d_begin, int nblk,
-                                double* d_bsum, hipStream_t st) {
+                                double* d_bsum, hipStream_t st, int op) {
   hipLaunchKernelGGL(k_reduce_blocks, dim3(nblk, nv), dim3(WAVE), 0, st, d_part, nv, d_begin,
-                     d_bsum);
+                     d_bsum, op);
   return hipGetLastError();
 }
 
 // total[v] = sum over ranks r, local blocks b < counts[r] (global block order)
 __global__ void k_reduce_total(const double* __restrict__ bsum_all, int nranks, int nbmax, int nv,
                                const int* __restrict__ counts, Map16 map,
-                               double* __restrict__ dst) {
+                               double* __restrict__ dst, int op) {
   const int v = threadIdx.x;
   if (v >= nv) return;
   double s = 0.0;
@@ -457,7 +465,7 @@ __global__ void k_reduce_total(const double* __restrict__ bsum_all, int nranks, 
     const int nb = counts[r];
     for (int b = 0; b < nb; ++b) {
       const double x = bsum_all[((int64_t)r * nbmax + b) * nv + v];
-      s = first ? x : s + x;
+      s = first ? x : (op == 0 ? s + x : fmin(s, x));
       first = false;
     }
   }
@@ -466,9 +474,90 @@ __global__ void k_reduce_total(const double* __restrict__ bsum_all, int nranks, 
 
 hipError_t launch_reduce_total(const double* d_bsum_all, int nranks, int nbmax, int nv,
                                const int* d_counts, const Map16& map, double* d_dst,
-                               hipStream_t st) {
+                               hipStream_t st, int op) {
   hipLaunchKernelGGL(k_reduce_total, dim3(1), dim3(64), 0, st, d_bsum_all, nranks, nbmax, nv,
-                     d_counts, map, d_dst);
+                     d_counts, map, d_dst, op);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// MLE prior update (src/sgvamp.py:139-160, Lagrangian_der)
+// ---------------------------------------------------------------------------
+// min over markers of r1_k^2 per cohort (partials [k], stride MAXK; min reduce).
+// The reference's exp_max = max_{k,m,l} (-r1_km^2 / 2) / v_kl is monotone in
+// r1^2 (also in floating point), so it is attained at min_m r1_km^2.
+__global__ __launch_bounds__(VTHREADS) void k_mle_minsq(const ChunkDesc* __restrict__ chs,
+                                                        MleArgs a, double* __restrict__ part) {
+  __shared__ double sm[VTHREADS / WAVE][MAXK];
+  const ChunkDesc ch = chs[blockIdx.x];
+  double mn[MAXK];
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) mn[k] = __builtin_inf();
+  CHUNK_LOOP(ch) {
+    const int64_t i = ch.voff + t;
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k)
+      if (k < a.K) {
+        const double r = a.r1[k][i];
+        mn[k] = fmin(mn[k], r * r);
+      }
+  }
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    double v = mn[k];
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, WAVE));
+    if (lane == 0) sm[wid][k] = v;
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < MAXK) {
+    const int k = threadIdx.x;
+    part[(int64_t)blockIdx.x * MAXK + k] = fmin(fmin(sm[0][k], sm[1][k]), fmin(sm[2][k], sm[3][k]));
+  }
+}
+
+hipError_t launch_mle_minsq(const ChunkDesc* d_ch, int nch, const MleArgs& a, double* d_part,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(k_mle_minsq, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part);
+  return hipGetLastError();
+}
+
+// S_l = sum_{k,m} a_k p_kml / Den_km with p_kml = exp(-r1^2/2/v_kl - exp_max) / sqrt(v_kl),
+// Den_km = sum_l p_kml omega_l (:153-158; the same operation order per element)
+constexpr int MLE_NV = MAXL + 1;
+static_assert(MLE_NV <= MAXNV, "mle partials");
+__global__ __launch_bounds__(VTHREADS) void k_mle_terms(const ChunkDesc* __restrict__ chs,
+                                                        MleArgs a, double* __restrict__ part) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  double acc[MLE_NV];
+#pragma unroll
+  for (int l = 0; l < MLE_NV; ++l) acc[l] = 0.0;
+  CHUNK_LOOP(ch) {
+    const int64_t i = ch.voff + t;
+#pragma unroll
+    for (int k = 0; k < MAXK; ++k)
+      if (k < a.K) {
+        const double r = a.r1[k][i];
+        const double nr2 = -(r * r);
+        double p[MLE_NV];
+        double den = 0.0;
+#pragma unroll
+        for (int l = 0; l < MLE_NV; ++l)
+          if (l < a.L) {
+            p[l] = exp(nr2 / 2.0 / a.v[k][l] - a.exp_max) / a.sv[k][l];
+            den = (l == 0) ? p[l] * a.omega[l] : den + p[l] * a.omega[l];
+          }
+#pragma unroll
+        for (int l = 0; l < MLE_NV; ++l)
+          if (l < a.L) acc[l] += a.a[k] * p[l] / den;
+      }
+  }
+  block_reduce_store<MLE_NV>(acc, part + (int64_t)blockIdx.x * MLE_NV, MLE_NV);
+}
+
+hipError_t launch_mle_terms(const ChunkDesc* d_ch, int nch, const MleArgs& a, double* d_part,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(k_mle_terms, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part);
   return hipGetLastError();
 }
 

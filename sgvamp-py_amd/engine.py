@@ -139,6 +139,21 @@ class Engine:
                         int(maxit), hb.dptr(lam_io), hb.dptr(om), hb.iptr(steps), hb.dptr(err))
         return float(lam_io[0]), om, int(steps[0]), float(err[0])
 
+    def mle_exp_max(self, gam1s, sigma2):
+        """max over (k, m, l) of (-r1_km^2 / 2) / (sigma2_l + 1/gam1_k) (src/sgvamp.py:152)."""
+        out = np.zeros(1)
+        sg = hb.f64(sigma2)
+        self.ctx.sgv_mle_exp_max(hb.dptr(hb.f64(gam1s)), len(sg), hb.dptr(sg), hb.dptr(out))
+        return float(out[0])
+
+    def mle_terms(self, a, gam1s, sigma2, omega, exp_max):
+        """The L marker sums of Lagrangian_der (src/sgvamp.py:153-157)."""
+        sg = hb.f64(sigma2)
+        out = np.zeros(len(sg))
+        self.ctx.sgv_mle_terms(hb.dptr(hb.f64(a)), hb.dptr(hb.f64(gam1s)), len(sg), hb.dptr(sg),
+                               hb.dptr(hb.f64(omega)), float(exp_max), hb.dptr(out))
+        return out
+
     def lmmse(self, it, gamw, gam2, alpha1, alpha2_prev, probes_local, cg_maxit, lmmse_damp, rho,
               learn_gamw, rtol=1e-5):
         K = self.K

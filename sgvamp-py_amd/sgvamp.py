@@ -338,7 +338,9 @@ class VAMP:
             if st["prior_update"] == "mle":
                 if rank == 0:
                     logging.info("...Updating prior parameters using MLE")
-                self.prior_update_mle(gam1s)
+                warn = self.prior_update_mle(gam1s)
+                if warn:
+                    rec["mle_warning"] = warn
             elif st["prior_update"] == "em":
                 if rank == 0:
                     logging.info("...Updating prior parameters using EM")
@@ -422,6 +424,50 @@ class VAMP:
         self.history.append(rec)
         return rec
 
+    def Lagrangian_der(self, x, omega0, sigma2, gam1s, exp_max):
+        """src/sgvamp.py:139-160.  The K x M x L marker sums run on the device over
+        the current r1 vectors (sgv_mle_terms); the rest is the reference's host
+        arithmetic.  exp_max (:152) depends only on r1, gam1s and sigma2 and is
+        computed once per update."""
+        L = self.L
+        y = np.zeros(L + 1)
+        omega = x[:L]
+        gam = x[L]
+        S = self.engine.mle_terms(self.a, gam1s, sigma2, omega, exp_max)
+        y[:L] = S + (omega0 - 1) / omega + gam
+        y[L] = sum(omega) - 1.0
+        return y
+
     def prior_update_mle(self, gam1s):
-        raise NotImplementedError("--prior-update mle (src/sgvamp.py:139-194) is not implemented "
-                                  "yet; use em")
+        """src/sgvamp.py:162-194: scipy's fsolve (MINPACK hybrd) on the host, as
+        the reference calls it, on the device-side Lagrangian."""
+        from scipy import optimize
+
+        omega0 = np.zeros(self.L)
+        omega0[0] = 1 - self.lam
+        omega0[1:] = self.lam * self.omegas
+        sigma2 = np.zeros(self.L)
+        sigma2[0] = 1e-16
+        sigma2[1:] = self.sigmas
+        x0 = np.zeros(self.L + 1)
+        x0[:-1] = omega0
+        if self.gam is None:
+            x0[-1] = 1
+        else:
+            x0[-1] = self.gam
+        exp_max = self.engine.mle_exp_max(gam1s, sigma2)
+        x, _, ier, _ = optimize.fsolve(func=self.Lagrangian_der, x0=x0,
+                                       args=(omega0, sigma2, gam1s, exp_max), full_output=True)
+        if ier != 1:
+            if self.rank == 0:
+                logging.info("WARNING: fsolve not converged. No prior update!")
+            return "WARNING: fsolve not converged. No prior update!"
+        elif any(s <= 0 for s in x[:-1]):
+            if self.rank == 0:
+                logging.info("WARNING: Negative values in MLE. No prior update!")
+            return "WARNING: Negative values in MLE. No prior update!"
+        x[:-1] /= sum(x[:-1])
+        self.lam = 1 - x[0]
+        self.omegas = np.array([w / sum(x[1:-1]) for w in x[1:-1]])
+        self.gam = x[self.L]
+        return None

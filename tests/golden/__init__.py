@@ -45,6 +45,8 @@ class Case:
         self.cg_info = d["cg_info"]
         self.em_steps = d["em_steps"]
         self.lam0_repr = str(d["lam0_repr"])
+        # the reference's "WARNING: ..." log lines (MLE: fsolve not converged / negative weights)
+        self.warnings = json.loads(str(d["warnings"])) if "warnings" in d.files else []
 
     @property
     def x0(self):

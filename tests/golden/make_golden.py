@@ -228,6 +228,15 @@ CASES = {
     # K=1, three-component prior (two slabs) -> multi-slab denoiser + EM omegas
     "k1_L3": dict(seed=16, M=400, N=[1500], blocks=[200, 200], iterations=10,
                   prior="auto3", lam_sim=0.1),
+    # MLE prior update (src/sgvamp.py:139-194, scipy fsolve), K=1 two components
+    "k1_mle": dict(seed=18, M=400, N=[1500], blocks=[200, 200], iterations=8,
+                   prior="auto", lam_sim=0.1, prior_update="mle"),
+    # MLE, K=2 shared LD, three components (two slabs)
+    "k2_mle_L3": dict(seed=19, M=360, N=[1200, 1800], blocks=[180, 180], iterations=8,
+                      prior="auto3", lam_sim=0.1, prior_update="mle"),
+    # MLE with the CLI default prior (slab variance far above the effect size)
+    "k1_mle_defaults": dict(seed=20, M=300, N=[1000], blocks=[300], iterations=6,
+                            prior_update="mle"),
     # K=4 shared LD, s>0, damping on, EM from iteration 2 (C5-like, small)
     "k4_shared_s_damp": dict(seed=17, M=320, N=[1000, 1200, 1400, 1600],
                              blocks=[160, 160], iterations=8, s=0.05, lmmse_damp=1,
@@ -304,6 +313,7 @@ def make_case(name, spec, workdir):
         metrics_csv=mrows, metrics_csv_text=np.array(mt),
         cg_iters=cg[..., 0], cg_info=cg[..., 1], em_steps=em,
         lam0_repr=np.array(results[0][3]),
+        warnings=np.array(json.dumps(list(results[0][2]))),
     )
     # R is block-diagonal by construction: store only the diagonal blocks,
     # concatenated row-major, one row per distinct LD matrix.

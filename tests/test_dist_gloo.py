@@ -76,7 +76,8 @@ def _single(case_name):
                         reducer=red, **c.kwargs())
 
 
-@pytest.mark.parametrize("case_name", ["k2_shared", "k1_blocks_csr_s_damp", "k4_shared_s_damp"])
+@pytest.mark.parametrize("case_name", ["k2_shared", "k1_blocks_csr_s_damp", "k4_shared_s_damp",
+                                       "k1_mle", "k2_mle_L3"])
 def test_two_rank_sharded_run_is_bit_identical(case_name):
     world = 2
     ctx = mp.get_context("fork")

@@ -259,6 +259,7 @@ def test_vamp_matches_reference_golden(name, packing, tmp_path):
     np.testing.assert_array_equal(info, c.cg_info)
     em = [h["em_steps"] for h in v.history if "em_steps" in h]
     assert em == list(c.em_steps)
+    assert [h["mle_warning"] for h in v.history if "mle_warning" in h] == c.warnings
     for k in range(c.K):
         text, rows = read_tsv(tmp_path / ("%s_cohort_%d.csv" % (name, k + 1)))
         assert text.splitlines()[0] == c.cohort_csv_text[k].splitlines()[0]

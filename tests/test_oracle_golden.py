@@ -48,6 +48,7 @@ def test_oracle_matches_reference(name, rs):
     np.testing.assert_array_equal(cg, c.cg_iters)
     np.testing.assert_array_equal(np.array(t["cg_info"]).transpose(1, 0, 2), c.cg_info)
     assert list(t["em_steps"]) == list(c.em_steps)
+    assert t["mle_warnings"] == c.warnings
     # cohort CSV rows [it, gamw, gam1, gam2, alpha1, alpha2, lam].  gam2 =
     # gam1 (1 - alpha1) / alpha1 amplifies rounding as alpha1 -> 0: the direct
     # products stay within 1e-6 (observed 6e-7); the carried products differ
