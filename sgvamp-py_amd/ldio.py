@@ -6,6 +6,11 @@
               detected from indptr/indices), or the build's block manifest
               ``*.blocks.json`` = {"block_sizes": [...], "files": [one .npy per
               block]} for LD that cannot exist as one dense array (M = 1e6).
+* PLINK .ld text LD (main.py:203-257): per cohort a CSR matrix with a unit
+              diagonal and every listed pair in both triangles (duplicates summed, as
+              scipy's COO -> CSR does); markers a cohort lacks are filled from another
+              cohort (the reference's MPI point-to-point exchange, emulated here in one
+              process: load_plink_ld_all)
 * true signal: .bin (f64) / .npy, multiplied by sqrt(N) (main.py:268-285)
 """
 import json
@@ -71,8 +76,82 @@ def load_ld(path, s):
         sizes = [int(b) for b in man["block_sizes"]]
         return BlockLD(block_sizes=sizes, loader=lambda b: np.load(files[b], mmap_mode="r"), s=s)
     if path.endswith(".ld"):
-        raise Exception("PLINK .ld text LD is not supported yet; convert it to .npz")
+        raise Exception("PLINK .ld LD needs every cohort's .ld and .bim: use load_plink_ld_all")
     raise Exception("Unsupported R matrix format!")
+
+
+def plink_ld_sources(bim_ref, bim_list, N_list):
+    """src/main.py:151-162: for cohort k and reference marker i, the cohort k asks
+    for marker i (== k: k holds it).  Reproduced as the reference computes it:
+    kx = argmax of N over the OTHER cohorts holding the marker is a position in
+    that list, used as a cohort id (main.py:161-162), so a marker may be asked of
+    a cohort that lacks it (then nothing arrives and r stays 0), or of k itself
+    (never requested)."""
+    M = len(bim_ref)
+    K = len(bim_list)
+    idx = {rs: i for i, rs in enumerate(bim_ref)}
+    sets = [set(b) for b in bim_list]
+    out = []
+    for k in range(K):
+        source = np.ones(M) * k
+        for rs in list(set(bim_ref) - sets[k]):
+            idx_rs = [j for j in range(K) if j != k and rs in sets[j]]
+            kx = np.argmax(np.array(N_list)[idx_rs])
+            source[idx[rs]] = kx
+        out.append(source)
+    return out
+
+
+def read_plink_ld(path, idx):
+    """One PLINK --r table (columns SNP_A, SNP_B, R): reference-indexed pairs."""
+    import pandas as pd
+
+    df = pd.read_table(path, sep=r"\s+")
+    indA = [idx[rs] for rs in list(df["SNP_A"])]
+    indB = [idx[rs] for rs in list(df["SNP_B"])]
+    return indA, indB, list(df["R"])
+
+
+def load_plink_ld_all(ld_paths, r, bim_ref, bim_list, N_list):
+    """All cohorts' .ld files -> (per-cohort scipy CSR R, updated r (K, M)).
+
+    src/main.py:203-257 with the exchange between cohort ranks done in one
+    process, in the reference's order: cohort k asks cohort j (j != k) for the
+    markers with source[k] == j; j answers with every entry of ITS OWN .ld that
+    touches a requested marker -- once per requested endpoint, so a pair whose
+    two markers were both requested arrives twice and, summed, doubles -- and
+    with its r at those markers; k appends the answers of j = 0..K-1 to its own
+    entries and overwrites r[source == j].  R = I + pairs + transposed pairs."""
+    import scipy.sparse
+
+    K = len(ld_paths)
+    M = len(bim_ref)
+    idx = {rs: i for i, rs in enumerate(bim_ref)}
+    own = [read_plink_ld(p, idx) for p in ld_paths]
+    sources = plink_ld_sources(bim_ref, bim_list, N_list)
+    r_in = np.asarray(r, dtype=np.float64)
+    r_out = r_in.copy()
+    mats = []
+    for k in range(K):
+        indA, indB, R_col = list(own[k][0]), list(own[k][1]), list(own[k][2])
+        source = sources[k]
+        for j in range(K):
+            if j == k or j not in source:
+                continue
+            req = [i for i in range(M) if source[i] == j]
+            jA, jB, jC = own[j]
+            for ind in req:
+                for i, corr in enumerate(jC):
+                    if jA[i] == ind or jB[i] == ind:
+                        indA.append(jA[i])
+                        indB.append(jB[i])
+                        R_col.append(corr)
+            r_out[k][source == j] = r_in[j][req]
+        ind_r = list(range(M)) + indA + indB
+        ind_c = list(range(M)) + indB + indA
+        v = np.array(list(np.ones(M)) + R_col + R_col)
+        mats.append(scipy.sparse.csr_matrix((v, (ind_r, ind_c)), shape=(M, M)))
+    return mats, r_out
 
 
 def load_true_signal(path, M, N):

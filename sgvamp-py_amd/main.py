@@ -26,7 +26,8 @@ if HERE not in sys.path:
     sys.path.insert(0, HERE)
 
 from comm import world_from_env  # noqa: E402
-from ldio import load_ld, load_r, load_true_signal, merge_bims  # noqa: E402
+from ldio import load_ld, load_plink_ld_all, load_r, load_true_signal, merge_bims  # noqa: E402
+from sgvamp import BlockLD  # noqa: E402
 from sgvamp import VAMP  # noqa: E402
 
 
@@ -154,13 +155,23 @@ def main(argv=None):
     r = np.stack([load_r(r_fpaths_list[k], M_list[k], N_list[k], i_maps[k], M) for k in range(K)])
     by_path = {}
     lds = []
-    for k in range(K):
-        p = ld_fpaths_list[k]
-        if p not in by_path:
-            by_path[p] = load_ld(p, s)
-        lds.append(by_path[p])
-        if lds[-1].M != M:
-            raise Exception(f"LD matrix {p} has {lds[-1].M} markers, expected {M}")
+    if any(p.endswith(".ld") for p in ld_fpaths_list):
+        # PLINK text LD: every cohort's table plus the missing-marker exchange (main.py:203-257)
+        if bim_fpaths is None or not all(p.endswith(".ld") for p in ld_fpaths_list):
+            raise Exception("PLINK .ld LD needs --bim-files and a .ld file for every cohort")
+        mats, r = load_plink_ld_all(ld_fpaths_list, r, bim_ref, bim_list, N_list)
+        for k in range(K):
+            by_path[k] = BlockLD.from_csr(mats[k], s=s)
+            lds.append(by_path[k])
+    else:
+        for k in range(K):
+            p = ld_fpaths_list[k]
+            if p not in by_path:
+                by_path[p] = load_ld(p, s)
+            lds.append(by_path[p])
+    for L in lds:
+        if L.M != M:
+            raise Exception(f"LD matrix has {L.M} markers, expected {M}")
     if rank == 0:
         logging.info(f"Loaded {len(by_path)} LD matrix/matrices, blocks {lds[0].block_sizes[:8]}"
                      f"{'...' if len(lds[0].block_sizes) > 8 else ''}\n")

@@ -102,3 +102,83 @@ def test_cli_flags_and_defaults_match_reference():
                       "--lmmse-damp", "1", "--learn-gamw", "0", "--prior-update", "none"])
     assert (a.ld_files, a.r_files, a.N, a.M, a.K, a.lmmse_damp, a.learn_gamw,
             a.prior_update) == ("x", "y", "10,20", "5,5", "2", "1", "0", "none")
+
+
+# ---------------------------------------------------------------------------
+# PLINK .ld text LD (src/main.py:151-162, 203-257).  The reference's exchange
+# runs over mpi4py point-to-point messages; mpi4py is absent here, so these
+# expectations are derived by hand from that code (parity unpinned by a run of
+# the reference), including its two quirks.
+# ---------------------------------------------------------------------------
+def write_ld(path, rows):
+    with open(path, "w") as f:
+        f.write(" CHR_A BP_A SNP_A CHR_B BP_B SNP_B R\n")
+        for a, b, r in rows:
+            f.write(" 1 0 %s 1 0 %s %r\n" % (a, b, r))
+
+
+def test_plink_ld_exchange_two_cohorts(tmp_path):
+    from ldio import load_plink_ld_all, plink_ld_sources
+
+    names = ["A", "B", "C", "D", "E"]
+    write_bim(tmp_path / "c0.bim", names, [1, 2, 3, 4, 5])
+    write_bim(tmp_path / "c1.bim", ["A", "B", "C"], [1, 2, 3])
+    df, lists = merge_bims([str(tmp_path / "c0.bim"), str(tmp_path / "c1.bim")])
+    ref = list(df["Variant"])
+    assert ref == names
+    write_ld(tmp_path / "c0.ld", [("A", "B", 0.5), ("B", "E", 0.1), ("C", "D", 0.3),
+                                  ("D", "E", 0.2)])
+    write_ld(tmp_path / "c1.ld", [("A", "C", 0.4)])
+    N = [100, 200]
+    src = plink_ld_sources(ref, lists, N)
+    np.testing.assert_array_equal(src[0], [0, 0, 0, 0, 0])
+    np.testing.assert_array_equal(src[1], [1, 1, 1, 0, 0])      # D, E asked of cohort 0
+    r = np.array([[1.0, 2, 3, 4, 5], [10.0, 20, 30, 0, 0]])
+    mats, r_out = load_plink_ld_all([str(tmp_path / "c0.ld"), str(tmp_path / "c1.ld")], r, ref,
+                                    lists, N)
+    E0 = np.eye(5)
+    for (i, j, v) in [(0, 1, 0.5), (1, 4, 0.1), (2, 3, 0.3), (3, 4, 0.2)]:
+        E0[i, j] = E0[j, i] = v
+    np.testing.assert_array_equal(mats[0].toarray(), E0)
+    # cohort 1: own (A,C); from cohort 0 every entry touching D, then every entry
+    # touching E -- (D,E) touches both, arrives twice and sums to 0.4
+    E1 = np.eye(5)
+    for (i, j, v) in [(0, 2, 0.4), (2, 3, 0.3), (3, 4, 0.4), (1, 4, 0.1)]:
+        E1[i, j] = E1[j, i] = v
+    np.testing.assert_allclose(mats[1].toarray(), E1, rtol=0, atol=1e-15)
+    np.testing.assert_array_equal(r_out[0], r[0])
+    np.testing.assert_array_equal(r_out[1], [10, 20, 30, 4, 5])
+
+
+def test_plink_ld_exchange_source_quirk(tmp_path):
+    """main.py:161-162: kx indexes the list of other cohorts holding the marker,
+    and is used as a cohort id."""
+    from ldio import load_plink_ld_all, plink_ld_sources
+
+    write_bim(tmp_path / "c0.bim", ["A", "B", "C", "D"], [1, 2, 3, 4])
+    write_bim(tmp_path / "c1.bim", ["A", "B", "D", "E"], [1, 2, 4, 5])
+    write_bim(tmp_path / "c2.bim", ["B", "C", "D", "E"], [2, 3, 4, 5])
+    df, lists = merge_bims([str(tmp_path / ("c%d.bim" % k)) for k in range(3)])
+    ref = list(df["Variant"])
+    assert ref == ["A", "B", "C", "D", "E"]
+    N = [100, 300, 200]
+    src = plink_ld_sources(ref, lists, N)
+    # cohort 0 lacks E: holders [1, 2], N [300, 200] -> kx = 0 = cohort 0 itself: never asked
+    np.testing.assert_array_equal(src[0], [0, 0, 0, 0, 0])
+    # cohort 1 lacks C: holders [0, 2], N [100, 200] -> kx = 1 = itself
+    np.testing.assert_array_equal(src[1], [1, 1, 1, 1, 1])
+    # cohort 2 lacks A: holders [0, 1], N [100, 300] -> kx = 1: asks cohort 1 (holds A)
+    np.testing.assert_array_equal(src[2], [1, 2, 2, 2, 2])
+    write_ld(tmp_path / "c0.ld", [("A", "C", 0.6)])
+    write_ld(tmp_path / "c1.ld", [("A", "B", 0.5), ("D", "E", 0.2), ("A", "D", 0.1)])
+    write_ld(tmp_path / "c2.ld", [("B", "C", 0.7)])
+    r = np.array([[1.0, 2, 3, 4, 0], [11.0, 12, 0, 14, 15], [0, 22.0, 23, 24, 25]])
+    mats, r_out = load_plink_ld_all([str(tmp_path / ("c%d.ld" % k)) for k in range(3)], r, ref,
+                                    lists, N)
+    E2 = np.eye(5)
+    for (i, j, v) in [(1, 2, 0.7), (0, 1, 0.5), (0, 3, 0.1)]:
+        E2[i, j] = E2[j, i] = v
+    np.testing.assert_array_equal(mats[2].toarray(), E2)
+    np.testing.assert_array_equal(r_out[2], [11, 22, 23, 24, 25])
+    np.testing.assert_array_equal(r_out[0], r[0])                # E never filled: r = 0
+    assert mats[0].toarray()[4].tolist() == [0, 0, 0, 0, 1]

@@ -1,0 +1,135 @@
+"""The process seam end to end on the GPU: sgvamp-py_amd/main.py with the
+reference's flags and file formats (src/main.py:27-330).
+
+* a golden case written out as the reference's input files (.npy LD, .npy r,
+  .bim, true signal) -> the output .bin/.csv files match the reference's;
+* PLINK .ld text LD (with a cohort missing markers) gives the same run as .npz
+  files holding the matrices the .ld loader builds (loader semantics:
+  tests/test_cli_io.py)."""
+import os
+
+import numpy as np
+import pytest
+
+from tests.golden import Case
+
+pytestmark = pytest.mark.gpu
+
+
+def _write_bim(path, names, coords):
+    with open(path, "w") as f:
+        for n, c in zip(names, coords):
+            f.write("1\t%s\t0\t%d\tA\tG\n" % (n, c))
+
+
+def _maxrel(a, b):
+    return float(np.max(np.abs(a - b)) / max(float(np.max(np.abs(b))), 1e-300))
+
+
+def _flags(f):
+    def j(v):
+        return ",".join(repr(float(x)) for x in v)
+    return ["--iterations", str(f["iterations"]), "--prior-vars", j(f["prior_vars"]),
+            "--prior-probs", j(f["prior_probs"]), "--gamw", repr(float(f["gamw"])),
+            "--gam1", repr(float(f["gam1"])), "--rho", repr(float(f["rho"])),
+            "--cg-maxit", str(f["cg_maxit"]), "--em-prior-maxit", str(f["em_prior_maxit"]),
+            "--learn-gamw", str(int(f["learn_gamw"])), "--lmmse-damp", str(int(f["lmmse_damp"])),
+            "--s", repr(float(f["s"])), "--prior-update", f["prior_update"],
+            "--update-prior-from", str(f["update_prior_from"]), "--seed", str(f["seed"])]
+
+
+@pytest.mark.parametrize("name", ["k1_dense", "k1_mle"])
+def test_cli_matches_reference_golden(name, tmp_path):
+    import main
+
+    c = Case(name)
+    f = c.flags
+    M = c.M
+    R = np.zeros((M, M))
+    o = 0
+    for B in c.ld_blocks[0]:
+        n = B.shape[0]
+        R[o:o + n, o:o + n] = B
+        o += n
+    np.save(tmp_path / "R.npy", R)
+    np.save(tmp_path / "r.npy", c.r[0])
+    np.save(tmp_path / "beta.npy", c.beta)
+    _write_bim(tmp_path / "c.bim", ["rs%d" % i for i in range(M)], range(1, M + 1))
+    out = tmp_path / "out"
+    out.mkdir()
+    argv = ["--ld-files", str(tmp_path / "R.npy"), "--r-files", str(tmp_path / "r.npy"),
+            "--true-signal-file", str(tmp_path / "beta.npy"), "--out-dir", str(out),
+            "--out-name", name, "--N", str(c.N[0]), "--M", str(M), "--K", "1",
+            "--bim-files", str(tmp_path / "c.bim")] + _flags(f)
+    main.main(argv)
+    for it in range(f["iterations"]):
+        xb = np.fromfile(out / ("%s_xhat_it_%d.bin" % (name, it)))
+        assert _maxrel(xb, c.xhat[it]) < 1e-8, it
+    with open(out / ("%s_cohort_1.csv" % name)) as fh:
+        rows = np.array([[float(x) for x in ln.split("\t")] for ln in fh.read().splitlines()[1:]])
+    np.testing.assert_allclose(rows, c.cohort_csv[0], rtol=1e-5, atol=0)
+    assert os.path.exists(out / (name + ".bim"))
+
+
+def test_cli_plink_ld_equals_npz(tmp_path):
+    import scipy.sparse
+
+    import main
+    from ldio import load_plink_ld_all, merge_bims
+
+    rs = np.random.RandomState(4)
+    M, nsamp = 240, 600
+    names = ["rs%d" % i for i in range(M)]
+    X = rs.normal(size=(nsamp, M))
+    for b in range(0, M, 60):                      # 4 LD blocks of 60
+        X[:, b + 1:b + 60] += 0.7 * X[:, b:b + 1]
+    X = (X - X.mean(0)) / X.std(0) / np.sqrt(nsamp)
+    C = X.T @ X
+    beta = np.zeros(M)
+    beta[rs.choice(M, 24, replace=False)] = rs.normal(0, np.sqrt(0.8 / 24), 24)
+    missing = set(range(100, 115))                 # cohort 1 lacks 15 markers
+    keep1 = [i for i in range(M) if i not in missing]
+    cohorts = [list(range(M)), keep1]
+    for k, idx in enumerate(cohorts):
+        _write_bim(tmp_path / ("c%d.bim" % k), [names[i] for i in idx], [i + 1 for i in idx])
+        with open(tmp_path / ("c%d.ld" % k), "w") as fh:
+            fh.write(" CHR_A BP_A SNP_A CHR_B BP_B SNP_B R\n")
+            for a in idx:
+                for b in idx:
+                    if a < b and a // 60 == b // 60:
+                        fh.write(" 1 %d %s 1 %d %s %r\n" % (a + 1, names[a], b + 1, names[b],
+                                                                   float(C[a, b])))
+        y = X @ beta * np.sqrt(nsamp) + rs.normal(0, np.sqrt(0.2), nsamp)
+        np.save(tmp_path / ("r%d.npy" % k), (X.T @ y)[idx])
+    bims = [str(tmp_path / ("c%d.bim" % k)) for k in range(2)]
+    common = ["--N", "600,600", "--M", "%d,%d" % (M, len(keep1)), "--K", "2",
+              "--bim-files", ",".join(bims), "--iterations", "5", "--prior-vars",
+              "0,%r" % (0.8 / 24 / 2), "--prior-probs", "0.9,0.1", "--seed", "3"]
+    out_a = tmp_path / "a"
+    out_a.mkdir()
+    main.main(["--ld-files", ",".join(str(tmp_path / ("c%d.ld" % k)) for k in range(2)),
+               "--r-files", ",".join(str(tmp_path / ("r%d.npy" % k)) for k in range(2)),
+               "--out-dir", str(out_a), "--out-name", "a"] + common)
+    # the same matrices and exchanged r vectors as .npz / reference-ordered .npy
+    df, lists = merge_bims(bims)
+    ref = list(df["Variant"])
+    r_ref = np.zeros((2, M))
+    for k, idx in enumerate(cohorts):
+        r_ref[k][idx] = np.load(tmp_path / ("r%d.npy" % k))
+    mats, r_x = load_plink_ld_all([str(tmp_path / ("c%d.ld" % k)) for k in range(2)], r_ref, ref,
+                                  lists, [600, 600])
+    assert mats[1][105, 105] == 1.0 and r_x[1][105] == r_ref[0][105]   # filled from cohort 0
+    for k in range(2):
+        scipy.sparse.save_npz(tmp_path / ("R%d.npz" % k), mats[k])
+        np.save(tmp_path / ("rx%d.npy" % k), r_x[k])
+    out_b = tmp_path / "b"
+    out_b.mkdir()
+    full = ["--N", "600,600", "--M", "%d,%d" % (M, M), "--K", "2", "--iterations", "5",
+            "--prior-vars", "0,%r" % (0.8 / 24 / 2), "--prior-probs", "0.9,0.1", "--seed", "3"]
+    main.main(["--ld-files", ",".join(str(tmp_path / ("R%d.npz" % k)) for k in range(2)),
+               "--r-files", ",".join(str(tmp_path / ("rx%d.npy" % k)) for k in range(2)),
+               "--out-dir", str(out_b), "--out-name", "a"] + full)
+    for it in range(5):
+        a = np.fromfile(out_a / ("a_xhat_it_%d.bin" % it))
+        b = np.fromfile(out_b / ("a_xhat_it_%d.bin" % it))
+        np.testing.assert_array_equal(a, b)
