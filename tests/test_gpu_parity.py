@@ -365,3 +365,47 @@ def test_vamp_medium_scale_vs_oracle(prior, rs, tmp_path):
     assert [h["cg_iters"][0] for h in v.history] == [list(x[0]) for x in t["cg_iters"]]
     assert [h.get("em_steps") for h in v.history][1:] == list(t["em_steps"])
     eng.close()
+
+
+@pytest.mark.parametrize("K,ridge,damp", [(4, 0.05, True), (8, 0.05, True), (4, 0.0, False),
+                                          (8, 0.0, False)])
+def test_vamp_medium_scale_shared_ld_vs_oracle(K, ridge, damp, tmp_path):
+    """C3/C5-like: K cohorts sharing one LD (2K CG columns -> the f64 MFMA passes
+    over multi-panel, multi-chunk blocks: 4x4x4 groups, 16x16x4 at 13..16
+    columns), ridge s and LMMSE damping on, R_s x carried through the CG; vs the
+    oracle with the same algebra (cg_track).  With s = 0 the blocks are rank
+    deficient (n_b > N): 5-9 CG iterations, columns stopping at different
+    iterations, so one solve walks through several column counts / kernels."""
+    sizes = [1300, 700, 1100]
+    nsamp = 900
+    M = sum(sizes)
+    rs = np.random.RandomState(8)
+    cm = M // 10
+    beta = np.zeros(M)
+    beta[rs.choice(M, cm, replace=False)] = rs.normal(0, np.sqrt(0.8 / cm), cm)
+    eng = Engine(sizes, K=K)
+    g = eng.synth_ld_g(0, 77, nsamp, beta).sum(axis=0)
+    rvec = []
+    for k in range(K):
+        y = g + np.random.RandomState(100 + k).normal(0, np.sqrt(0.2), nsamp)
+        eng.synth_r(k, 77, nsamp, y)
+        rvec.append(eng.get_vector(hb.VEC_R, k).copy())
+    blocks = [eng.get_ld_block(0, b) for b in range(len(sizes))]
+    assert {eng.ld_block_format(0, b) for b in range(len(sizes))} == {1}
+    N = [float(nsamp)] * K
+    prior = dict(prior_vars=[0.0, 0.8 / cm / K], prior_probs=[0.9, 0.1])
+    v = VAMP(N=N, Nt=sum(N), M=M, K=K, rho=0.5, gamw=5.0, gam1=1e-6, a=[1 / K] * K,
+             out_dir=str(tmp_path), out_name="kk", seed=5, write_files=False, **prior)
+    v.attach_engine(eng, x0=beta * np.sqrt(nsamp))
+    eng.set_ridge(ridge)
+    its = 6
+    xh = v.infer(None, None, its, x0=beta * np.sqrt(nsamp), lmmse_damp=damp, prior_update="em")
+    L = vo.BlockLD(blocks, s=ridge)
+    t = vo.infer([L], [0] * K, rvec, N, its, rho=0.5, gamw=5.0, gam1=1e-6, x0=beta * np.sqrt(nsamp),
+                 seed=5, lmmse_damp=damp, reducer=vo.Reducer("blocked", bounds=L.bounds),
+                 rs_recurrence=True, **prior)
+    for it in range(its):
+        assert maxrel(xh[it].ravel() / np.sqrt(sum(N)), np.asarray(t["xhat"][it])) < 1e-8, it
+    assert [h["cg_iters"] for h in v.history] == [[list(c) for c in x] for x in t["cg_iters"]]
+    assert [h.get("em_steps") for h in v.history][1:] == list(t["em_steps"])
+    eng.close()
