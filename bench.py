@@ -60,6 +60,8 @@ def parse():
                    help="rehearsal: every rank on device 0 with the host exchange (RCCL refuses "
                         "two ranks on one device); timings are then not a multi-GPU result")
     p.add_argument("--prior", choices=["matched", "cli"], default="matched")
+    p.add_argument("--ridge", type=float, default=0.0, help="--s of the CLI (C5: 0.1)")
+    p.add_argument("--lmmse-damp", type=int, default=0, help="--lmmse-damp of the CLI (C5: 1)")
     p.add_argument("--ld-format", choices=["packed", "dense"], default="packed",
                    help="LD block storage: packed symmetric panels (default) or full squares")
     return p.parse_args()
@@ -113,7 +115,7 @@ def cpu_baseline(eng, args, ref_flags):
     n = eng.block_sizes[0]
     B = eng.get_ld_block(0, 0)
     r = eng.get_vector(hb.VEC_R, 0)[:n].copy()
-    L = vo.BlockLD([B])
+    L = vo.BlockLD([B], s=args.ridge)
     its = args.cpu_iters
     t0 = time.perf_counter()
     vo.infer([L], [0], [r], [args.nsamp], its, reducer=vo.Reducer(), seed=args.seed, **ref_flags)
@@ -151,11 +153,14 @@ def main():
     a = np.array(N_list) / Nt
     cm = int(eng.M * 0.5)
     if args.prior == "matched":
-        prior = dict(prior_vars=[0.0, 0.8 / cm], prior_probs=[0.5, 0.5])
+        # simulated effect variance 0.8/cm in x = beta*sqrt(N_k) scale is 0.8/cm * N_k; the
+        # reference scales slab variances by Nt (src/sgvamp.py:27): 0.8/cm * N_k / Nt
+        prior = dict(prior_vars=[0.0, 0.8 / cm * N_list[0] / Nt], prior_probs=[0.5, 0.5])
     else:
         prior = dict(prior_vars=[0.0, 1.0], prior_probs=[0.99, 0.01])
     flags = dict(rho=0.5, gamw=5.0, gam1=1e-6, **prior)
-    run = dict(cg_maxit=500, em_prior_maxit=100, learn_gamw=True, lmmse_damp=False,
+    eng.set_ridge(args.ridge)
+    run = dict(cg_maxit=500, em_prior_maxit=100, learn_gamw=True, lmmse_damp=bool(args.lmmse_damp),
                prior_update="em", update_prior_from=1)
     tmp = tempfile.mkdtemp(prefix="sgvamp_bench_")
     v = VAMP(N=N_list if K > 1 else N_list[0], Nt=Nt, M=eng.M, K=K, a=a, out_dir=tmp,
@@ -187,9 +192,12 @@ def main():
     dt = max(comm.allgather(t1 - t0))
     tm = eng.timers()
     for rec in recs:
-        log("[bench] it=%d cg=%s em=%s passes=%d %.1f ms l2=%s" % (
-            rec["it"], rec["cg_iters"], rec.get("em_steps"), rec["ld_passes"], rec["wall_s"] * 1e3,
-            "%.4f" % rec["metrics"][1] if "metrics" in rec else "-"))
+        log("[bench] it=%d cg=%s em=%s passes=%d %.1f ms l2=%s waits(ms): probes %.2f outputs %.2f "
+            "writes %.2f" % (
+                rec["it"], rec["cg_iters"], rec.get("em_steps"), rec["ld_passes"],
+                rec["wall_s"] * 1e3, "%.4f" % rec["metrics"][1] if "metrics" in rec else "-",
+                rec.get("wait_probes_ms", 0.0), rec.get("outputs_ms", 0.0),
+                rec.get("wait_write_ms", 0.0)))
 
     steps = args.steps
     value = steps / dt
@@ -202,8 +210,13 @@ def main():
     mfma = args.ld_format == "packed" and 2 * K >= 3     # NC >= 3: the f64 MFMA pass
     traffic, traffic_src = read_traffic(("k_sym_mfma" if mfma else "k_sym_pass")
                                         if args.ld_format == "packed" else "k_ld_pass")
-    cname = {1: "C2 (BASELINE.json configs[1])", 4: "C3 (BASELINE.json configs[2])"}.get(K, "C2-like")
-    if eng.M != 200000:
+    if eng.M == 200000 and args.ridge == 0 and not args.lmmse_damp:
+        cname = {1: "C2 (BASELINE.json configs[1])", 4: "C3 (BASELINE.json configs[2])"}.get(K, "custom")
+    elif eng.M == 1000000 and K == 1 and args.ridge == 0 and not args.lmmse_damp:
+        cname = "C4 (BASELINE.json configs[3]) on %d GPU(s)" % world
+    elif eng.M == 1000000 and K == 8 and args.ridge == 0.1 and args.lmmse_damp:
+        cname = "C5 (BASELINE.json configs[4]) on %d GPU(s)" % world
+    else:
         cname = "custom"
     passes = sum(r["ld_passes"] for r in recs)
     ld_bytes_total = ld_bytes_launch * comm.Get_size()
@@ -228,6 +241,7 @@ def main():
                                                          args.block_size, args.nsamp,
                                                          prior["prior_vars"], prior["prior_probs"]),
             "K": K, "M": eng.M, "ld_blocks": args.blocks, "block_size": args.block_size,
+            "s": args.ridge, "lmmse_damp": bool(args.lmmse_damp),
             "N": args.nsamp, "parallelism": "LD blocks sharded over %d GPU rank(s)" % world,
         },
         "roofline": {

@@ -190,6 +190,14 @@ int sgv_mle_terms(sgv_ctx* ctx, const double* a /* K */, const double* gam1s /* 
                   const double* sigma2 /* L */, const double* omega /* L */, double exp_max,
                   double* sums /* L */);
 
+/* The per-iteration output vectors without a host wait (src/sgvamp.py:281,283):
+ * sgv_outputs_begin queues this rank's slices of xhat1 and r1[0..K-1] (unscaled,
+ * marker order) into pinned slot 0 or 1; sgv_outputs_wait -- callable from a
+ * writer thread -- waits for that copy and returns the slot's buffer
+ * [(K + 1) x M_local] doubles, valid until the slot is begun again. */
+int sgv_outputs_begin(sgv_ctx* ctx, int slot);
+int sgv_outputs_wait(sgv_ctx* ctx, int slot, double** data);
+
 int sgv_lmmse(sgv_ctx* ctx, int it, const double* gamw, const double* gam2,
               const double* alpha1, const double* alpha2_prev, const int8_t* probes,
               int cg_maxit, double rtol, int lmmse_damp, double rho, int learn_gamw,

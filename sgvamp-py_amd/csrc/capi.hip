@@ -96,6 +96,11 @@ struct sgv_ctx {
   size_t rowpart_cap = 0, colpart_cap = 0, part_cap = 0;
   int mfma_min = 3;              // see mfma_min_default
   double* d_pk = nullptr;        // RHS interleaved [Mpad][16] for the MFMA pass
+  // asynchronous per-iteration outputs (xhat1, r1[k]): device pack buffer and two
+  // pinned host slots, each with its completion event (sgv_outputs_begin/wait)
+  double* d_out = nullptr;
+  double* h_out[2] = {nullptr, nullptr};
+  hipEvent_t ev_out[2] = {nullptr, nullptr};
   size_t pk_cap = 0;
   // chunk / row-group layouts
   int nch = 0;
@@ -793,6 +798,11 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   if (c->d_rowpart) (void)hipFree(c->d_rowpart);
   if (c->d_colpart) (void)hipFree(c->d_colpart);
   if (c->d_pk) (void)hipFree(c->d_pk);
+  if (c->d_out) (void)hipFree(c->d_out);
+  for (int i = 0; i < 2; ++i) {
+    if (c->h_out[i]) (void)hipHostFree(c->h_out[i]);
+    if (c->ev_out[i]) (void)hipEventDestroy(c->ev_out[i]);
+  }
   for (BlkDesc* d : c->d_blks) (void)hipFree(d);
   (void)hipFree(c->d_ch);
   (void)hipFree(c->d_ch_doff);
@@ -1246,6 +1256,43 @@ extern "C" int sgv_mle_terms(sgv_ctx* c, const double* a, const double* gam1s, i
   double tot[MAXL + 1];
   CHK(reduce_host(c, MAXL + 1, c->d_ch_begin, tot));
   for (int l = 0; l < L; ++l) sums[l] = tot[l];
+  return SGV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// per-iteration outputs without a host wait (src/sgvamp.py:281,283)
+// ---------------------------------------------------------------------------
+extern "C" int sgv_outputs_begin(sgv_ctx* c, int slot) {
+  ENTER(c);
+  if (slot < 0 || slot > 1) return fail(c, SGV_ERR_ARG, "slot must be 0 or 1");
+  const size_t n = (size_t)std::max<int64_t>(c->Mloc, 1);
+  const size_t bytes = sizeof(double) * n * (c->K + 1);
+  if (!c->d_out) {
+    HIPCHK(hipMalloc(&c->d_out, bytes));
+    for (int i = 0; i < 2; ++i) {
+      HIPCHK(hipHostMalloc(&c->h_out[i], bytes));
+      HIPCHK(hipEventCreateWithFlags(&c->ev_out[i], hipEventDisableTiming));
+    }
+  }
+  HIPCHK(launch_pack(c->d_ch, c->nch, c->d_ch_doff, c->xhat1, c->d_out, c->st));
+  for (int k = 0; k < c->K; ++k)
+    HIPCHK(launch_pack(c->d_ch, c->nch, c->d_ch_doff, c->r1[k], c->d_out + n * (k + 1), c->st));
+  HIPCHK(hipMemcpyAsync(c->h_out[slot], c->d_out, sizeof(double) * n * (c->K + 1),
+                        hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipEventRecord(c->ev_out[slot], c->st));
+  return SGV_OK;
+}
+
+// May be called from another host thread than the one driving the context: it
+// only waits on the slot's event and returns the pinned buffer (valid until the
+// slot's next sgv_outputs_begin).
+extern "C" int sgv_outputs_wait(sgv_ctx* c, int slot, double** data) {
+  if (!c || slot < 0 || slot > 1 || !data || !c->ev_out[slot]) return SGV_ERR_ARG;
+  if (hipSetDevice(c->dev) != hipSuccess) return SGV_ERR_HIP;
+  hipError_t e;
+  while ((e = hipEventQuery(c->ev_out[slot])) == hipErrorNotReady) __builtin_ia32_pause();
+  if (e != hipSuccess) return SGV_ERR_HIP;
+  *data = c->h_out[slot];
   return SGV_OK;
 }
 

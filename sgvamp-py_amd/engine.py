@@ -139,6 +139,19 @@ class Engine:
                         int(maxit), hb.dptr(lam_io), hb.dptr(om), hb.iptr(steps), hb.dptr(err))
         return float(lam_io[0]), om, int(steps[0]), float(err[0])
 
+    def outputs_begin(self, slot):
+        """Queue xhat1 and r1[k] (this rank's slice) into pinned slot 0/1 (no wait)."""
+        self.ctx.sgv_outputs_begin(int(slot))
+
+    def outputs_wait(self, slot):
+        """Wait for slot's copy (any thread); returns a (K + 1, Mloc) view of the
+        pinned buffer, valid until the slot is begun again."""
+        p = hb._c_dbl_p()
+        rc = self.ctx.lib.sgv_outputs_wait(self.ctx.h, int(slot), ctypes.byref(p))
+        if rc != hb.SGV_OK:
+            raise hb.HipError("sgv_outputs_wait failed (%d)" % rc)
+        return np.ctypeslib.as_array(p, shape=(self.K + 1, max(self.Mloc, 1)))[:, :self.Mloc]
+
     def mle_exp_max(self, gam1s, sigma2):
         """max over (k, m, l) of (-r1_km^2 / 2) / (sigma2_l + 1/gam1_k) (src/sgvamp.py:152)."""
         out = np.zeros(1)

@@ -285,26 +285,39 @@ class VAMP:
         # host work that overlaps the GPU: the next iteration's probes are drawn
         # (in stream order) while the current one runs; output files are written
         # by a writer thread (at most one iteration in flight).
-        self._probe_pool = ThreadPoolExecutor(max_workers=1)
-        self._write_pool = ThreadPoolExecutor(max_workers=1)
-        self._next_probes = self._probe_pool.submit(self._draw_probes)
+        # one thread per cohort stream (numpy's legacy binomial releases the GIL),
+        # writers in parallel per file
+        self._probe_pool = ThreadPoolExecutor(max_workers=self.K)
+        self._write_pool = ThreadPoolExecutor(max_workers=self.K + 1)
+        self._out_pool = ThreadPoolExecutor(max_workers=1)   # waits for the output copies
+        self._next_probes = self._submit_probes()
         self._pending_write = None
         if self.rank == 0:
             logging.debug(f"a = {self.a}")
 
-    def _draw_probes(self):
+    def _draw_probe(self, k):
         """u_k = binomial(p=1/2, n=1, size=M)*2-1 (src/sgvamp.py:326), local slice."""
         eng = self.engine
-        u = np.empty((self.K, eng.Mloc), dtype=np.int8)
-        for k in range(self.K):
-            u[k] = (self._st["probes"][k].binomial(p=1 / 2, n=1, size=self.M) * 2 - 1)[eng.sl]
-        return u
+        return (self._st["probes"][k].binomial(p=1 / 2, n=1, size=self.M) * 2 - 1)[eng.sl] \
+            .astype(np.int8)
 
-    def _write_outputs(self, it, xhat_loc, r1_locs):
+    def _submit_probes(self):
+        # each cohort's stream is drawn in its own task; the next iteration's draws
+        # are submitted only after this iteration's are consumed (stream order kept)
+        return [self._probe_pool.submit(self._draw_probe, k) for k in range(self.K)]
+
+    def _write_outputs(self, it, slot):
+        """Writer side of one iteration's files: wait for the pinned copy queued by
+        sgv_outputs_begin, then write xhat1 and every r1, one file per task."""
         Nt = self.Nt
-        self.write_xhat_to_file(it, xhat_loc / np.sqrt(Nt))           # :281
-        for k, r1 in enumerate(r1_locs):
-            self.write_r1_to_file(it, r1 / np.sqrt(Nt), k + 1)        # :283
+        out = self.engine.outputs_wait(slot)
+        futs = [self._write_pool.submit(lambda: self.write_xhat_to_file(
+            it, out[0] / np.sqrt(Nt)))]                                              # :281
+        for k in range(self.K):
+            futs.append(self._write_pool.submit(
+                lambda k=k: self.write_r1_to_file(it, out[k + 1] / np.sqrt(Nt), k + 1)))   # :283
+        for f in futs:
+            f.result()
 
     def flush(self):
         """Wait for the output files of every finished iteration."""
@@ -314,7 +327,7 @@ class VAMP:
 
     def finish(self):
         self.flush()
-        for pool in ("_probe_pool", "_write_pool"):
+        for pool in ("_probe_pool", "_write_pool", "_out_pool"):
             if getattr(self, pool, None) is not None:
                 getattr(self, pool).shutdown(wait=True)
                 setattr(self, pool, None)
@@ -359,18 +372,20 @@ class VAMP:
         alpha1_prev = list(alpha1)
         der_sum = eng.denoise(gam1s, self.a, self.lam, self.omegas, self.sigmas, rho,
                               damp=it > 0)                            # :273-276, 285
-        if self.write_files or st["return_xhat"]:
+        if self.write_files:
+            # the previous iteration's files are written (its pinned slot is free),
+            # then this iteration's copies are queued without a wait
+            t0 = time.perf_counter()
+            self.flush()
+            rec["wait_write_ms"] = (time.perf_counter() - t0) * 1e3
+            eng.outputs_begin(it % 2)
+            self._pending_write = self._out_pool.submit(self._write_outputs, it, it % 2)
+        if st["return_xhat"]:
             xhat_loc = eng.get_vector(hb.VEC_XHAT1)
-            if self.write_files:
-                r1_locs = [eng.get_vector(hb.VEC_R1, k) for k in range(K)]
-                self.flush()
-                self._pending_write = self._write_pool.submit(self._write_outputs, it, xhat_loc,
-                                                              r1_locs)
-            if st["return_xhat"]:
-                full = xhat_loc
-                if self.comm.Get_size() > 1:
-                    full = np.concatenate(self.comm.allgather(xhat_loc))
-                st["xhat1s"].append(full.reshape((M, 1)))
+            full = xhat_loc
+            if self.comm.Get_size() > 1:
+                full = np.concatenate(self.comm.allgather(xhat_loc))
+            st["xhat1s"].append(full.reshape((M, 1)))
         gam2 = [0.0] * K
         for k in range(K):
             a1 = der_sum[k] / M                                       # np.mean (:285)
@@ -383,8 +398,10 @@ class VAMP:
             logging.debug(f"[rank = {rank}] gam2 = {gam2[0]}")
         for k in range(K):
             logging.info(f"...LMMSE cohort {k}")
-        u = self._next_probes.result()                                # :326
-        self._next_probes = self._probe_pool.submit(self._draw_probes)
+        t0 = time.perf_counter()
+        u = np.stack([f.result() for f in self._next_probes])        # :326
+        rec["wait_probes_ms"] = (time.perf_counter() - t0) * 1e3
+        self._next_probes = self._submit_probes()
         out, cg, passes = eng.lmmse(it, gamw, gam2, alpha1, alpha2, u, st["cg_maxit"],
                                     st["lmmse_damp"], rho, st["learn_gamw"])
         rec.update(cg_iters=cg[:, [0, 2]].tolist(), cg_info=cg[:, [1, 3]].tolist(),
