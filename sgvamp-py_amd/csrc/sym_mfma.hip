@@ -50,12 +50,17 @@ __device__ __forceinline__ void lds_order() {
 constexpr int MF_CW = 512;   // chunk width (class 1 items)
 constexpr int MF_LDP = 34;   // staging row pitch (doubles): conflict-free both ways
 
-template <int NG, int NW>
+// NS column splits: the waves form NS sets; set s handles column groups
+// [s*NG, (s+1)*NG) over the whole chunk (NS*NG groups of 4 columns, NG groups of
+// registers per wave).  NS = 2 was measured slower than one 16x16x4 group (the
+// repeat R reads of the second set go back to HBM); the launcher uses NS = 1.
+template <int NG, int NW, int NS>
 __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restrict__ items,
                                                          const double* __restrict__ pk, int ncol,
                                                          double* __restrict__ rowpart,
                                                          double* __restrict__ colpart) {
-  constexpr int WC = MF_CW / NW;   // columns per wave
+  constexpr int NWS = NW / NS;     // waves per column split
+  constexpr int WC = MF_CW / NWS;  // columns per wave
   constexpr int NT = WC / 32;      // 32-column steps per wave
   static_assert(NT >= 1, "at least one step per wave");
   __shared__ double red[2][NW][256];
@@ -68,7 +73,8 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restri
   const double* base = it.P + (it.c0 - it.r0);        // panel row 0, chunk column 0
   const int64_t w = it.w;
   const double* pkb = pk + (int64_t)it.voff * 16;     // Pk of this block (block-relative index)
-  const int cw0 = wid * WC;                            // first chunk column of this wave
+  const int cw0 = (wid % NWS) * WC;                    // first chunk column of this wave
+  const int cq0 = 4 * NG * (wid / NWS);                // first RHS column of this wave's groups
   double* sb = stg[wid];
 
   // row-part B operands: P at this wave's columns, reused by every row group
@@ -80,7 +86,8 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restri
       const int col = cw0 + 32 * t + 2 * pc + e;
 #pragma unroll
       for (int q = 0; q < NG; ++q) {
-        const double v = ldg(pkb + (int64_t)(it.c0 + (col < it.nc ? col : 0)) * 16 + 4 * q + n4);
+        const double v = ldg(pkb + (int64_t)(it.c0 + (col < it.nc ? col : 0)) * 16 + cq0 + 4 * q +
+                             n4);
         brow[t][e][q] = col < it.nc ? v : 0.0;
       }
     }
@@ -110,7 +117,8 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restri
       const int rB = 16 * g + 4 * a + hi;
 #pragma unroll
       for (int q = 0; q < NG; ++q) {
-        const double v = ldg(pkb + (int64_t)(it.r0 + (rB < it.H ? rB : 0)) * 16 + 4 * q + n4);
+        const double v = ldg(pkb + (int64_t)(it.r0 + (rB < it.H ? rB : 0)) * 16 + cq0 + 4 * q +
+                             n4);
         bc[a][q] = rB < it.H ? v : 0.0;
       }
     }
@@ -175,15 +183,16 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restri
         double v = drow[r][q];
         v = v + __shfl_xor(v, 4);
         v = v + __shfl_xor(v, 8);
-        if (bq == 0) rb[((4 * r + hi) << 4) + 4 * q + n4] = v;   // D row 4r + m (m = hi)
+        if (bq == 0) rb[((4 * r + hi) << 4) + cq0 + 4 * q + n4] = v;   // D row 4r + m (m = hi)
       }
     __syncthreads();
     if (threadIdx.x < 256) {
       const int t = threadIdx.x, row = t >> 4, cc = t & 15;
       if (16 * g + row < it.H && cc < ncol) {
-        double s = red[g & 1][0][t];
+        const int w0 = (cc / (4 * NG)) * NWS;          // the waves of cc's column split
+        double s = red[g & 1][w0][t];
 #pragma unroll
-        for (int v = 1; v < NW; ++v) s += red[g & 1][v][t];
+        for (int v = 1; v < NWS; ++v) s += red[g & 1][w0 + v][t];
         rowpart[((int64_t)it.item * SYM_H + 16 * g + row) * ncol + cc] = s;
       }
     }
@@ -193,7 +202,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restri
   // D_b[m][n] at lane 16m + 4b + n holds column pair 4b + m = pc, column c = 4q + n
 #pragma unroll
   for (int q = 0; q < NG; ++q) {
-    const int cc = 4 * q + n4;
+    const int cc = cq0 + 4 * q + n4;
     if (cc < ncol) {
       double* out = colpart + ((int64_t)it.item * ncol + cc) * MF_CW;
 #pragma unroll
@@ -350,11 +359,11 @@ __global__ __launch_bounds__(256) void k_pack16(PassArgs pa, int ncol, int64_t m
   pk[t] = c < ncol ? pa.in[c][i] : 0.0;
 }
 
-template <int NG, int NW>
+template <int NG, int NW, int NS>
 static void launch_mf(const SymItem* d_items, int nitems, const double* d_pk, int nc,
                       double* rowpart, double* colpart, hipStream_t st) {
-  hipLaunchKernelGGL((k_sym_mfma<NG, NW>), dim3(nitems), dim3(NW * 64), 0, st, d_items, d_pk, nc,
-                     rowpart, colpart);
+  hipLaunchKernelGGL((k_sym_mfma<NG, NW, NS>), dim3(nitems), dim3(NW * 64), 0, st, d_items, d_pk,
+                     nc, rowpart, colpart);
 }
 
 hipError_t launch_sym_mfma(int nc, const SymItem* d_items, int nitems, const PassArgs& pa,
@@ -364,10 +373,12 @@ hipError_t launch_sym_mfma(int nc, const SymItem* d_items, int nitems, const Pas
   const int64_t n16 = mpad * 16;
   hipLaunchKernelGGL(k_pack16, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, st, pa, nc,
                      mpad, d_pk);
+  // 9..16 columns: one 16x16x4 group beats three/four 4x4x4 groups (register
+  // pressure) and splitting the groups over two wave sets (the repeat R reads do
+  // not come from cache): measured in DESIGN.md
   switch ((nc + 3) / 4) {
-    case 1: launch_mf<1, 4>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
-    case 2: launch_mf<2, 4>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
-    case 3: launch_mf<3, 4>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
+    case 1: launch_mf<1, 4, 1>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
+    case 2: launch_mf<2, 4, 1>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
     default:
       hipLaunchKernelGGL(k_sym_mfma16, dim3(nitems), dim3(256), 0, st, d_items, d_pk, nc, rowpart,
                          colpart);
