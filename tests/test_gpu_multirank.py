@@ -6,7 +6,7 @@ other code is the sharded product path: LD block ranges per rank, rank-local
 vectors, the ordered cross-rank reduction (bitwise the same scalars as one
 rank), rank-sliced output files.  tools/two_rank_gpu.py checks the merged files
 against the reference's golden outputs (maxrel < 1e-8, identical CG and EM
-counts)."""
+counts) and, rerun on one rank, bitwise against the one-rank output files."""
 import os
 import socket
 import subprocess
@@ -27,7 +27,7 @@ def _free_port():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,cases", [
-    (2, ["k2_shared", "k1_blocks_csr_s_damp", "k4_shared_s_damp", "k1_L3"]),
+    (2, ["k2_shared", "k1_blocks_csr_s_damp", "k4_shared_s_damp", "k1_L3", "k1_mle"]),
     (3, ["k2_shared", "k1_blocks_csr_s_damp"]),
 ])
 def test_sharded_ranks_match_golden(world, cases):
