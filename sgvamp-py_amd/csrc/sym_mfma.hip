@@ -54,7 +54,7 @@ constexpr int MF_LDP = 34;   // staging row pitch (doubles): conflict-free both 
 // [s*NG, (s+1)*NG) over the whole chunk (NS*NG groups of 4 columns, NG groups of
 // registers per wave).  NS = 2 was measured slower than one 16x16x4 group (the
 // repeat R reads of the second set go back to HBM); the launcher uses NS = 1.
-template <int NG, int NW, int NS>
+template <int NG, int NW, int NS, int PD>
 __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restrict__ items,
                                                          const double* __restrict__ pk, int ncol,
                                                          double* __restrict__ rowpart,
@@ -63,6 +63,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restri
   constexpr int WC = MF_CW / NWS;  // columns per wave
   constexpr int NT = WC / 32;      // 32-column steps per wave
   static_assert(NT >= 1, "at least one step per wave");
+  static_assert(PD >= 1 && NT % PD == 0, "prefetch depth divides the steps per row group");
   __shared__ double red[2][NW][256];
   __shared__ __attribute__((aligned(16))) double stg[NW][16 * MF_LDP];
   const SymItem it = items[blockIdx.x];
@@ -124,9 +125,11 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restri
     }
   };
   const int ng = (it.H + 15) / 16;
-  d2 cfn[4];
+  // ring of PD steps in flight per wave
+  d2 cfq[PD][4];
   double bcn[4][NG];
-  load_cf(0, 0, cfn);
+#pragma unroll
+  for (int p = 0; p < PD; ++p) load_cf(0, p, cfq[p]);
   load_bcol(0, bcn);
 
 #pragma unroll 1
@@ -144,14 +147,15 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restri
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       d2 cf[4], rf[4];
+      const int slot = t % PD;                         // compile-time after unrolling
 #pragma unroll
-      for (int a = 0; a < 4; ++a) cf[a] = cfn[a];
-      // the next step's loads go out here, ahead of this step's LDS and MFMA work
-      if (t + 1 < NT) {
-        load_cf(g, t + 1, cfn);
+      for (int a = 0; a < 4; ++a) cf[a] = cfq[slot][a];
+      // step (g, t) + PD goes out here, ahead of this step's LDS and MFMA work
+      if (t + PD < NT) {
+        load_cf(g, t + PD, cfq[slot]);
       } else if (g + 1 < ng) {
-        load_cf(g + 1, 0, cfn);
-        load_bcol(g + 1, bcn);
+        load_cf(g + 1, t + PD - NT, cfq[slot]);
+        if (t + PD == NT) load_bcol(g + 1, bcn);
       }
       lds_order();                                     // previous step's tile reads issued
 #pragma unroll
@@ -166,13 +170,16 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restri
       lds_order();                                     // tile written
 #pragma unroll
       for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + (4 * r + n4) * MF_LDP + 2 * pc);
+      // x halves of all 4*NG chains, then the y halves: a chain's two MFMAs are
+      // 4*NG issues apart instead of back to back (same per-chain order)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int q = 0; q < NG; ++q) {
-          drow[r][q] = MFMA4(rf[r].x, brow[t][0][q], drow[r][q]);
-          drow[r][q] = MFMA4(rf[r].y, brow[t][1][q], drow[r][q]);
-        }
+        for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(rf[r].x, brow[t][0][q], drow[r][q]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(rf[r].y, brow[t][1][q], drow[r][q]);
     }
     // row sums: the 4 blocks (lanes differing in bits 2,3), then the waves in order
     double* rb = red[g & 1][wid];
@@ -359,11 +366,11 @@ __global__ __launch_bounds__(256) void k_pack16(PassArgs pa, int ncol, int64_t m
   pk[t] = c < ncol ? pa.in[c][i] : 0.0;
 }
 
-template <int NG, int NW, int NS>
+template <int NG, int NW, int NS, int PD>
 static void launch_mf(const SymItem* d_items, int nitems, const double* d_pk, int nc,
                       double* rowpart, double* colpart, hipStream_t st) {
-  hipLaunchKernelGGL((k_sym_mfma<NG, NW, NS>), dim3(nitems), dim3(NW * 64), 0, st, d_items, d_pk,
-                     nc, rowpart, colpart);
+  hipLaunchKernelGGL((k_sym_mfma<NG, NW, NS, PD>), dim3(nitems), dim3(NW * 64), 0, st, d_items,
+                     d_pk, nc, rowpart, colpart);
 }
 
 hipError_t launch_sym_mfma(int nc, const SymItem* d_items, int nitems, const PassArgs& pa,
@@ -377,8 +384,9 @@ hipError_t launch_sym_mfma(int nc, const SymItem* d_items, int nitems, const Pas
   // pressure) and splitting the groups over two wave sets (the repeat R reads do
   // not come from cache): measured in DESIGN.md
   switch ((nc + 3) / 4) {
-    case 1: launch_mf<1, 4, 1>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
-    case 2: launch_mf<2, 4, 1>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
+    // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
+    case 1: launch_mf<1, 4, 1, 2>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
+    case 2: launch_mf<2, 4, 1, 2>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
     default:
       hipLaunchKernelGGL(k_sym_mfma16, dim3(nitems), dim3(256), 0, st, d_items, d_pk, nc, rowpart,
                          colpart);

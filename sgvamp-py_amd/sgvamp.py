@@ -18,6 +18,7 @@ Same constructor and ``infer`` arguments, same log lines, same output files
 * all vector arithmetic runs in libsgvamp_hip.so; there is no CPU fallback.
 """
 import csv
+import gc
 import logging
 import os
 import time
@@ -292,6 +293,10 @@ class VAMP:
         self._out_pool = ThreadPoolExecutor(max_workers=1)   # waits for the output copies
         self._next_probes = self._submit_probes()
         self._pending_write = None
+        # everything allocated so far (imports, LD upload) lives for the whole run:
+        # keep it out of the cyclic collector's scans, whose full passes otherwise
+        # stall an iteration for milliseconds at a time
+        gc.freeze()
         if self.rank == 0:
             logging.debug(f"a = {self.a}")
 
