@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--share-device", action="store_true",
                    help="rehearsal: every rank on device 0 with the host exchange (RCCL refuses "
                         "two ranks on one device); timings are then not a multi-GPU result")
+    p.add_argument("--exchange", choices=["auto", "rccl", "host"], default="auto",
+                   help="cross-rank exchange; auto = RCCL when N > 1, none at N = 1.  An explicit "
+                        "choice at N = 1 runs a one-rank communicator (measures the exchange cost)")
     p.add_argument("--prior", choices=["matched", "cli"], default="matched")
     p.add_argument("--ridge", type=float, default=0.0, help="--s of the CLI (C5: 0.1)")
     p.add_argument("--lmmse-damp", type=int, default=0, help="--lmmse-damp of the CLI (C5: 1)")
@@ -145,7 +148,8 @@ def main():
     K = args.K
     t_setup = time.perf_counter()
     eng = Engine(sizes, K, ld_of=[0] * K, comm=comm, device=device,
-                 exchange="host" if args.share_device else None)
+                 exchange="host" if args.share_device else
+                 (None if args.exchange == "auto" else args.exchange))
     eng.set_ld_packing(args.ld_format == "packed")
     beta, _ = make_problem(eng, comm, args)
     N_list = [args.nsamp] * K

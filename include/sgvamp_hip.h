@@ -82,7 +82,9 @@ const char* sgv_last_error(const sgv_ctx* ctx);
 /* Replaces mpi4py COMM_WORLD (src/main.py:16-18) and the per-iteration K x M
  * bcast all-gather (src/sgvamp.py:228-233), which disappears because all cohorts
  * of a marker are co-located.  What remains are ordered reductions of per-block
- * partial sums (ncclAllGather).  id: 128 bytes (ncclUniqueId) from rank 0. */
+ * partial sums (ncclAllGather).  id: 128 bytes (ncclUniqueId) from rank 0.
+ * nranks may be 1: a real one-rank communicator then carries the same gather
+ * (rehearses the RCCL calls on a single GPU; results bitwise unchanged). */
 int sgv_comm_unique_id(char* id_out /* 128 bytes */);
 int sgv_comm_init(sgv_ctx* ctx, int nranks, int rank, const char* id /* 128 bytes */,
                   const int* nblk_per_rank /* [nranks] */);

@@ -244,7 +244,7 @@ static int reduce_dev(sgv_ctx* c, int nv, const int* d_begin, const Map16& map, 
     HIPCHK(hipMemcpyAsync(c->d_bsum_all, c->h_bsum_all, sizeof(double) * cnt * c->nranks,
                           hipMemcpyHostToDevice, c->st));
   }
-  if (c->nranks > 1) {
+  if (c->comm || c->host_ag) {   // [nranks][nbmax][nv] gathered partials, also at one rank
     src = c->d_bsum_all;
     nr = c->nranks;
     nbm = c->nbmax;
@@ -876,7 +876,6 @@ extern "C" int sgv_comm_init(sgv_ctx* c, int nranks, int rank, const char* id,
   ENTER(c);
   if (!id) return fail(c, SGV_ERR_ARG, "bad comm arguments");
   CHK(comm_args(c, nranks, rank, nblk_per_rank));
-  if (nranks == 1) return SGV_OK;
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof uid);
   NCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
@@ -888,7 +887,6 @@ extern "C" int sgv_comm_init_host(sgv_ctx* c, int nranks, int rank, const int* n
   ENTER(c);
   if (!fn) return fail(c, SGV_ERR_ARG, "allgather callback is null");
   CHK(comm_args(c, nranks, rank, nblk_per_rank));
-  if (nranks == 1) return SGV_OK;
   CHK(comm_buffers(c, nranks, rank, nblk_per_rank));
   const size_t per = (size_t)c->nbmax * MAXNV;
   HIPCHK(hipHostMalloc(&c->h_bsum, sizeof(double) * per));

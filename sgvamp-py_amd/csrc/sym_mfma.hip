@@ -210,15 +210,11 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restri
 #pragma unroll
   for (int q = 0; q < NG; ++q) {
     const int cc = cq0 + 4 * q + n4;
-    if (cc < ncol) {
+    if (cc < ncol) {   // whole slot, 16-B stores (columns the finalize skips: don't care)
       double* out = colpart + ((int64_t)it.item * ncol + cc) * MF_CW;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int jl = cw0 + 32 * t + 2 * pc + e;
-          if (jl < it.nc && it.c0 + jl >= it.diag_end) out[jl] = dcol[t][e][q];
-        }
+        *(d2*)(out + cw0 + 32 * t + 2 * pc) = d2{dcol[t][0][q], dcol[t][1][q]};
     }
   }
 }
@@ -342,17 +338,13 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymItem* __restrict
   }
 
   // column sums (complete over the panel's rows), right of the diagonal block only
-  if (lo < ncol) {
+  if (lo < ncol) {   // whole slot, 16-B stores (columns the finalize skips: don't care)
     double* out = colpart + ((int64_t)it.item * ncol + lo) * MF_CW;
 #pragma unroll
     for (int t = 0; t < MF_NT; ++t)
 #pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int jl = cw0 + 32 * t + 2 * (hi + 4 * r) + e;
-          if (jl < it.nc && it.c0 + jl >= it.diag_end) out[jl] = dcol[t][e][r];
-        }
+      for (int r = 0; r < 4; ++r)
+        *(d2*)(out + cw0 + 32 * t + 2 * (hi + 4 * r)) = d2{dcol[t][0][r], dcol[t][1][r]};
   }
 }
 

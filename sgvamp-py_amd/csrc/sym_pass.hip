@@ -114,18 +114,18 @@ __global__ __launch_bounds__(256) void k_sym_pass(const SymItem* __restrict__ it
       rowpart[((int64_t)it.item * SYM_H + rbase + rr) * NC + cc] = y;
   }
 
-  // column parts: waves 0..3 in order
+  // column parts: waves 0..3 in order.  The item's whole NC x CW slot is
+  // written with 16-B stores, a wave covering 1 KiB contiguously: columns the
+  // finalize never reads (inside the diagonal block, past the block edge) get
+  // don't-care values.  Per-column predicated 8-B stores here cost ~8 % of the
+  // pass (measured) for < 1 % of its bytes.
   if (has_cols) {
     __syncthreads();
-    double* out = colpart + (int64_t)it.item * NC * CW;
+    d2* out = (d2*)(colpart + (int64_t)it.item * NC * CW);
     for (int t = threadIdx.x; t < NC * CW / 2; t += 256) {
       const int c = t / (CW / 2), q = t % (CW / 2);
-      const int jl = 2 * q;
       const d2 a = cbw[0][c][q], b = cbw[1][c][q], e = cbw[2][c][q], f = cbw[3][c][q];
-      const double s0 = ((a.x + b.x) + e.x) + f.x;
-      const double s1 = ((a.y + b.y) + e.y) + f.y;
-      if (jl < it.nc && it.c0 + jl >= it.diag_end) out[c * CW + jl] = s0;
-      if (jl + 1 < it.nc && it.c0 + jl + 1 >= it.diag_end) out[c * CW + jl + 1] = s1;
+      out[t] = d2{((a.x + b.x) + e.x) + f.x, ((a.y + b.y) + e.y) + f.y};
     }
   }
 }

@@ -19,7 +19,10 @@ class Engine:
         """block_sizes: global LD block sizes (marker order).  ld_of[k]: index of
         the LD matrix cohort k uses (cohorts sharing an LD share LD passes).
         exchange: "rccl" (default) or "host" (the communicator's allgather_f64
-        carries the per-block partials; env SGV_EXCHANGE overrides the default)."""
+        carries the per-block partials; env SGV_EXCHANGE overrides the default).
+        With one rank no communicator is made unless `exchange` is passed
+        explicitly (a one-rank RCCL/host exchange: same results, used to rehearse
+        the exchange on one GPU)."""
         from comm import SingleComm
 
         self.comm = comm or SingleComm()
@@ -52,7 +55,7 @@ class Engine:
         if self.exchange not in ("rccl", "host"):
             raise ValueError("exchange must be 'rccl' or 'host', got %r" % self.exchange)
         self._ag_cb = None
-        if self.nranks > 1:
+        if self.nranks > 1 or exchange is not None:
             counts = np.array([r1 - r0 for r0, r1 in self.ranges], dtype=np.int32)
             if self.exchange == "host":
                 self._ag_cb = hb.make_allgather(self.comm, self.nranks)

@@ -51,3 +51,46 @@ def test_sharded_ranks_match_golden(world, cases):
     for r, (p, out) in enumerate(zip(procs, outs)):
         assert p.returncode == 0, "rank %d failed:\n%s" % (r, out[-4000:])
     assert outs[0].count("-> OK") == len(cases), outs[0]
+
+
+def _run_case_files(name, out, exchange):
+    """One-rank run of golden case `name`; returns {file name: bytes}."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "sgvamp-py_amd"))
+    from sgvamp import VAMP, BlockLD
+    from tests.golden import Case
+
+    c = Case(name)
+    f = c.flags
+    lds = [BlockLD(blocks, s=f["s"]) for blocks in c.ld_blocks]
+    R = lds[0] if len(lds) == 1 else [lds[c.ld_of[k]] for k in range(c.K)]
+    Nt = sum(c.N)
+    v = VAMP(N=c.N, Nt=Nt, M=c.M, K=c.K, rho=f["rho"], gamw=f["gamw"], gam1=f["gam1"],
+             a=np.array(c.N) / Nt, prior_vars=f["prior_vars"], prior_probs=f["prior_probs"],
+             out_dir=str(out), out_name=name, seed=f["seed"], device=0, exchange=exchange)
+    v.infer(R, c.r, f["iterations"], x0=c.x0, cg_maxit=f["cg_maxit"],
+            em_prior_maxit=f["em_prior_maxit"], learn_gamw=f["learn_gamw"],
+            lmmse_damp=f["lmmse_damp"], prior_update=f["prior_update"],
+            update_prior_from=f["update_prior_from"])
+    v.engine.close()
+    return {fn: open(os.path.join(out, fn), "rb").read() for fn in sorted(os.listdir(out))
+            if fn.endswith(".bin")}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["k2_shared", "k1_blocks_csr_s_damp"])
+def test_one_rank_exchange_rehearsal_bitwise(name, tmp_path):
+    """The RCCL exchange on one GPU: a real one-rank communicator (ncclCommInitRank,
+    ncclAllGather on the library stream) carries the ordered per-block partials;
+    the host exchange likewise.  Both must leave every output file bitwise
+    identical to the run without a communicator."""
+    (tmp_path / "none").mkdir()
+    base = _run_case_files(name, tmp_path / "none", None)
+    for ex in ("rccl", "host"):
+        d = tmp_path / ex
+        d.mkdir()
+        got = _run_case_files(name, d, ex)
+        assert got.keys() == base.keys() and len(base) > 0
+        for fn in base:
+            assert got[fn] == base[fn], (ex, fn)

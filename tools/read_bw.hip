@@ -49,6 +49,67 @@ __global__ __launch_bounds__(256) void k_read_rows(const d2* __restrict__ p, siz
   if (acc.x == 12345.678) out[0] = acc.y;
 }
 
+// occupancy sweep: U 1-KiB row loads in flight per wave, WGs per CU pinned by
+// dynamic LDS (160 KiB / lds_kib)
+template <int U>
+__global__ __launch_bounds__(256) void k_read_occ(const d2* __restrict__ p, size_t n, int per,
+                                                  double* out) {
+  extern __shared__ double dyn[];
+  const size_t base = (size_t)blockIdx.x * per * 256;
+  d2 acc = {0.0, 0.0};
+  for (int j = 0; j < per; j += U) {
+    d2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      v[u] = __builtin_nontemporal_load(
+          (const __attribute__((address_space(1))) d2*)(p + base + (size_t)(j + u) * 256 + threadIdx.x));
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u];
+  }
+  if (acc.x == 12345.678) { dyn[threadIdx.x] = acc.y; out[0] = dyn[(threadIdx.x + 1) & 255]; }
+}
+
+// LD-pass tile patterns over a row-major matrix with row stride W doubles:
+// one WG per 256-row x 1024-column tile; each wave owns 8 consecutive rows per
+// sub-sweep.  ROWMAJ = 0: the 8 rows are read together, 1 KiB per row per step
+// (k_sym_pass order); ROWMAJ = 1: one row's 8 KiB at a time.
+template <int ROWMAJ>
+__global__ __launch_bounds__(256) void k_read_tile(const double* __restrict__ p, int W, int ntc,
+                                                   double* out) {
+  extern __shared__ double dyn[];
+  const int tr = blockIdx.x / ntc, tc = blockIdx.x % ntc;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const double* base = p + (size_t)tr * 256 * W + tc * 1024 + 2 * lane;
+  d2 acc = {0.0, 0.0};
+  for (int sub = 0; sub < 8; ++sub) {
+    const int r0 = sub * 32 + wid * 8;
+    if (ROWMAJ == 0) {
+#pragma unroll 2
+      for (int s = 0; s < 8; ++s) {
+        d2 v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+          v[r] = __builtin_nontemporal_load((const __attribute__((address_space(1))) d2*)(
+              base + (size_t)(r0 + r) * W + s * 128));
+#pragma unroll
+        for (int r = 0; r < 8; ++r) acc += v[r];
+      }
+    } else {
+#pragma unroll 2
+      for (int r = 0; r < 8; ++r) {
+        d2 v[8];
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+          v[s] = __builtin_nontemporal_load((const __attribute__((address_space(1))) d2*)(
+              base + (size_t)(r0 + r) * W + s * 128));
+#pragma unroll
+        for (int s = 0; s < 8; ++s) acc += v[s];
+      }
+    }
+  }
+  if (acc.x == 12345.678) { dyn[threadIdx.x] = acc.y; out[0] = dyn[(threadIdx.x + 1) & 255]; }
+}
+
 template <class F>
 static void timeit(const char* name, F launch, double bytes) {
   hipEvent_t e0, e1;
@@ -95,6 +156,32 @@ int main() {
     timeit(nm, [&] { hipLaunchKernelGGL(k_read_rows<true>, dim3(grid), dim3(256), 0, 0, p, n, per, out); }, (double)grid * per * 256 * 16);
     snprintf(nm, sizeof nm, "chunked per-block %4d KiB plain", per * 4);
     timeit(nm, [&] { hipLaunchKernelGGL(k_read_rows<false>, dim3(grid), dim3(256), 0, 0, p, n, per, out); }, (double)grid * per * 256 * 16);
+  }
+  CK(hipFuncSetAttribute((const void*)k_read_occ<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  CK(hipFuncSetAttribute((const void*)k_read_occ<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  CK(hipFuncSetAttribute((const void*)k_read_tile<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  CK(hipFuncSetAttribute((const void*)k_read_tile<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  for (int W : {25088, 25104, 24576, 24592, 24704, 16384, 16400, 12288, 12304, 20480, 20496}) {   // row strides (doubles)
+    const int ntc = W / 1024;
+    const int ntr = (int)(n * 2 / ((size_t)256 * W));
+    const size_t grid = (size_t)ntr * ntc;
+    const double by = (double)grid * 256 * 1024 * 8;
+    for (int lds_kib : {64}) {
+      char nm[80];
+      snprintf(nm, sizeof nm, "tile W=%d %d WG/CU 8rows x 1KiB", W, 160 / lds_kib);
+      timeit(nm, [&] { hipLaunchKernelGGL(k_read_tile<0>, dim3(grid), dim3(256), lds_kib * 1024, 0, (const double*)p, W, ntc, out); }, by);
+      snprintf(nm, sizeof nm, "tile W=%d %d WG/CU 1row x 8KiB", W, 160 / lds_kib);
+      timeit(nm, [&] { hipLaunchKernelGGL(k_read_tile<1>, dim3(grid), dim3(256), lds_kib * 1024, 0, (const double*)p, W, ntc, out); }, by);
+    }
+  }
+  for (int lds_kib : {80, 54, 40, 32, 20, 10}) {
+    const int per = 256;
+    const size_t grid = n / ((size_t)per * 256);
+    char nm[80];
+    snprintf(nm, sizeof nm, "occ %d WG/CU u8  (%3d KiB/CU in flight)", 160 / lds_kib, 160 / lds_kib * 4 * 8);
+    timeit(nm, [&] { hipLaunchKernelGGL(k_read_occ<8>, dim3(grid), dim3(256), lds_kib * 1024, 0, p, n, per, out); }, (double)grid * per * 256 * 16);
+    snprintf(nm, sizeof nm, "occ %d WG/CU u16 (%3d KiB/CU in flight)", 160 / lds_kib, 160 / lds_kib * 4 * 16);
+    timeit(nm, [&] { hipLaunchKernelGGL(k_read_occ<16>, dim3(grid), dim3(256), lds_kib * 1024, 0, p, n, per, out); }, (double)grid * per * 256 * 16);
   }
   return 0;
 }
