@@ -24,9 +24,13 @@ def main():
     ap.add_argument("--nsamp", type=int, default=2000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--ncols", default="1,2,3,4,8,12,16")
+    ap.add_argument("--lib", default=None, help="A/B: load this build of libsgvamp_hip.so")
     ap.add_argument("--formats", default="packed,packed_valu,dense",
                     help="packed (f64 MFMA pass from 3 columns), packed_valu, dense")
     a = ap.parse_args()
+    if a.lib:
+        import hip_backend
+        hip_backend.load(a.lib)
     sizes = [a.block_size] * a.blocks
     M = sum(sizes)
     for fmt in a.formats.split(","):
