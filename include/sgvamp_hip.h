@@ -208,6 +208,11 @@ int sgv_lmmse(sgv_ctx* ctx, int it, const double* gamw, const double* gam2,
 /* Metrics src/sgvamp.py:379-387: out[0] = <xhat1, x0>, out[1] = |xhat1|^2,
  * out[2] = |xhat1 - x0|^2, out[3] = |x0|^2 (global sums). */
 int sgv_metrics(sgv_ctx* ctx, double* out4);
+/* Split form of sgv_metrics: begin queues the kernel and the ordered reduction
+ * (call after sgv_denoise; xhat1/x0 must not change before end), end waits for
+ * it and returns the same 4 sums.  Lets the host skip a sync per iteration. */
+int sgv_metrics_begin(sgv_ctx* ctx);
+int sgv_metrics_end(sgv_ctx* ctx, double* out4);
 
 /* ---- operator seam, exposed for tests ------------------------------------ */
 

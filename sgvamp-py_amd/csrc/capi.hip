@@ -101,6 +101,17 @@ struct sgv_ctx {
   double* d_out = nullptr;
   double* h_out[2] = {nullptr, nullptr};
   hipEvent_t ev_out[2] = {nullptr, nullptr};
+  // probe upload: two pinned slots used alternately, stream-ordered copy into
+  // d_probe (no host wait; a slot is reused two iterations later)
+  int8_t* h_probe[2] = {nullptr, nullptr};
+  hipEvent_t ev_probe[2] = {nullptr, nullptr};
+  int8_t* d_probe = nullptr;
+  size_t probe_cap = 0;
+  int probe_slot = 0;
+  // metrics queued behind the denoiser, read at the end of the iteration
+  double* h_met = nullptr;        // fine-grained pinned [4]
+  hipEvent_t ev_met = nullptr;
+  int met_pending = 0;
   size_t pk_cap = 0;
   // chunk / row-group layouts
   int nch = 0;
@@ -228,6 +239,10 @@ static void resolve_timers(sgv_ctx* c) {
 // partials [nparts][nv] -> d_dst[map.d[v]] (global, ordered); stays on device
 static int reduce_dev(sgv_ctx* c, int nv, const int* d_begin, const Map16& map, double* d_dst,
                       int op = 0) {
+  if (!c->comm && !c->host_ag) {   // one rank: fused, bitwise the same as the two steps
+    HIPCHK(launch_reduce_local(c->d_part, nv, d_begin, c->nblk, map, d_dst, c->st, op));
+    return SGV_OK;
+  }
   HIPCHK(launch_reduce_blocks(c->d_part, nv, d_begin, c->nblk, c->d_bsum, c->st, op));
   const double* src = c->d_bsum;
   int nr = 1, nbm = c->nblk;
@@ -253,9 +268,10 @@ static int reduce_dev(sgv_ctx* c, int nv, const int* d_begin, const Map16& map, 
   return SGV_OK;
 }
 
+// the ordered total is stored by the reduction kernel straight into h_tot
+// (fine-grained pinned memory): no copy launch before the host reads it
 static int reduce_host(sgv_ctx* c, int nv, const int* d_begin, double* out, int op = 0) {
-  CHK(reduce_dev(c, nv, d_begin, identity_map(), c->d_tot, op));
-  HIPCHK(hipMemcpyAsync(c->h_tot, c->d_tot, sizeof(double) * nv, hipMemcpyDeviceToHost, c->st));
+  CHK(reduce_dev(c, nv, d_begin, identity_map(), c->h_tot, op));
   CHK(stream_wait(c));
   resolve_timers(c);
   std::memcpy(out, c->h_tot, sizeof(double) * nv);
@@ -288,6 +304,32 @@ static int h2d(sgv_ctx* c, const void* host, size_t bytes) {
   std::memcpy(c->h_stage, host, bytes);
   HIPCHK(hipMemcpyAsync(c->d_stage, c->h_stage, bytes, hipMemcpyHostToDevice, c->st));
   return stream_wait(c);
+}
+
+// K x Mloc int8 probes -> d_probe, queued on the stream without a host wait
+static int upload_probes(sgv_ctx* c, const int8_t* probes) {
+  const size_t bytes = std::max<size_t>((size_t)c->K * c->Mloc, 8);
+  if (bytes > c->probe_cap) {
+    CHK(stream_wait(c));
+    for (int i = 0; i < 2; ++i) {
+      if (c->h_probe[i]) HIPCHK(hipHostFree(c->h_probe[i]));
+      c->h_probe[i] = nullptr;
+      HIPCHK(hipHostMalloc(&c->h_probe[i], bytes));
+      if (!c->ev_probe[i]) HIPCHK(hipEventCreateWithFlags(&c->ev_probe[i], hipEventDisableTiming));
+    }
+    if (c->d_probe) HIPCHK(hipFree(c->d_probe));
+    c->d_probe = nullptr;
+    HIPCHK(hipMalloc(&c->d_probe, bytes));
+    c->probe_cap = bytes;
+  }
+  const int slot = c->probe_slot;
+  c->probe_slot ^= 1;
+  HIPCHK(hipEventSynchronize(c->ev_probe[slot]));   // this slot's previous copy (long done)
+  std::memcpy(c->h_probe[slot], probes, (size_t)c->K * c->Mloc);
+  HIPCHK(hipMemcpyAsync(c->d_probe, c->h_probe[slot], (size_t)c->K * c->Mloc,
+                        hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipEventRecord(c->ev_probe[slot], c->st));
+  return SGV_OK;
 }
 
 static int upload_vec(sgv_ctx* c, const double* host, double* dpad) {
@@ -776,7 +818,7 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   CREATE_HIP(hipMemcpy(c->d_counts, &nblk, sizeof(int), hipMemcpyHostToDevice));
   CREATE_HIP(hipMalloc(&c->d_tot, sizeof(double) * 64));
   CREATE_HIP(hipMalloc(&c->d_pq, sizeof(double) * 2 * MAXC));
-  CREATE_HIP(hipHostMalloc(&c->h_tot, sizeof(double) * 64));
+  CREATE_HIP(hipHostMalloc(&c->h_tot, sizeof(double) * 64, hipHostMallocCoherent));
   c->xnz.assign(2 * K, 0);
   c->rx0_valid.assign(2 * K, 0);
 #undef CREATE_HIP
@@ -802,7 +844,12 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   for (int i = 0; i < 2; ++i) {
     if (c->h_out[i]) (void)hipHostFree(c->h_out[i]);
     if (c->ev_out[i]) (void)hipEventDestroy(c->ev_out[i]);
+    if (c->h_probe[i]) (void)hipHostFree(c->h_probe[i]);
+    if (c->ev_probe[i]) (void)hipEventDestroy(c->ev_probe[i]);
   }
+  if (c->d_probe) (void)hipFree(c->d_probe);
+  if (c->h_met) (void)hipHostFree(c->h_met);
+  if (c->ev_met) (void)hipEventDestroy(c->ev_met);
   for (BlkDesc* d : c->d_blks) (void)hipFree(d);
   (void)hipFree(c->d_ch);
   (void)hipFree(c->d_ch_doff);
@@ -1307,10 +1354,10 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
   int passes = 0;
 
   // probes u_k (:326), int8 +-1 -> f64
-  CHK(h2d(c, probes, (size_t)K * c->Mloc));
+  CHK(upload_probes(c, probes));
   for (int k = 0; k < K; ++k)
-    HIPCHK(launch_unpack_i8(c->d_ch, c->nch, c->d_ch_doff,
-                            (const int8_t*)c->d_stage + (size_t)k * c->Mloc, c->U[k], c->st));
+    HIPCHK(launch_unpack_i8(c->d_ch, c->nch, c->d_ch_doff, c->d_probe + (size_t)k * c->Mloc,
+                            c->U[k], c->st));
 
   // warm start needs R_s x0: carried from the previous iteration (rs_rec), or the
   // previous gamw pass; a pass only when X was set from outside
@@ -1475,9 +1522,7 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
       CHK(ld_pass(c, ld, nc, pa));
       ++passes;
       double gt[MAXC];
-      CHK(reduce_dev(c, nc, ld_parts(c, ld), map, c->d_tot));
-      HIPCHK(hipMemcpyAsync(c->h_tot, c->d_tot, sizeof(double) * ncol, hipMemcpyDeviceToHost,
-                            c->st));
+      CHK(reduce_dev(c, nc, ld_parts(c, ld), map, c->h_tot));
       CHK(stream_wait(c));
       resolve_timers(c);
       std::memcpy(gt, c->h_tot, sizeof(double) * ncol);
@@ -1507,6 +1552,34 @@ extern "C" int sgv_metrics(sgv_ctx* c, double* out4) {
   if (!out4) return fail(c, SGV_ERR_ARG, "out4 is null");
   HIPCHK(launch_metrics(c->d_ch, c->nch, c->xhat1, c->x0, c->d_part, c->st));
   return reduce_host(c, 4, c->d_ch_begin, out4);
+}
+
+// The same sums, queued without a host wait (xhat1 and x0 are not written
+// again before sgv_metrics_end); the ordered totals land in pinned memory.
+// With the host exchange the reduction itself waits, so begin completes it.
+extern "C" int sgv_metrics_begin(sgv_ctx* c) {
+  ENTER(c);
+  if (!c->h_met) {
+    HIPCHK(hipHostMalloc(&c->h_met, sizeof(double) * 4, hipHostMallocCoherent));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_met, hipEventDisableTiming));
+  }
+  HIPCHK(launch_metrics(c->d_ch, c->nch, c->xhat1, c->x0, c->d_part, c->st));
+  CHK(reduce_dev(c, 4, c->d_ch_begin, identity_map(), c->h_met));
+  HIPCHK(hipEventRecord(c->ev_met, c->st));
+  c->met_pending = 1;
+  return SGV_OK;
+}
+
+extern "C" int sgv_metrics_end(sgv_ctx* c, double* out4) {
+  ENTER(c);
+  if (!out4) return fail(c, SGV_ERR_ARG, "out4 is null");
+  if (!c->met_pending) return fail(c, SGV_ERR_ARG, "sgv_metrics_end without sgv_metrics_begin");
+  hipError_t e;
+  while ((e = hipEventQuery(c->ev_met)) == hipErrorNotReady) __builtin_ia32_pause();
+  if (e != hipSuccess) return fail(c, SGV_ERR_HIP, "metrics wait: %s", hipGetErrorString(e));
+  std::memcpy(out4, c->h_met, sizeof(double) * 4);
+  c->met_pending = 0;
+  return SGV_OK;
 }
 
 // ---------------------------------------------------------------------------

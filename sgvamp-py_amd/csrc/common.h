@@ -196,6 +196,8 @@ hipError_t launch_sym_finalize(int nc, int cls, const SymPanel* d_panels, int np
 // op 0: ordered sum; op 1: min (exact in any order)
 hipError_t launch_reduce_blocks(const double* d_part, int nv, const int* d_begin, int nblk,
                                 double* d_bsum, hipStream_t st, int op = 0);
+hipError_t launch_reduce_local(const double* d_part, int nv, const int* d_begin, int nblk,
+                               const Map16& map, double* d_dst, hipStream_t st, int op = 0);
 hipError_t launch_reduce_total(const double* d_bsum_all, int nranks, int nbmax, int nv,
                                const int* d_counts, const Map16& map, double* d_dst,
                                hipStream_t st, int op = 0);

@@ -472,6 +472,40 @@ __global__ void k_reduce_total(const double* __restrict__ bsum_all, int nranks, 
   dst[map.d[v]] = s;
 }
 
+// One rank, no exchange: both steps in one launch.  Wave v computes every
+// block's sum exactly as k_reduce_blocks does (same lane stride, same
+// wave_sum) and folds them in block order exactly as k_reduce_total does, so
+// the result is bitwise the two-kernel one.
+__global__ __launch_bounds__(WAVE) void k_reduce_local(const double* __restrict__ part, int nv,
+                                                       const int* __restrict__ begin, int nblk,
+                                                       Map16 map, double* __restrict__ dst,
+                                                       int op) {
+  const int v = blockIdx.x, lane = threadIdx.x;
+  double tot = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    const int p0 = begin[b], p1 = begin[b + 1];
+    double s;
+    if (op == 0) {
+      s = 0.0;
+      for (int p = p0 + lane; p < p1; p += WAVE) s += part[(int64_t)p * nv + v];
+      s = wave_sum(s);
+    } else {
+      s = __builtin_inf();
+      for (int p = p0 + lane; p < p1; p += WAVE) s = fmin(s, part[(int64_t)p * nv + v]);
+      for (int o = 32; o > 0; o >>= 1) s = fmin(s, __shfl_xor(s, o, WAVE));
+    }
+    tot = (b == 0) ? s : (op == 0 ? tot + s : fmin(tot, s));
+  }
+  if (lane == 0) dst[map.d[v]] = tot;
+}
+
+hipError_t launch_reduce_local(const double* d_part, int nv, const int* d_begin, int nblk,
+                               const Map16& map, double* d_dst, hipStream_t st, int op) {
+  hipLaunchKernelGGL(k_reduce_local, dim3(nv), dim3(WAVE), 0, st, d_part, nv, d_begin, nblk, map,
+                     d_dst, op);
+  return hipGetLastError();
+}
+
 hipError_t launch_reduce_total(const double* d_bsum_all, int nranks, int nbmax, int nv,
                                const int* d_counts, const Map16& map, double* d_dst,
                                hipStream_t st, int op) {

@@ -191,6 +191,15 @@ class Engine:
         self.ctx.sgv_metrics(hb.dptr(out))
         return out
 
+    def metrics_begin(self):
+        """Queue the metric sums behind the denoiser (no host wait)."""
+        self.ctx.sgv_metrics_begin()
+
+    def metrics_end(self):
+        out = np.zeros(4)
+        self.ctx.sgv_metrics_end(hb.dptr(out))
+        return out
+
     # ---- operator seam (tests) ------------------------------------------------
     def ld_matvec(self, ld, V_local):
         V = np.ascontiguousarray(np.atleast_2d(V_local), dtype=np.float64)

@@ -60,6 +60,8 @@ _SIGS = {
                   ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_int, _c_dbl_p, _c_int_p,
                   _c_int_p],
     "sgv_metrics": [_vp, _c_dbl_p],
+    "sgv_metrics_begin": [_vp],
+    "sgv_metrics_end": [_vp, _c_dbl_p],
     "sgv_ld_matvec": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, _c_dbl_p],
     "sgv_cg_solve": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, _c_dbl_p, _c_dbl_p, _c_dbl_p,
                      ctypes.c_int, ctypes.c_double, _c_int_p, _c_int_p],

@@ -180,12 +180,16 @@ class VAMP:
         """Native-endian f64, M values, no header.  Each rank writes its marker
         slice at its byte offset, so no gather is needed."""
         path = os.path.join(self.out_dir, fname)
+        # written from the array's buffer: .tobytes() would copy under the GIL
+        # (writer threads stalled the iteration loop by up to a switch interval)
+        buf = memoryview(np.ascontiguousarray(local, dtype=np.float64)).cast("B")
         fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
         try:
             if self.rank == 0:
                 os.ftruncate(fd, self.M * 8)
-            os.pwrite(fd, np.ascontiguousarray(local, dtype=np.float64).tobytes(),
-                      self.engine.marker0 * 8)
+            off, pos = self.engine.marker0 * 8, 0
+            while pos < len(buf):
+                pos += os.pwrite(fd, buf[pos:], off + pos)
         finally:
             os.close(fd)
 
@@ -291,6 +295,13 @@ class VAMP:
         self._probe_pool = ThreadPoolExecutor(max_workers=self.K)
         self._write_pool = ThreadPoolExecutor(max_workers=self.K + 1)
         self._out_pool = ThreadPoolExecutor(max_workers=1)   # waits for the output copies
+        # per-iteration CSV rows, appended in order off the main thread (the GPU
+        # would otherwise idle through each open/append/close).  Rows are handed
+        # to the writer just before the LMMSE call, while the main thread waits in
+        # C with the GIL released, so the writer's Python never delays a launch.
+        self._csv_pool = ThreadPoolExecutor(max_workers=1)
+        self._csv_futs = []
+        self._csv_rows = []
         self._next_probes = self._submit_probes()
         self._pending_write = None
         # everything allocated so far (imports, LD upload) lives for the whole run:
@@ -330,9 +341,26 @@ class VAMP:
             self._pending_write.result()
             self._pending_write = None
 
+    def _queue_csv(self, fn, *args):
+        if getattr(self, "_csv_pool", None) is None:
+            fn(*args)
+            return
+        self._csv_rows.append((fn, args))
+
+    def _submit_csv(self):
+        if not getattr(self, "_csv_rows", None):
+            return
+        rows, self._csv_rows = self._csv_rows, []
+        self._csv_futs = [f for f in self._csv_futs if not f.done() or f.result() is not None]
+        self._csv_futs.append(self._csv_pool.submit(lambda: [fn(*a) for fn, a in rows]))
+
     def finish(self):
+        self._submit_csv()
         self.flush()
-        for pool in ("_probe_pool", "_write_pool", "_out_pool"):
+        for f in getattr(self, "_csv_futs", []):
+            f.result()                    # re-raise a failed append
+        self._csv_futs = []
+        for pool in ("_probe_pool", "_write_pool", "_out_pool", "_csv_pool"):
             if getattr(self, pool, None) is not None:
                 getattr(self, pool).shutdown(wait=True)
                 setattr(self, pool, None)
@@ -345,11 +373,12 @@ class VAMP:
         gam1, gamw, alpha1, alpha2 = st["gam1"], st["gamw"], st["alpha1"], st["alpha2"]
         t_it = time.perf_counter()
         rec = dict(it=it)
+        # lazy %-arguments: nothing is formatted unless the level is enabled
         if rank == 0:
-            logging.info(f"\n -----ITERATION {it} -----")
+            logging.info("\n -----ITERATION %s -----", it)
         gam1s = np.array(gam1, dtype=np.float64)                      # :228-233
         if rank == 0:
-            logging.debug(f"gam1s={gam1s}")
+            logging.debug("gam1s=%s", gam1s)
             logging.info("...Data from all ranks collected")
 
         if it >= st["update_prior_from"]:                             # :242-259
@@ -366,12 +395,12 @@ class VAMP:
                     gam1s, self.a, self.sigmas, st["em_prior_maxit"], self.lam, self.omegas)
                 rec["em_steps"] = steps
                 if rank == 0:
-                    logging.info(f"... prior-learning EM algorithm performed {steps} steps "
-                                 f"and had final relative error = {err:0.9f}")
+                    logging.info("... prior-learning EM algorithm performed %s steps "
+                                 "and had final relative error = %0.9f", steps, err)
         if rank == 0:
-            logging.debug(f"lam={self.lam}")
-            logging.debug(f"omegas={self.omegas}")
-            logging.debug(f"sigmas={self.sigmas}")
+            logging.debug("lam=%s", self.lam)
+            logging.debug("omegas=%s", self.omegas)
+            logging.debug("sigmas=%s", self.sigmas)
             logging.info("...Denoising")
 
         alpha1_prev = list(alpha1)
@@ -385,6 +414,8 @@ class VAMP:
             rec["wait_write_ms"] = (time.perf_counter() - t0) * 1e3
             eng.outputs_begin(it % 2)
             self._pending_write = self._out_pool.submit(self._write_outputs, it, it % 2)
+        if self._has_x0:
+            eng.metrics_begin()       # of xhat1, read back at the end (:379-387)
         if st["return_xhat"]:
             xhat_loc = eng.get_vector(hb.VEC_XHAT1)
             full = xhat_loc
@@ -399,48 +430,50 @@ class VAMP:
             alpha1[k] = a1
             gam2[k] = gam1[k] * (1 - a1) / a1                         # :305
         if rank == 0:
-            logging.debug(f"[rank = {rank}] alpha1 = {alpha1[0]}")
-            logging.debug(f"[rank = {rank}] gam2 = {gam2[0]}")
+            logging.debug("[rank = %s] alpha1 = %s", rank, alpha1[0])
+            logging.debug("[rank = %s] gam2 = %s", rank, gam2[0])
         for k in range(K):
-            logging.info(f"...LMMSE cohort {k}")
+            logging.info("...LMMSE cohort %s", k)
         t0 = time.perf_counter()
         u = np.stack([f.result() for f in self._next_probes])        # :326
         rec["wait_probes_ms"] = (time.perf_counter() - t0) * 1e3
         self._next_probes = self._submit_probes()
+        self._submit_csv()            # previous iteration's rows, written during the LMMSE
         out, cg, passes = eng.lmmse(it, gamw, gam2, alpha1, alpha2, u, st["cg_maxit"],
                                     st["lmmse_damp"], rho, st["learn_gamw"])
         rec.update(cg_iters=cg[:, [0, 2]].tolist(), cg_info=cg[:, [1, 3]].tolist(),
                    ld_passes=passes)
         for k in range(K):
             if cg[k, 1] > 0:
-                logging.info(f"Rank {k} WARNING: CG 1 convergence after {cg[k, 1]} "
-                             f"iterations not achieved!")
+                logging.info("Rank %s WARNING: CG 1 convergence after %s "
+                             "iterations not achieved!", k, cg[k, 1])
             if cg[k, 3] > 0:
-                logging.info(f"Rank {k} WARNING: CG 2 convergence after {cg[k, 3]} "
-                             f"iterations not achieved!")
+                logging.info("Rank %s WARNING: CG 2 convergence after %s "
+                             "iterations not achieved!", k, cg[k, 3])
             alpha2[k] = out[k, hb.O_ALPHA2]
             gam1[k] = out[k, hb.O_GAM1]
             if st["learn_gamw"]:
                 gamw[k] = float(out[k, hb.O_GAMW])                    # :363-364
         if rank == 0:
-            logging.debug(f"[rank = {rank}] alpha2 = {alpha2[0]}")
-            logging.debug(f"gamw = {gamw[0]:0.9f} \n")
+            logging.debug("[rank = %s] alpha2 = %s", rank, alpha2[0])
+            logging.debug("gamw = %0.9f \n", gamw[0])
         for k in range(K):
             st["gamws"][k].append(gamw[k])                            # :373
             gamw[k] = max(gamw[k], 1.0)                               # :374
             if rank == 0 and self.write_files:
-                self.write_params_to_file([it, gamw[k], gam1[k], gam2[k], alpha1[k],
-                                           alpha2[k], self.lam], k)  # :377
+                self._queue_csv(self.write_params_to_file,
+                                [it, gamw[k], gam1[k], gam2[k], alpha1[k], alpha2[k],
+                                 self.lam], k)                        # :377
         if self._has_x0:                                              # :379-387
-            s = eng.metrics()
+            s = eng.metrics_end()
             alignment = s[0] / np.sqrt(s[1]) / np.sqrt(s[3])
             l2 = np.sqrt(s[2]) / np.sqrt(s[3])
             rec["metrics"] = (alignment, l2)
             if rank == 0:
-                logging.debug(f"Alignment(xhat1, x0) = {alignment:0.9f} \n")
-                logging.debug(f"L2_error(xhat1, x0) = {l2:0.9f} \n")
+                logging.debug("Alignment(xhat1, x0) = %0.9f \n", alignment)
+                logging.debug("L2_error(xhat1, x0) = %0.9f \n", l2)
                 if self.write_files:
-                    self.write_metrics_to_file([it, alignment, l2])
+                    self._queue_csv(self.write_metrics_to_file, [it, alignment, l2])
         rec.update(gamw=list(gamw), gam1=list(gam1), gam2=gam2, alpha1=list(alpha1),
                    alpha2=list(alpha2), lam=self.lam, wall_s=time.perf_counter() - t_it)
         self.history.append(rec)
