@@ -409,3 +409,50 @@ def test_vamp_medium_scale_shared_ld_vs_oracle(K, ridge, damp, tmp_path):
     assert [h["cg_iters"] for h in v.history] == [[list(c) for c in x] for x in t["cg_iters"]]
     assert [h.get("em_steps") for h in v.history][1:] == list(t["em_steps"])
     eng.close()
+
+
+@pytest.mark.parametrize("K", [1, 4])
+def test_vamp_50_iterations_vs_oracle(K, tmp_path):
+    """The north-star accuracy bar (BASELINE.json): xhat within 1e-5 relative of
+    the reference algorithm after 50 iterations.  K = 4 cohorts share one LD, so
+    the CG runs 8 columns through the f64 MFMA pass; K = 1 uses the VALU pass.
+    EM prior learning, the R_s x recurrence and LMMSE damping are on, as in a
+    production run.  Oracle: oracle/vamp_oracle.py (pinned to the reference's
+    golden fixtures by tests/test_oracle_golden.py)."""
+    tol = 1e-5                       # north_star: "<= 1e-5 rel error vs reference xhat"
+    sizes = [1300, 700, 1100]
+    nsamp = 900
+    M = sum(sizes)
+    rs = np.random.RandomState(21)
+    cm = M // 10
+    beta = np.zeros(M)
+    beta[rs.choice(M, cm, replace=False)] = rs.normal(0, np.sqrt(0.8 / cm), cm)
+    eng = Engine(sizes, K=K)
+    g = eng.synth_ld_g(0, 91, nsamp, beta).sum(axis=0)
+    rvec = []
+    for k in range(K):
+        y = g + np.random.RandomState(200 + k).normal(0, np.sqrt(0.2), nsamp)
+        eng.synth_r(k, 91, nsamp, y)
+        rvec.append(eng.get_vector(hb.VEC_R, k).copy())
+    blocks = [eng.get_ld_block(0, b) for b in range(len(sizes))]
+    N = [float(nsamp)] * K
+    prior = dict(prior_vars=[0.0, 0.8 / cm / K], prior_probs=[0.9, 0.1])
+    ridge = 0.05
+    v = VAMP(N=N, Nt=sum(N), M=M, K=K, rho=0.5, gamw=5.0, gam1=1e-6, a=[1 / K] * K,
+             out_dir=str(tmp_path), out_name="n50", seed=9, write_files=False, **prior)
+    x0 = beta * np.sqrt(nsamp)
+    v.attach_engine(eng, x0=x0)
+    eng.set_ridge(ridge)
+    its = 50
+    xh = v.infer(None, None, its, x0=x0, lmmse_damp=True, prior_update="em")
+    L = vo.BlockLD(blocks, s=ridge)
+    t = vo.infer([L], [0] * K, rvec, N, its, rho=0.5, gamw=5.0, gam1=1e-6, x0=x0, seed=9,
+                 lmmse_damp=True, reducer=vo.Reducer("blocked", bounds=L.bounds),
+                 rs_recurrence=True, **prior)
+    worst = max(maxrel(xh[it].ravel() / np.sqrt(sum(N)), np.asarray(t["xhat"][it]))
+                for it in range(its))
+    final = maxrel(xh[-1].ravel() / np.sqrt(sum(N)), np.asarray(t["xhat"][-1]))
+    print("K=%d: worst maxrel over 50 iterations %.3e, final %.3e" % (K, worst, final))
+    assert worst < tol, worst
+    assert final < tol, final
+    eng.close()
