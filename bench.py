@@ -189,7 +189,7 @@ def main():
     recs = []
     for it in range(args.warmup, args.warmup + args.steps):
         recs.append(v.step(it))
-    v.flush()                                           # output files of the timed steps
+    v.drain()                                           # output files and CSV rows of the timed steps
     eng.sync()
     t1 = time.perf_counter()
     comm.barrier()

@@ -354,12 +354,16 @@ class VAMP:
         self._csv_futs = [f for f in self._csv_futs if not f.done() or f.result() is not None]
         self._csv_futs.append(self._csv_pool.submit(lambda: [fn(*a) for fn, a in rows]))
 
-    def finish(self):
+    def drain(self):
+        """Wait for every output of the finished iterations: .bin files and CSV rows."""
         self._submit_csv()
         self.flush()
         for f in getattr(self, "_csv_futs", []):
             f.result()                    # re-raise a failed append
         self._csv_futs = []
+
+    def finish(self):
+        self.drain()
         for pool in ("_probe_pool", "_write_pool", "_out_pool", "_csv_pool"):
             if getattr(self, pool, None) is not None:
                 getattr(self, pool).shutdown(wait=True)
