@@ -133,3 +133,68 @@ def test_cli_plink_ld_equals_npz(tmp_path):
         a = np.fromfile(out_a / ("a_xhat_it_%d.bin" % it))
         b = np.fromfile(out_b / ("a_xhat_it_%d.bin" % it))
         np.testing.assert_array_equal(a, b)
+
+
+def test_cli_two_ranks_bitwise_equal_one_rank(tmp_path):
+    """main.py under torchrun-style env with 2 ranks (LD blocks sharded; both ranks
+    on device 0 with the host exchange, since RCCL refuses two ranks per device):
+    every output .bin file is bitwise the single-process one (ordered per-block
+    reductions), and the per-cohort CSV is identical."""
+    import socket
+    import subprocess
+    import sys
+
+    import scipy.sparse
+
+    import main
+
+    rs = np.random.RandomState(11)
+    M, nsamp = 360, 800
+    X = rs.normal(size=(nsamp, M))
+    for b in range(0, M, 90):                       # 4 LD blocks of 90
+        X[:, b + 1:b + 90] += 0.6 * X[:, b:b + 1]
+    X = (X - X.mean(0)) / X.std(0) / np.sqrt(nsamp)
+    C = X.T @ X
+    mask = np.zeros((M, M), dtype=bool)
+    for b in range(0, M, 90):
+        mask[b:b + 90, b:b + 90] = True
+    scipy.sparse.save_npz(tmp_path / "R.npz", scipy.sparse.csr_matrix(np.where(mask, C, 0.0)))
+    beta = np.zeros(M)
+    beta[rs.choice(M, 36, replace=False)] = rs.normal(0, np.sqrt(0.8 / 36), 36)
+    y = X @ beta * np.sqrt(nsamp) + rs.normal(0, np.sqrt(0.2), nsamp)
+    np.save(tmp_path / "r.npy", X.T @ y)
+    np.save(tmp_path / "beta.npy", beta)
+
+    def argv(out):
+        return ["--ld-files", str(tmp_path / "R.npz"), "--r-files", str(tmp_path / "r.npy"),
+                "--true-signal-file", str(tmp_path / "beta.npy"), "--out-dir", str(out),
+                "--out-name", "t", "--N", str(nsamp), "--M", str(M), "--K", "1",
+                "--iterations", "6", "--prior-vars", "0,%r" % (0.8 / 36),
+                "--prior-probs", "0.9,0.1", "--seed", "4", "--s", "0.02"]
+
+    one = tmp_path / "one"
+    one.mkdir()
+    main.main(argv(one))
+    two = tmp_path / "two"
+    two.mkdir()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path.insert(0, %r); import main; main.main(sys.argv[1:])"
+            % os.path.join(root, "sgvamp-py_amd"))
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SGV_EXCHANGE="host")
+        procs.append(subprocess.Popen([sys.executable, "-c", code] + argv(two), env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    for p in procs:
+        out, _ = p.communicate(timeout=240)
+        assert p.returncode == 0, out[-3000:]
+    bins = sorted(f for f in os.listdir(one) if f.endswith(".bin"))
+    assert len(bins) == 12 and bins == sorted(f for f in os.listdir(two) if f.endswith(".bin"))
+    for f in bins:
+        assert (one / f).read_bytes() == (two / f).read_bytes(), f
+    assert (one / "t_cohort_1.csv").read_text() == (two / "t_cohort_1.csv").read_text()
