@@ -47,6 +47,12 @@ struct LdPlan {
   int nitems[4] = {0, 0, 0, 0};
   SymPanel* d_panels[4] = {nullptr, nullptr, nullptr, nullptr};
   int npanels = 0;
+  // MFMA pass: strips (dispatch order), their class-1 items in strip order, and
+  // the class-1 panels with their strip ranges
+  SymStrip* d_strips = nullptr;
+  SymItem* d_sitems = nullptr;
+  SymPanel* d_spanels = nullptr;
+  int nstrips = 0;
   double stored_bytes = 0.0, dense_bytes = 0.0;
 };
 
@@ -366,6 +372,9 @@ static void free_plan(LdPlan& p) {
     if (p.d_items[k]) (void)hipFree(p.d_items[k]);
     if (p.d_panels[k]) (void)hipFree(p.d_panels[k]);
   }
+  if (p.d_strips) (void)hipFree(p.d_strips);
+  if (p.d_sitems) (void)hipFree(p.d_sitems);
+  if (p.d_spanels) (void)hipFree(p.d_spanels);
   p = LdPlan();
 }
 
@@ -437,6 +446,71 @@ static int grow(sgv_ctx* c, double** buf, size_t* cap, size_t need) {
   return SGV_OK;
 }
 
+// panels per MFMA strip (env SGV_MFMA_STRIP, read when a plan is built; 1 =
+// one (panel, chunk) item per workgroup)
+static int mfma_strip_len() {
+  const char* e = std::getenv("SGV_MFMA_STRIP");
+  const int v = e ? std::atoi(e) : 8;
+  return std::max(1, std::min(64, v));
+}
+
+// MFMA strips of one LD matrix from the class-1 (512-column) tables.  Chunk
+// (parity p, c0 = 256 p + 512 k) of a block holds the items (g, c0) of panels
+// g = p, p + 2, ..., G = c0 / 256 (the diagonal panel); they are cut into strips
+// of up to S panels in increasing order, colpart slots numbered per chunk.
+// The chunk's strips hold the column sums of panel G's rows (offset 0, "own")
+// and of panel G + 1's rows (offset 256, "other").  Dispatch order: most panels
+// first (the short strips fill the tail).
+static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
+                        const std::vector<SymPanel>& panels, LdPlan* pl) {
+  const int S = mfma_strip_len();
+  std::vector<SymItem> sitems;
+  std::vector<SymStrip> strips;
+  std::vector<SymPanel> sp = panels;
+  int bp0 = 0;
+  for (int b = 0; b < c->nblk; ++b) {
+    if (c->ldb[ld][b].fmt != 1) continue;
+    const int64_t n = c->bn[b];
+    const int np = (int)c->ldb[ld][b].poff.size();
+    for (int p = 0; p < 2; ++p)
+      for (int64_t c0 = (int64_t)SYM_H * p; c0 < n; c0 += 2 * SYM_H) {
+        const int G = (int)(c0 / SYM_H);
+        const int sb = (int)strips.size();
+        for (int g0 = p; g0 <= G; g0 += 2 * S) {
+          SymStrip st;
+          st.it0 = (int)sitems.size();
+          st.npan = 0;
+          st.slot = (int)strips.size();
+          st.pad_ = 0;
+          for (int g = g0; g <= G && g < g0 + 2 * S; g += 2) {
+            const SymPanel& pn = panels[bp0 + g];
+            const int idx = pn.item_begin + (int)((c0 - (int64_t)SYM_H * g) / (2 * SYM_H));
+            if (idx >= pn.item_end || items[idx].c0 != c0)
+              return fail(c, SGV_ERR_STATE, "strip plan: item (%d, %lld) missing", g,
+                          (long long)c0);
+            sitems.push_back(items[idx]);
+            ++st.npan;
+          }
+          strips.push_back(st);
+        }
+        sp[bp0 + G].own_sb = sb;
+        sp[bp0 + G].own_se = (int)strips.size();
+        if (G + 1 < np) {
+          sp[bp0 + G + 1].oth_sb = sb;
+          sp[bp0 + G + 1].oth_se = (int)strips.size();
+        }
+      }
+    bp0 += np;
+  }
+  std::stable_sort(strips.begin(), strips.end(),
+                   [](const SymStrip& a, const SymStrip& b) { return a.npan > b.npan; });
+  pl->nstrips = (int)strips.size();
+  CHK(upload_table(c, strips, &pl->d_strips));
+  CHK(upload_table(c, sitems, &pl->d_sitems));
+  CHK(upload_table(c, sp, &pl->d_spanels));
+  return SGV_OK;
+}
+
 // launch tables of LD matrix ld: dense row groups, packed (panel, chunk) items
 // per chunk-width class, panels; unified partial slots in block order
 static int ensure_plan(sgv_ctx* c, int ld) {
@@ -501,6 +575,7 @@ static int ensure_plan(sgv_ctx* c, int ld) {
         pn.blk_panel0 = blk_panel0;
         pn.part = pbeg[b] + (int)g;
         pn.pad_ = 0;
+        pn.own_sb = pn.own_se = pn.oth_sb = pn.oth_se = 0;
         panels.push_back(pn);
       }
     }
@@ -508,13 +583,14 @@ static int ensure_plan(sgv_ctx* c, int ld) {
     pl.npanels = (int)panels.size();
     CHK(upload_table(c, items, &pl.d_items[cls]));
     CHK(upload_table(c, panels, &pl.d_panels[cls]));
+    if (cls == 1) CHK(build_strips(c, ld, items, panels, &pl));
     const size_t ncmax = (size_t)sym_class_nc(cls);
     rowpart_need = std::max(rowpart_need, items.size() * SYM_H * ncmax);
     colpart_need = std::max(colpart_need, items.size() * ncmax * (size_t)cw);
   }
   if (pl.npanels) {   // the MFMA pass: class-1 items with up to 16 columns
     rowpart_need = std::max(rowpart_need, (size_t)pl.nitems[1] * SYM_H * MAXC);
-    colpart_need = std::max(colpart_need, (size_t)pl.nitems[1] * MAXC * 512);
+    colpart_need = std::max(colpart_need, (size_t)pl.nstrips * MAXC * 512);
     CHK(grow(c, &c->d_pk, &c->pk_cap, (size_t)c->Mpad * 16));
   }
   CHK(grow(c, &c->d_rowpart, &c->rowpart_cap, rowpart_need));
@@ -545,17 +621,21 @@ static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa) {
   if (pl.npanels) {
     const bool mf = c->mfma_min > 0 && nc >= c->mfma_min;
     const int cls = mf ? 1 : sym_class(nc);
-    if (mf)
-      HIPCHK(launch_sym_mfma(nc, pl.d_items[cls], pl.nitems[cls], pa, c->Mpad, c->d_pk,
+    if (mf) {
+      HIPCHK(launch_sym_mfma(nc, pl.d_strips, pl.nstrips, pl.d_sitems, pa, c->Mpad, c->d_pk,
                              c->d_rowpart, c->d_colpart, c->st));
-    else
+      HIPCHK(launch_sym_finalize_strip(nc, pl.d_spanels, pl.npanels, pa, c->d_rowpart,
+                                       c->d_colpart, c->d_part, c->st));
+      c->aux_bytes += 2.0 * 8.0 * nc * ((double)pl.nitems[cls] * SYM_H + (double)pl.nstrips * 512);
+      c->aux_bytes += 8.0 * (double)c->Mpad * (16 + nc);   // Pk pack
+    } else {
       HIPCHK(launch_sym_pass(nc, cls, pl.d_items[cls], pl.nitems[cls], pa, c->d_rowpart,
                              c->d_colpart, c->st));
-    HIPCHK(launch_sym_finalize(nc, cls, pl.d_panels[cls], pl.npanels, pa, c->d_rowpart,
-                               c->d_colpart, c->d_part, c->st));
-    const double cw = (double)(1024 >> cls);
-    c->aux_bytes += 2.0 * 8.0 * nc * (double)pl.nitems[cls] * (SYM_H + cw);
-    if (mf) c->aux_bytes += 8.0 * (double)c->Mpad * (16 + nc);   // Pk pack
+      HIPCHK(launch_sym_finalize(nc, cls, pl.d_panels[cls], pl.npanels, pa, c->d_rowpart,
+                                 c->d_colpart, c->d_part, c->st));
+      const double cw = (double)(1024 >> cls);
+      c->aux_bytes += 2.0 * 8.0 * nc * (double)pl.nitems[cls] * (SYM_H + cw);
+    }
   }
   HIPCHK(hipEventRecord(e1, c->st));
   c->pending.emplace_back(e0, e1);

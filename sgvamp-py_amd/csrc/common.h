@@ -79,6 +79,18 @@ struct SymPanel {
   int32_t blk_panel0;            // index (in the panel table) of the block's first panel
   int32_t part;                  // partial slot
   int32_t pad_;
+  // MFMA strips (k_sym_finalize_strip): the column sums of this panel's rows
+  // sit in the strips of two 512-column chunks -- the chunk starting at r0 (the
+  // panels of this panel's parity, row offset 0) and the one starting at
+  // r0 - 256 (the other parity, row offset 256); colpart slots [sb, se)
+  int32_t own_sb, own_se, oth_sb, oth_se;
+};
+// MFMA pass work item: one 512-column chunk (block-relative c0, shared by all
+// its panels) over npan panels of one parity, g0, g0 + 2, ... (increasing);
+// their (panel, chunk) items are sitems[it0 .. it0 + npan), column sums go to
+// colpart slot `slot`
+struct SymStrip {
+  int32_t it0, npan, slot, pad_;
 };
 
 // element (i, j) of a packed block is stored iff j >= 256 * floor(i / 256)
@@ -182,9 +194,12 @@ int ld_pass_rows_per_group();
 // chunk-width class cls: CW = 1024 >> cls columns per work item
 hipError_t launch_sym_pass(int nc, int cls, const SymItem* d_items, int nitems,
                            const PassArgs& pa, double* rowpart, double* colpart, hipStream_t st);
-hipError_t launch_sym_mfma(int nc, const SymItem* d_items, int nitems, const PassArgs& pa,
-                           int64_t mpad, double* d_pk, double* rowpart, double* colpart,
-                           hipStream_t st);
+hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
+                           const PassArgs& pa, int64_t mpad, double* d_pk, double* rowpart,
+                           double* colpart, hipStream_t st);
+hipError_t launch_sym_finalize_strip(int nc, const SymPanel* d_panels, int npanels,
+                                     const PassArgs& pa, const double* rowpart,
+                                     const double* colpart, double* partials, hipStream_t st);
 hipError_t launch_sym_finalize(int nc, int cls, const SymPanel* d_panels, int npanels,
                                const PassArgs& pa, const double* rowpart, const double* colpart,
                                double* partials, hipStream_t st);

@@ -16,11 +16,13 @@
 //   A_b[m][k] at lane 16k + 4b + m,  B_b[k][n] at lane 16k + 4b + n,
 //   D_b[m][n] at lane 16m + 4b + n.
 //
-// Same items (panel x 512-column chunk), partial layout and finalize as the
-// VALU pass (class 1): rowpart[item][256][NC], colpart[item][NC][512].
+// Work items are strips (see k_sym_mfma): one 512-column chunk over several
+// panels.  Row sums go to rowpart[item][256][NC] per (panel, chunk) item as in
+// the VALU pass (class 1), column sums to colpart[strip][NC][512];
+// k_sym_finalize_strip combines them.
 //
-// One workgroup per item, NW waves; wave w owns chunk columns
-// [w*512/NW, (w+1)*512/NW) and sweeps the panel's rows in 16-row groups.
+// One workgroup per strip, NW waves; wave w owns chunk columns
+// [w*512/NW, (w+1)*512/NW) and sweeps each panel's rows in 16-row groups.
 // Each 16 x 32 sub-tile is loaded from HBM once, 16 B per lane:
 //   col fragment  lane l: R[row 4a + (l>>4)][col pair (l&15), + e]   (a = 0..3)
 //       A_b[m][k] = R[row k][pair 4b+m]: Dcol[pair][c] += R[j][i] P[j][c]
@@ -30,7 +32,7 @@
 // is read back without bank conflicts.  Each 4x4x4 block contracts its own 4
 // column pairs, so the 4 blocks' row partials are summed by two xor-shuffles
 // per row group (fixed order), then over the waves through LDS (wave order).
-// Dcol accumulates over all 256 rows in registers; every order is fixed.
+// Dcol accumulates over all rows of the strip in registers; every order is fixed.
 #include "common.h"
 
 namespace sgv {
@@ -50,32 +52,37 @@ __device__ __forceinline__ void lds_order() {
 constexpr int MF_CW = 512;   // chunk width (class 1 items)
 constexpr int MF_LDP = 34;   // staging row pitch (doubles): conflict-free both ways
 
-// NS column splits: the waves form NS sets; set s handles column groups
-// [s*NG, (s+1)*NG) over the whole chunk (NS*NG groups of 4 columns, NG groups of
-// registers per wave).  NS = 2 was measured slower than one 16x16x4 group (the
-// repeat R reads of the second set go back to HBM); the launcher uses NS = 1.
-template <int NG, int NW, int NS, int PD>
-__global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restrict__ items,
+// Strips: a workgroup owns one 512-column chunk over up to S panels of one
+// parity (g0, g0 + 2, ...: the panels whose items share that chunk's column
+// alignment), so the column sums stay in registers across the panels and reach
+// HBM once per strip instead of once per (panel, chunk) item.  The chunk's
+// diagonal panel (r0 == c0) is the strip's last; its diagonal block (chunk
+// columns 0..255, waves 0 and 1) must not feed the column sums, so those waves
+// take zero B operands there (exact: R * 0 adds 0).  Row sums are still written
+// per (panel, chunk) item.  Panel descriptors are wave-uniform (SGPRs); the
+// prefetch of the next row group crosses panel boundaries through selects.
+template <int NG, int NW, int PD>
+__global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
+                                                         const SymItem* __restrict__ sitems,
                                                          const double* __restrict__ pk, int ncol,
                                                          double* __restrict__ rowpart,
                                                          double* __restrict__ colpart) {
-  constexpr int NWS = NW / NS;     // waves per column split
-  constexpr int WC = MF_CW / NWS;  // columns per wave
+  static_assert(NW == 4, "waves 0 and 1 own the diagonal half of a chunk");
+  constexpr int WC = MF_CW / NW;   // columns per wave (128)
   constexpr int NT = WC / 32;      // 32-column steps per wave
-  static_assert(NT >= 1, "at least one step per wave");
-  static_assert(PD >= 1 && NT % PD == 0, "prefetch depth divides the steps per row group");
+  static_assert(PD >= 1 && PD <= NT && NT % PD == 0, "prefetch depth divides the steps");
   __shared__ double red[2][NW][256];
   __shared__ __attribute__((aligned(16))) double stg[NW][16 * MF_LDP];
-  const SymItem it = items[blockIdx.x];
+  const SymStrip sp = strips[blockIdx.x];
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lo = lane & 15, hi = lane >> 4, bq = (lane >> 2) & 3, n4 = lane & 3;
   const int pc = hi + 4 * bq;                          // this lane's column pair in a fragment
-  const double* base = it.P + (it.c0 - it.r0);        // panel row 0, chunk column 0
-  const int64_t w = it.w;
-  const double* pkb = pk + (int64_t)it.voff * 16;     // Pk of this block (block-relative index)
-  const int cw0 = (wid % NWS) * WC;                    // first chunk column of this wave
-  const int cq0 = 4 * NG * (wid / NWS);                // first RHS column of this wave's groups
+  SymItem cur = sitems[sp.it0];
+  const int c0 = cur.c0, ncc = cur.nc;                 // the strip's chunk
+  const double* pkb = pk + (int64_t)cur.voff * 16;    // Pk of this block (block-relative index)
+  const int cw0 = wid * WC;                            // first chunk column of this wave
+  const bool dhalf = cw0 < SYM_H;                      // wave inside a diagonal panel's diag block
   double* sb = stg[wid];
 
   // row-part B operands: P at this wave's columns, reused by every row group
@@ -87,9 +94,8 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restri
       const int col = cw0 + 32 * t + 2 * pc + e;
 #pragma unroll
       for (int q = 0; q < NG; ++q) {
-        const double v = ldg(pkb + (int64_t)(it.c0 + (col < it.nc ? col : 0)) * 16 + cq0 + 4 * q +
-                             n4);
-        brow[t][e][q] = col < it.nc ? v : 0.0;
+        const double v = ldg(pkb + (int64_t)(c0 + (col < ncc ? col : 0)) * 16 + 4 * q + n4);
+        brow[t][e][q] = col < ncc ? v : 0.0;
       }
     }
   double dcol[NT][2][NG];
@@ -100,129 +106,147 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restri
 #pragma unroll
       for (int q = 0; q < NG; ++q) dcol[t][e][q] = 0.0;
 
-  // fragment loads of step (g, t), 16 B per lane, branch-free: a row past H
-  // clamps (its P is 0), a column past the chunk loads column 0 (finite; it
-  // meets a zero B in the row part and is never stored by the column part)
-  // ok = false (the prefetch past the panel's last row group) reads the
-  // cache-resident Pk instead: the prefetch stays unconditional, so the load
-  // count is the same on every path and the compiler never drains vmcnt(0)
-  // at a branch join or the row-group loop head
-  auto load_cf = [&](int g, int t, d2* cf, bool ok = true) {
-    const int xc = cw0 + 32 * t + 2 * lo;
-    // the base is chosen as an opaque integer: a pointer select here is turned
-    // back into a branch with one load per side
-    uint64_t b0 = ok ? (uint64_t)base : (uint64_t)pkb;
+  // fragment loads of step (g, t) of a panel (b0 = its element (r0, c0)), 16 B
+  // per lane, branch-free: a row past H clamps (its P is 0), a column past the
+  // chunk loads column 0 (finite; it meets a zero B in the row part and is never
+  // read from the column part).  The base is an opaque integer: a pointer select
+  // is turned back into a branch with one load per side.  Past the strip's last
+  // row group the caller passes the cache-resident Pk with stride 0 (a dummy
+  // fetch: the load count is the same on every path, so the compiler never
+  // drains vmcnt(0) at a branch join or the row-group loop head).
+  auto load_cf = [&](uint64_t b0, int64_t ws, int H, int g, int t, d2* cf) {
     asm volatile("" : "+s"(b0));
-    const int64_t ws = ok ? w : 0;
+    const int xc = cw0 + 32 * t + 2 * lo;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int rB = 16 * g + 4 * a + hi;
-      const double* row = (const double*)b0 + (int64_t)(rB < it.H ? rB : it.H - 1) * ws;
-      cf[a] = ldg_nt((const d2*)(row + (xc < it.nc ? xc : 0)));
+      const double* row = (const double*)b0 + (int64_t)(rB < H ? rB : H - 1) * ws;
+      cf[a] = ldg_nt((const d2*)(row + (xc < ncc ? xc : 0)));
     }
   };
-  auto load_bcol = [&](int g, double (*bc)[NG]) {
+  // column-part B operands of row group g of a panel (first row r0): P at its
+  // rows; zero past H and, for the diagonal panel, in the diagonal-block waves
+  auto load_bcol = [&](int r0, int H, bool zero, int g, double (*bc)[NG]) {
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int rB = 16 * g + 4 * a + hi;
 #pragma unroll
       for (int q = 0; q < NG; ++q) {
-        const double v = ldg(pkb + (int64_t)(it.r0 + (rB < it.H ? rB : 0)) * 16 + cq0 + 4 * q +
-                             n4);
-        bc[a][q] = rB < it.H ? v : 0.0;
+        const double v = ldg(pkb + (int64_t)(r0 + (rB < H ? rB : 0)) * 16 + 4 * q + n4);
+        bc[a][q] = (rB < H && !zero) ? v : 0.0;
       }
     }
   };
-  const int ng = (it.H + 15) / 16;
+  auto pbase = [&](const SymItem& x) { return (uint64_t)(x.P + (x.c0 - x.r0)); };
+
+  uint64_t curb = pbase(cur);
   // ring of PD steps in flight per wave
   d2 cfq[PD][4];
   double bcn[4][NG];
 #pragma unroll
-  for (int p = 0; p < PD; ++p) load_cf(0, p, cfq[p]);
-  load_bcol(0, bcn);
+  for (int p = 0; p < PD; ++p) load_cf(curb, cur.w, cur.H, 0, p, cfq[p]);
+  load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
 
+  int gg = 0;                                          // row groups done (LDS buffer parity)
 #pragma unroll 1
-  for (int g = 0; g < ng; ++g) {                      // ng is uniform over the workgroup
-    double bcol[4][NG];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int q = 0; q < NG; ++q) bcol[a][q] = bcn[a][q];
-    double drow[4][NG];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int q = 0; q < NG; ++q) drow[r][q] = 0.0;
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      d2 cf[4], rf[4];
-      const int slot = t % PD;                         // compile-time after unrolling
-#pragma unroll
-      for (int a = 0; a < 4; ++a) cf[a] = cfq[slot][a];
-      // step (g, t) + PD goes out here, ahead of this step's LDS and MFMA work
-      if (t + PD < NT) {
-        load_cf(g, t + PD, cfq[slot]);
-      } else {   // next row group; past the last one a dummy (cached) fetch
-        load_cf(g + 1, t + PD - NT, cfq[slot], g + 1 < ng);
-        if (t + PD == NT) load_bcol(g + 1, bcn);     // rows past H clamp (cached Pk)
-      }
-      lds_order();                                     // previous step's tile reads issued
-#pragma unroll
-      for (int a = 0; a < 4; ++a) *(d2*)(sb + (4 * a + hi) * MF_LDP + 2 * lo) = cf[a];
-      lds_order();                                     // tile written
-      // the row fragment reads go out right behind the writes (a wave's DS
-      // operations execute in order); the column MFMAs cover their latency
-#pragma unroll
-      for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + (4 * r + n4) * MF_LDP + 2 * pc);
+  for (int s = 0; s < sp.npan; ++s) {                  // uniform over the workgroup
+    const bool more = s + 1 < sp.npan;
+    const SymItem nx = sitems[sp.it0 + (more ? s + 1 : s)];
+    const uint64_t nxb = more ? pbase(nx) : (uint64_t)pkb;
+    const int ng = (cur.H + 15) / 16;
+#pragma unroll 1
+    for (int g = 0; g < ng; ++g, ++gg) {
+      // the next row group: this panel's g + 1, or the next panel's first
+      const bool same = g + 1 < ng;
+      const uint64_t gb = same ? curb : nxb;
+      const int64_t gw = same ? cur.w : (more ? nx.w : 0);
+      const int gH = same ? cur.H : (more ? nx.H : 1);
+      const int gn = same ? g + 1 : 0;
+      const int gr0 = same ? cur.r0 : nx.r0;
+      const bool gz = dhalf && gr0 == c0;
+      double bcol[4][NG];
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int q = 0; q < NG; ++q) {
-          dcol[t][0][q] = MFMA4(cf[a].x, bcol[a][q], dcol[t][0][q]);
-          dcol[t][1][q] = MFMA4(cf[a].y, bcol[a][q], dcol[t][1][q]);
+        for (int q = 0; q < NG; ++q) bcol[a][q] = bcn[a][q];
+      double drow[4][NG];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < NG; ++q) drow[r][q] = 0.0;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        d2 cf[4], rf[4];
+        const int slot = t % PD;                       // compile-time after unrolling
+#pragma unroll
+        for (int a = 0; a < 4; ++a) cf[a] = cfq[slot][a];
+        // step + PD goes out here, ahead of this step's LDS and MFMA work
+        if (t + PD < NT) {
+          load_cf(curb, cur.w, cur.H, g, t + PD, cfq[slot]);
+        } else {
+          load_cf(gb, gw, gH, gn, t + PD - NT, cfq[slot]);
+          if (t + PD == NT) load_bcol(gr0, gH, gz, gn, bcn);
         }
-      // x halves of all 4*NG chains, then the y halves: a chain's two MFMAs are
-      // 4*NG issues apart instead of back to back (same per-chain order)
+        lds_order();                                   // previous step's tile reads issued
+#pragma unroll
+        for (int a = 0; a < 4; ++a) *(d2*)(sb + (4 * a + hi) * MF_LDP + 2 * lo) = cf[a];
+        lds_order();                                   // tile written
+        // the row fragment reads go out right behind the writes (a wave's DS
+        // operations execute in order); the column MFMAs cover their latency
+#pragma unroll
+        for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + (4 * r + n4) * MF_LDP + 2 * pc);
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int q = 0; q < NG; ++q) {
+            dcol[t][0][q] = MFMA4(cf[a].x, bcol[a][q], dcol[t][0][q]);
+            dcol[t][1][q] = MFMA4(cf[a].y, bcol[a][q], dcol[t][1][q]);
+          }
+        // x halves of all 4*NG chains, then the y halves: a chain's two MFMAs are
+        // 4*NG issues apart instead of back to back (same per-chain order)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(rf[r].x, brow[t][0][q], drow[r][q]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(rf[r].y, brow[t][1][q], drow[r][q]);
+      }
+      // row sums: the 4 blocks (lanes differing in bits 2,3), then the waves in order
+      double* rb = red[gg & 1][wid];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(rf[r].x, brow[t][0][q], drow[r][q]);
+        for (int q = 0; q < NG; ++q) {
+          double v = drow[r][q];
+          v = v + __shfl_xor(v, 4);
+          v = v + __shfl_xor(v, 8);
+          if (bq == 0) rb[((4 * r + hi) << 4) + 4 * q + n4] = v;   // D row 4r + m (m = hi)
+        }
+      __syncthreads();
+      if (threadIdx.x < 256) {
+        const int t = threadIdx.x, row = t >> 4, cc = t & 15;
+        if (16 * g + row < cur.H && cc < ncol) {
+          double v = red[gg & 1][0][t];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(rf[r].y, brow[t][1][q], drow[r][q]);
-    }
-    // row sums: the 4 blocks (lanes differing in bits 2,3), then the waves in order
-    double* rb = red[g & 1][wid];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int q = 0; q < NG; ++q) {
-        double v = drow[r][q];
-        v = v + __shfl_xor(v, 4);
-        v = v + __shfl_xor(v, 8);
-        if (bq == 0) rb[((4 * r + hi) << 4) + cq0 + 4 * q + n4] = v;   // D row 4r + m (m = hi)
-      }
-    __syncthreads();
-    if (threadIdx.x < 256) {
-      const int t = threadIdx.x, row = t >> 4, cc = t & 15;
-      if (16 * g + row < it.H && cc < ncol) {
-        const int w0 = (cc / (4 * NG)) * NWS;          // the waves of cc's column split
-        double s = red[g & 1][w0][t];
-#pragma unroll
-        for (int v = 1; v < NWS; ++v) s += red[g & 1][w0 + v][t];
-        rowpart[((int64_t)it.item * SYM_H + 16 * g + row) * ncol + cc] = s;
+          for (int w = 1; w < NW; ++w) v += red[gg & 1][w][t];
+          rowpart[((int64_t)cur.item * SYM_H + 16 * g + row) * ncol + cc] = v;
+        }
       }
     }
+    cur = nx;
+    curb = nxb;
   }
 
-  // column sums (complete over the panel's rows), right of the diagonal block only:
-  // D_b[m][n] at lane 16m + 4b + n holds column pair 4b + m = pc, column c = 4q + n
+  // column sums over the strip's panels: D_b[m][n] at lane 16m + 4b + n holds
+  // column pair 4b + m = pc, column c = 4q + n.  Whole slot, 16-B stores
+  // (columns the finalize never reads: don't care).
 #pragma unroll
   for (int q = 0; q < NG; ++q) {
-    const int cc = cq0 + 4 * q + n4;
-    if (cc < ncol) {   // whole slot, 16-B stores (columns the finalize skips: don't care)
-      double* out = colpart + ((int64_t)it.item * ncol + cc) * MF_CW;
+    const int cc = 4 * q + n4;
+    if (cc < ncol) {
+      double* out = colpart + ((int64_t)sp.slot * ncol + cc) * MF_CW;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
         *(d2*)(out + cw0 + 32 * t + 2 * pc) = d2{dcol[t][0][q], dcol[t][1][q]};
@@ -232,7 +256,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymItem* __restri
 
 // 13..16 right-hand sides: v_mfma_f64_16x16x4f64 (one 16-column group, 140
 // cycles per 16x16x4) keeps fewer accumulators and B operands in registers
-// than four 4x4x4 groups, which spill at 4 waves.  Same structure as above:
+// than four 4x4x4 groups, which spill at 4 waves.  Same strips as above:
 //   col fragment -> A (m = column, k = row); LDS tile -> row fragment
 //   lane l: R[row (l&15)][col 8s + 2(l>>4) + e] -> A (m = row, k = column);
 //   16x16x4 f64 C/D layout (cdna_hip_programming.md): D[(l>>4) + 4r][l & 15].
@@ -241,21 +265,23 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int MF_WC = MF_CW / 4;
 constexpr int MF_NT = MF_WC / 32;
 
-__global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymItem* __restrict__ items,
+__global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restrict__ strips,
+                                                     const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
                                                      double* __restrict__ rowpart,
                                                      double* __restrict__ colpart) {
   constexpr int LDP = MF_LDP;
   __shared__ double red[2][4][256];
   __shared__ __attribute__((aligned(16))) double stg[4][16 * LDP];
-  const SymItem it = items[blockIdx.x];
+  const SymStrip sp = strips[blockIdx.x];
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lo = lane & 15, hi = lane >> 4;
-  const double* base = it.P + (it.c0 - it.r0);        // panel row 0, chunk column 0
-  const int64_t w = it.w;
-  const double* pkb = pk + (int64_t)it.voff * 16;     // Pk of this block (block-relative index)
+  SymItem cur = sitems[sp.it0];
+  const int c0 = cur.c0, ncc = cur.nc;
+  const double* pkb = pk + (int64_t)cur.voff * 16;    // Pk of this block (block-relative index)
   const int cw0 = wid * MF_WC;                         // first chunk column of this wave
+  const bool dhalf = cw0 < SYM_H;
 
   double* sb = stg[wid];
   // row-part B operands (P at this wave's columns), reused by every row group
@@ -267,100 +293,161 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymItem* __restrict
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int col = cw0 + 32 * t + 8 * s + 2 * hi + e;
-        const double v = ldg(pkb + (int64_t)(it.c0 + (col < it.nc ? col : 0)) * 16 + lo);
-        brow[t][s][e] = col < it.nc ? v : 0.0;
+        const double v = ldg(pkb + (int64_t)(c0 + (col < ncc ? col : 0)) * 16 + lo);
+        brow[t][s][e] = col < ncc ? v : 0.0;
       }
   d4 dcol[MF_NT][2];
 #pragma unroll
   for (int t = 0; t < MF_NT; ++t) dcol[t][0] = dcol[t][1] = d4{0.0, 0.0, 0.0, 0.0};
 
-  // fragment loads of step (g, t), 16 B per lane; rows past H clamp (their P is 0);
-  // ok = false: dummy fetch from the cached Pk (unconditional prefetch, as above)
-  auto load_cf = [&](int g, int t, d2* cf, bool ok = true) {
-    const int xc = cw0 + 32 * t + 2 * lo;
-    uint64_t b0 = ok ? (uint64_t)base : (uint64_t)pkb;
+  auto load_cf = [&](uint64_t b0, int64_t ws, int H, int g, int t, d2* cf) {
     asm volatile("" : "+s"(b0));
-    const int64_t ws = ok ? w : 0;
+    const int xc = cw0 + 32 * t + 2 * lo;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int rB = 16 * g + 4 * a + hi;
-      const double* row = (const double*)b0 + (int64_t)(rB < it.H ? rB : it.H - 1) * ws;
-      // branch-free: a column past the chunk loads column 0 (finite), meets a
-      // zero B in the row part and is never stored by the column part
-      cf[a] = ldg_nt((const d2*)(row + (xc < it.nc ? xc : 0)));
+      const double* row = (const double*)b0 + (int64_t)(rB < H ? rB : H - 1) * ws;
+      cf[a] = ldg_nt((const d2*)(row + (xc < ncc ? xc : 0)));
     }
   };
-  auto load_bcol = [&](int g, double* bc) {
+  auto load_bcol = [&](int r0, int H, bool zero, int g, double* bc) {
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int rB = 16 * g + 4 * a + hi;
-      const double v = ldg(pkb + (int64_t)(it.r0 + (rB < it.H ? rB : 0)) * 16 + lo);
-      bc[a] = rB < it.H ? v : 0.0;
+      const double v = ldg(pkb + (int64_t)(r0 + (rB < H ? rB : 0)) * 16 + lo);
+      bc[a] = (rB < H && !zero) ? v : 0.0;
     }
   };
-  const int ng = (it.H + 15) / 16;
+  auto pbase = [&](const SymItem& x) { return (uint64_t)(x.P + (x.c0 - x.r0)); };
+
+  uint64_t curb = pbase(cur);
   d2 cfn[4];
   double bcn[4];
-  load_cf(0, 0, cfn);
-  load_bcol(0, bcn);
+  load_cf(curb, cur.w, cur.H, 0, 0, cfn);
+  load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
 
+  int gg = 0;
 #pragma unroll 1
-  for (int g = 0; g < ng; ++g) {                      // ng is uniform over the workgroup
-    double bcol[4];
+  for (int s = 0; s < sp.npan; ++s) {
+    const bool more = s + 1 < sp.npan;
+    const SymItem nx = sitems[sp.it0 + (more ? s + 1 : s)];
+    const uint64_t nxb = more ? pbase(nx) : (uint64_t)pkb;
+    const int ng = (cur.H + 15) / 16;
+#pragma unroll 1
+    for (int g = 0; g < ng; ++g, ++gg) {
+      const bool same = g + 1 < ng;
+      const uint64_t gb = same ? curb : nxb;
+      const int64_t gw = same ? cur.w : (more ? nx.w : 0);
+      const int gH = same ? cur.H : (more ? nx.H : 1);
+      const int gn = same ? g + 1 : 0;
+      const int gr0 = same ? cur.r0 : nx.r0;
+      const bool gz = dhalf && gr0 == c0;
+      double bcol[4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) bcol[a] = bcn[a];
-    d4 drow0 = d4{0.0, 0.0, 0.0, 0.0}, drow1 = drow0;
+      for (int a = 0; a < 4; ++a) bcol[a] = bcn[a];
+      d4 drow0 = d4{0.0, 0.0, 0.0, 0.0}, drow1 = drow0;
 #pragma unroll
-    for (int t = 0; t < MF_NT; ++t) {
-      d2 cf[4], rf[4];
+      for (int t = 0; t < MF_NT; ++t) {
+        d2 cf[4], rf[4];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) cf[a] = cfn[a];
-      // next step's loads are issued here, ahead of this step's LDS and MFMA work
-      if (t + 1 < MF_NT) {
-        load_cf(g, t + 1, cfn);
-      } else {   // next row group; past the last one a dummy (cached) fetch
-        load_cf(g + 1, 0, cfn, g + 1 < ng);
-        load_bcol(g + 1, bcn);                         // rows past H clamp (cached Pk)
+        for (int a = 0; a < 4; ++a) cf[a] = cfn[a];
+        // next step's loads are issued here, ahead of this step's LDS and MFMA work
+        if (t + 1 < MF_NT) {
+          load_cf(curb, cur.w, cur.H, g, t + 1, cfn);
+        } else {
+          load_cf(gb, gw, gH, gn, 0, cfn);
+          load_bcol(gr0, gH, gz, gn, bcn);
+        }
+        lds_order();                                   // previous step's tile reads done
+#pragma unroll
+        for (int a = 0; a < 4; ++a) *(d2*)(sb + (4 * a + hi) * LDP + 2 * lo) = cf[a];
+        lds_order();                                   // tile written
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) rf[s2] = *(const d2*)(sb + lo * LDP + 8 * s2 + 2 * hi);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          dcol[t][0] = MFMA16(cf[a].x, bcol[a], dcol[t][0]);
+          dcol[t][1] = MFMA16(cf[a].y, bcol[a], dcol[t][1]);
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          drow0 = MFMA16(rf[s2].x, brow[t][s2][0], drow0);
+          drow1 = MFMA16(rf[s2].y, brow[t][s2][1], drow1);
+        }
       }
-      lds_order();                                     // previous step's tile reads done
+      // row sums of this 16-row group: waves 0..3 in order
+      double* rb = red[gg & 1][wid];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) *(d2*)(sb + (4 * a + hi) * LDP + 2 * lo) = cf[a];
-      lds_order();                                     // tile written
-#pragma unroll
-      for (int s = 0; s < 4; ++s) rf[s] = *(const d2*)(sb + lo * LDP + 8 * s + 2 * hi);
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        dcol[t][0] = MFMA16(cf[a].x, bcol[a], dcol[t][0]);
-        dcol[t][1] = MFMA16(cf[a].y, bcol[a], dcol[t][1]);
-      }
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        drow0 = MFMA16(rf[s].x, brow[t][s][0], drow0);
-        drow1 = MFMA16(rf[s].y, brow[t][s][1], drow1);
+      for (int r = 0; r < 4; ++r) rb[((hi + 4 * r) << 4) + lo] = drow0[r] + drow1[r];
+      __syncthreads();
+      {
+        const int t = threadIdx.x, row = t >> 4, cc = t & 15;
+        const double v = ((red[gg & 1][0][t] + red[gg & 1][1][t]) + red[gg & 1][2][t]) +
+                         red[gg & 1][3][t];
+        if (16 * g + row < cur.H && cc < ncol)
+          rowpart[((int64_t)cur.item * SYM_H + 16 * g + row) * ncol + cc] = v;
       }
     }
-    // row sums of this 16-row group: waves 0..3 in order
-    double* rb = red[g & 1][wid];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) rb[((hi + 4 * r) << 4) + lo] = drow0[r] + drow1[r];
-    __syncthreads();
-    {
-      const int t = threadIdx.x, row = t >> 4, cc = t & 15;
-      const double s = ((red[g & 1][0][t] + red[g & 1][1][t]) + red[g & 1][2][t]) + red[g & 1][3][t];
-      if (16 * g + row < it.H && cc < ncol)
-        rowpart[((int64_t)it.item * SYM_H + 16 * g + row) * ncol + cc] = s;
-    }
+    cur = nx;
+    curb = nxb;
   }
 
-  // column sums (complete over the panel's rows), right of the diagonal block only
-  if (lo < ncol) {   // whole slot, 16-B stores (columns the finalize skips: don't care)
-    double* out = colpart + ((int64_t)it.item * ncol + lo) * MF_CW;
+  // column sums over the strip's panels (whole slot, 16-B stores)
+  if (lo < ncol) {
+    double* out = colpart + ((int64_t)sp.slot * ncol + lo) * MF_CW;
 #pragma unroll
     for (int t = 0; t < MF_NT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         *(d2*)(out + cw0 + 32 * t + 2 * (hi + 4 * r)) = d2{dcol[t][0][r], dcol[t][1][r]};
   }
+}
+
+// one workgroup per panel; thread t = panel row r0 + t: this panel's row parts
+// (chunk order), then the strips of the own-parity chunk (column offset t),
+// then those of the other-parity chunk (offset 256 + t) -- fixed order
+template <int NC>
+__global__ __launch_bounds__(256) void k_sym_finalize_strip(const SymPanel* __restrict__ panels,
+                                                            PassArgs pa,
+                                                            const double* __restrict__ rowpart,
+                                                            const double* __restrict__ colpart,
+                                                            double* __restrict__ partials) {
+  const SymPanel pn = panels[blockIdx.x];
+  const int t = threadIdx.x;
+  const int tr = t < pn.H ? t : 0;
+  double y[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) y[c] = 0.0;
+  for (int itm = pn.item_begin; itm < pn.item_end; ++itm) {
+    const double* rp = rowpart + ((int64_t)itm * SYM_H + t) * NC;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) y[c] += ldg(rp + c);
+  }
+  for (int sl = pn.own_sb; sl < pn.own_se; ++sl) {
+    const double* cp = colpart + (int64_t)sl * NC * MF_CW + tr;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) y[c] += ldg(cp + c * MF_CW);
+  }
+  for (int sl = pn.oth_sb; sl < pn.oth_se; ++sl) {
+    const double* cp = colpart + (int64_t)sl * NC * MF_CW + SYM_H + tr;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) y[c] += ldg(cp + c * MF_CW);
+  }
+  double acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = 0.0;
+  if (t < pn.H) {
+    const int64_t idx = pn.voff + pn.r0 + t;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const double in = pa.in[c][idx];
+      const double o = pa.c1[c] * y[c] + pa.c2[c] * in;
+      pa.out[c][idx] = o;
+      if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * y[c] + pa.ys0 * in;
+      if (pa.dot[c]) acc[c] = pa.dot[c][idx] * o;
+    }
+  }
+  block_reduce_store<NC>(acc, partials + (int64_t)pn.part * NC, NC);
 }
 
 // Pk[i][c] = in[c][i] for c < ncol, 0 for ncol <= c < 16 (i over the padded vector)
@@ -373,16 +460,17 @@ __global__ __launch_bounds__(256) void k_pack16(PassArgs pa, int ncol, int64_t m
   pk[t] = c < ncol ? pa.in[c][i] : 0.0;
 }
 
-template <int NG, int NW, int NS, int PD>
-static void launch_mf(const SymItem* d_items, int nitems, const double* d_pk, int nc,
-                      double* rowpart, double* colpart, hipStream_t st) {
-  hipLaunchKernelGGL((k_sym_mfma<NG, NW, NS, PD>), dim3(nitems), dim3(NW * 64), 0, st, d_items,
-                     d_pk, nc, rowpart, colpart);
+template <int NG, int NW, int PD>
+static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
+                      const double* d_pk, int nc, double* rowpart, double* colpart,
+                      hipStream_t st) {
+  hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD>), dim3(nstrips), dim3(NW * 64), 0, st, d_strips,
+                     d_sitems, d_pk, nc, rowpart, colpart);
 }
 
-hipError_t launch_sym_mfma(int nc, const SymItem* d_items, int nitems, const PassArgs& pa,
-                           int64_t mpad, double* d_pk, double* rowpart, double* colpart,
-                           hipStream_t st) {
+hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
+                           const PassArgs& pa, int64_t mpad, double* d_pk, double* rowpart,
+                           double* colpart, hipStream_t st) {
   if (nc < 1 || nc > 16) return hipErrorInvalidValue;
   const int64_t n16 = mpad * 16;
   hipLaunchKernelGGL(k_pack16, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, st, pa, nc,
@@ -392,13 +480,31 @@ hipError_t launch_sym_mfma(int nc, const SymItem* d_items, int nitems, const Pas
   // not come from cache): measured in DESIGN.md
   switch ((nc + 3) / 4) {
     // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
-    case 1: launch_mf<1, 4, 1, 2>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
-    case 2: launch_mf<2, 4, 1, 2>(d_items, nitems, d_pk, nc, rowpart, colpart, st); break;
+    case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, st); break;
+    case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, st); break;
     default:
-      hipLaunchKernelGGL(k_sym_mfma16, dim3(nitems), dim3(256), 0, st, d_items, d_pk, nc, rowpart,
-                         colpart);
+      hipLaunchKernelGGL(k_sym_mfma16, dim3(nstrips), dim3(256), 0, st, d_strips, d_sitems, d_pk,
+                         nc, rowpart, colpart);
       break;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_sym_finalize_strip(int nc, const SymPanel* d_panels, int npanels,
+                                     const PassArgs& pa, const double* rowpart,
+                                     const double* colpart, double* partials, hipStream_t st) {
+#define FIN_CASE(N)                                                                        \
+  case N:                                                                                  \
+    hipLaunchKernelGGL(k_sym_finalize_strip<N>, dim3(npanels), dim3(256), 0, st, d_panels, \
+                       pa, rowpart, colpart, partials);                                    \
+    break;
+  switch (nc) {
+    FIN_CASE(1) FIN_CASE(2) FIN_CASE(3) FIN_CASE(4) FIN_CASE(5) FIN_CASE(6) FIN_CASE(7) FIN_CASE(8)
+    FIN_CASE(9) FIN_CASE(10) FIN_CASE(11) FIN_CASE(12) FIN_CASE(13) FIN_CASE(14) FIN_CASE(15)
+    FIN_CASE(16)
+    default: return hipErrorInvalidValue;
+  }
+#undef FIN_CASE
   return hipGetLastError();
 }
 

@@ -456,3 +456,24 @@ def test_vamp_50_iterations_vs_oracle(K, tmp_path):
     assert worst < tol, worst
     assert final < tol, final
     eng.close()
+
+
+@pytest.mark.parametrize("strip", [1, 2, 3, 8])
+@pytest.mark.parametrize("ncol", [4, 8, 16])
+def test_mfma_strips_vs_numpy(strip, ncol, monkeypatch):
+    """MFMA pass work items are strips of up to SGV_MFMA_STRIP panels of one
+    parity sharing a 512-column chunk (sym_mfma.hip); blocks with up to 20
+    panels, so chunks split into several strips at every setting."""
+    monkeypatch.setenv("SGV_MFMA_STRIP", str(strip))
+    sizes = [5000, 513, 2600, 1]
+    blocks = rand_blocks(sizes, seed=strip + ncol, symmetric=True)
+    eng = Engine(sizes, K=1)
+    for b, B in enumerate(blocks):
+        eng.set_ld_block(0, b, B)
+    eng.set_ridge(0.1)
+    V = np.random.RandomState(ncol).normal(size=(ncol, sum(sizes)))
+    Y = eng.ld_matvec(0, V)
+    L = vo.BlockLD(blocks, s=0.1)
+    for j in range(ncol):
+        assert maxrel(Y[j], L.matvec_Rs(V[j])) < 1e-12, j
+    eng.close()
