@@ -446,6 +446,12 @@ static int grow(sgv_ctx* c, double** buf, size_t* cap, size_t need) {
   return SGV_OK;
 }
 
+// VALU-pass items dispatched largest first (env SGV_SYM_LPT=0: panel/chunk order)
+static bool sym_lpt() {
+  const char* e = std::getenv("SGV_SYM_LPT");
+  return !(e && e[0] == '0');
+}
+
 // panels per MFMA strip (env SGV_MFMA_STRIP, read when a plan is built; 1 =
 // one (panel, chunk) item per workgroup)
 static int mfma_strip_len() {
@@ -581,7 +587,16 @@ static int ensure_plan(sgv_ctx* c, int ld) {
     }
     pl.nitems[cls] = (int)items.size();
     pl.npanels = (int)panels.size();
-    CHK(upload_table(c, items, &pl.d_items[cls]));
+    {
+      // dispatch order: largest items first (rows x columns), so the small edge
+      // items fill the tail of the launch; the `item` field keeps the partial slot
+      std::vector<SymItem> order = items;
+      if (sym_lpt())
+        std::stable_sort(order.begin(), order.end(), [](const SymItem& a, const SymItem& b) {
+          return (int64_t)a.H * a.nc > (int64_t)b.H * b.nc;
+        });
+      CHK(upload_table(c, order, &pl.d_items[cls]));
+    }
     CHK(upload_table(c, panels, &pl.d_panels[cls]));
     if (cls == 1) CHK(build_strips(c, ld, items, panels, &pl));
     const size_t ncmax = (size_t)sym_class_nc(cls);

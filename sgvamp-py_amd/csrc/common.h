@@ -185,6 +185,52 @@ __device__ __forceinline__ void block_reduce_store(double (&v)[NV], double* __re
   }
 }
 
+// ---- packed-pass finalize (sym_pass.hip, sym_mfma.hip) --------------------
+constexpr int FIN_Q = 4;   // threads per panel row in the finalize kernels
+
+// Combine the FIN_Q parts of a row's sum in order (part 0 first), then, on
+// part 0: out = c1*y + c2*in (and yout, R_s in), and the panel's partial dots
+// (wave butterfly, waves 0..3 in order) -> partials[pn.part * NC + c].
+// Called by every thread of a 256*FIN_Q workgroup.
+template <int NC>
+__device__ __forceinline__ void fin_epilogue(const SymPanel& pn, const PassArgs& pa, double (&y)[NC],
+                                             double* __restrict__ partials) {
+  __shared__ double s_y[FIN_Q - 1][256];
+  __shared__ double s_w[4][NC];
+  const int t = threadIdx.x & 255, q = threadIdx.x >> 8;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    if (q) s_y[q - 1][t] = y[c];
+    __syncthreads();
+    if (!q) {
+      double v = y[c];
+#pragma unroll
+      for (int p = 0; p < FIN_Q - 1; ++p) v += s_y[p][t];
+      y[c] = v;
+    }
+    __syncthreads();
+  }
+  const int lane = t & (WAVE - 1), wid = t / WAVE;
+  const bool row = q == 0 && t < pn.H;   // part 0 writes the outputs
+  const int64_t idx = pn.voff + pn.r0 + (t < pn.H ? t : 0);
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    double acc = 0.0;
+    if (row) {
+      const double in = pa.in[c][idx];
+      const double o = pa.c1[c] * y[c] + pa.c2[c] * in;
+      pa.out[c][idx] = o;
+      if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * y[c] + pa.ys0 * in;
+      if (pa.dot[c]) acc = pa.dot[c][idx] * o;
+    }
+    const double s = wave_sum(acc);
+    if (q == 0 && lane == 0) s_w[wid][c] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < NC)
+    partials[(int64_t)pn.part * NC + t] = ((s_w[0][t] + s_w[1][t]) + s_w[2][t]) + s_w[3][t];
+}
+
 // ---- launchers (defined in the .hip files) ------------------------------
 // LD pass: one workgroup per row group; partials[rg.part * nc + c].
 hipError_t launch_ld_pass(int nc, const BlkDesc* d_blks, const RowGroup* d_rg, int nrg,

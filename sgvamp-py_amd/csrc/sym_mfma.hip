@@ -403,51 +403,37 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
   }
 }
 
-// one workgroup per panel; thread t = panel row r0 + t: this panel's row parts
-// (chunk order), then the strips of the own-parity chunk (column offset t),
-// then those of the other-parity chunk (offset 256 + t) -- fixed order
+// one workgroup per panel, FIN_Q threads per row (row t = r0 + (thread & 255),
+// part q = thread >> 8): part q sums the panel's row parts item_begin + q, + 2q,
+// ..., then the strips own_sb + q, ... of the own-parity chunk (column offset
+// t) and oth_sb + q, ... of the other-parity chunk (offset 256 + t); parts are
+// added in order (fin_epilogue) -- fixed order throughout
 template <int NC>
-__global__ __launch_bounds__(256) void k_sym_finalize_strip(const SymPanel* __restrict__ panels,
-                                                            PassArgs pa,
-                                                            const double* __restrict__ rowpart,
-                                                            const double* __restrict__ colpart,
-                                                            double* __restrict__ partials) {
+__global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize_strip(
+    const SymPanel* __restrict__ panels, PassArgs pa, const double* __restrict__ rowpart,
+    const double* __restrict__ colpart, double* __restrict__ partials) {
   const SymPanel pn = panels[blockIdx.x];
-  const int t = threadIdx.x;
+  const int t = threadIdx.x & 255, q = threadIdx.x >> 8;
   const int tr = t < pn.H ? t : 0;
   double y[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) y[c] = 0.0;
-  for (int itm = pn.item_begin; itm < pn.item_end; ++itm) {
+  for (int itm = pn.item_begin + q; itm < pn.item_end; itm += FIN_Q) {
     const double* rp = rowpart + ((int64_t)itm * SYM_H + t) * NC;
 #pragma unroll
     for (int c = 0; c < NC; ++c) y[c] += ldg(rp + c);
   }
-  for (int sl = pn.own_sb; sl < pn.own_se; ++sl) {
+  for (int sl = pn.own_sb + q; sl < pn.own_se; sl += FIN_Q) {
     const double* cp = colpart + (int64_t)sl * NC * MF_CW + tr;
 #pragma unroll
     for (int c = 0; c < NC; ++c) y[c] += ldg(cp + c * MF_CW);
   }
-  for (int sl = pn.oth_sb; sl < pn.oth_se; ++sl) {
+  for (int sl = pn.oth_sb + q; sl < pn.oth_se; sl += FIN_Q) {
     const double* cp = colpart + (int64_t)sl * NC * MF_CW + SYM_H + tr;
 #pragma unroll
     for (int c = 0; c < NC; ++c) y[c] += ldg(cp + c * MF_CW);
   }
-  double acc[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) acc[c] = 0.0;
-  if (t < pn.H) {
-    const int64_t idx = pn.voff + pn.r0 + t;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const double in = pa.in[c][idx];
-      const double o = pa.c1[c] * y[c] + pa.c2[c] * in;
-      pa.out[c][idx] = o;
-      if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * y[c] + pa.ys0 * in;
-      if (pa.dot[c]) acc[c] = pa.dot[c][idx] * o;
-    }
-  }
-  block_reduce_store<NC>(acc, partials + (int64_t)pn.part * NC, NC);
+  fin_epilogue<NC>(pn, pa, y, partials);
 }
 
 // Pk[i][c] = in[c][i] for c < ncol, 0 for ncol <= c < 16 (i over the padded vector)
@@ -495,7 +481,7 @@ hipError_t launch_sym_finalize_strip(int nc, const SymPanel* d_panels, int npane
                                      const double* colpart, double* partials, hipStream_t st) {
 #define FIN_CASE(N)                                                                        \
   case N:                                                                                  \
-    hipLaunchKernelGGL(k_sym_finalize_strip<N>, dim3(npanels), dim3(256), 0, st, d_panels, \
+    hipLaunchKernelGGL(k_sym_finalize_strip<N>, dim3(npanels), dim3(256 * FIN_Q), 0, st, d_panels, \
                        pa, rowpart, colpart, partials);                                    \
     break;
   switch (nc) {

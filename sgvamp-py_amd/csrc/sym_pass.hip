@@ -130,40 +130,44 @@ __global__ __launch_bounds__(256) void k_sym_pass(const SymItem* __restrict__ it
   }
 }
 
-// one workgroup per panel; thread t = panel row r0 + t.  The item offsets of
-// the block's earlier panels are staged in LDS first, so the column-partial
-// loads of the panel loop are independent of each other (no descriptor load
-// in the chain) and, with NC a compile-time constant, unconditional: the
-// compiler keeps them in flight together instead of draining vmcnt at every
-// per-column branch.
+// one workgroup per panel, FIN_Q threads per panel row (row t = r0 + (thread
+// & 255), part q = thread >> 8): part q sums the row's chunk row-parts
+// item_begin + q, + 2q, ... and the column parts of the block's earlier panels
+// q, q + FIN_Q, ...; the parts are then added in order q = 0..3.  The item
+// offsets of the earlier panels are staged in LDS first, so the column-partial
+// loads are independent of each other (no descriptor load in the chain) and,
+// with NC a compile-time constant, unconditional: the compiler keeps them in
+// flight together.  Splitting the chains 4 ways shortens the latency-bound
+// loop (at one LD block per GPU the finalize was ~4 % of the pass).
 template <int NC>
-__global__ __launch_bounds__(256) void k_sym_finalize(const SymPanel* __restrict__ panels, int cw,
-                                                      PassArgs pa,
-                                                      const double* __restrict__ rowpart,
-                                                      const double* __restrict__ colpart,
-                                                      double* __restrict__ partials) {
+__global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize(const SymPanel* __restrict__ panels,
+                                                              int cw, PassArgs pa,
+                                                              const double* __restrict__ rowpart,
+                                                              const double* __restrict__ colpart,
+                                                              double* __restrict__ partials) {
   constexpr int PCH = 1024;   // panels staged per round
   __shared__ int s_ib[PCH];
   const SymPanel pn = panels[blockIdx.x];
-  const int t = threadIdx.x;
+  const int t = threadIdx.x & 255, q = threadIdx.x >> 8;
   double y[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) y[c] = 0.0;
   const int i = pn.r0 + (t < pn.H ? t : 0);   // block-relative row
-  // this panel's row parts, chunk order
-  for (int itm = pn.item_begin; itm < pn.item_end; ++itm) {
+  // this panel's row parts, chunk order within the part
+  for (int itm = pn.item_begin + q; itm < pn.item_end; itm += FIN_Q) {
     const double* rp = rowpart + ((int64_t)itm * SYM_H + t) * NC;
 #pragma unroll
     for (int c = 0; c < NC; ++c) y[c] += ldg(rp + c);
   }
-  // column parts of the earlier panels of this block, panel order
+  // column parts of the earlier panels of this block, panel order within the part
   for (int g0 = 0; g0 < pn.g; g0 += PCH) {
     const int gn = min(PCH, pn.g - g0);
     __syncthreads();
-    for (int k = t; k < gn; k += 256) s_ib[k] = panels[pn.blk_panel0 + g0 + k].item_begin;
+    for (int k = threadIdx.x; k < gn; k += 256 * FIN_Q)
+      s_ib[k] = panels[pn.blk_panel0 + g0 + k].item_begin;
     __syncthreads();
 #pragma unroll 4
-    for (int k = 0; k < gn; ++k) {
+    for (int k = q; k < gn; k += FIN_Q) {
       const int rel = i - (g0 + k) * SYM_H;      // column relative to that panel's first row
       const int ch = rel / cw;
       const double* cp = colpart + ((int64_t)(s_ib[k] + ch) * NC) * cw + (rel - ch * cw);
@@ -171,21 +175,7 @@ __global__ __launch_bounds__(256) void k_sym_finalize(const SymPanel* __restrict
       for (int c = 0; c < NC; ++c) y[c] += ldg(cp + (int64_t)c * cw);
     }
   }
-  double acc[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) acc[c] = 0.0;
-  if (t < pn.H) {
-    const int64_t idx = pn.voff + i;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const double in = pa.in[c][idx];
-      const double o = pa.c1[c] * y[c] + pa.c2[c] * in;
-      pa.out[c][idx] = o;
-      if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * y[c] + pa.ys0 * in;
-      if (pa.dot[c]) acc[c] = pa.dot[c][idx] * o;
-    }
-  }
-  block_reduce_store<NC>(acc, partials + (int64_t)pn.part * NC, NC);
+  fin_epilogue<NC>(pn, pa, y, partials);
 }
 
 template <int NC, int NSEG>
@@ -220,7 +210,7 @@ hipError_t launch_sym_finalize(int nc, int cls, const SymPanel* d_panels, int np
   const int cw = 1024 >> cls;
 #define FIN_CASE(N)                                                                              \
   case N:                                                                                        \
-    hipLaunchKernelGGL(k_sym_finalize<N>, dim3(npanels), dim3(256), 0, st, d_panels, cw, pa,     \
+    hipLaunchKernelGGL(k_sym_finalize<N>, dim3(npanels), dim3(256 * FIN_Q), 0, st, d_panels, cw, pa,     \
                        rowpart, colpart, partials);                                              \
     break;
   switch (nc) {
