@@ -76,6 +76,14 @@ static int mfma_min_default() {
   }();
   return v;
 }
+// CG loop driver: 1 (default) = pipelined, device-side control (cg_loop_dev);
+// 0 = host-side stop test per iteration (cg_loop).  Env SGV_CG_PIPE.
+static int cg_pipe_default() {
+  const char* e = std::getenv("SGV_CG_PIPE");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+constexpr int CG_RING = 4;   // mirror slots of the pipelined CG
+
 static int sym_class_nc(int cls) { return std::min(16, 2 << (cls + 1)); }   // widest NC using cls
 
 struct sgv_ctx {
@@ -157,6 +165,14 @@ struct sgv_ctx {
   std::vector<int> rx0_valid;  // RX0[c] == R_s X[c]
   int rs_rec = 1;              // carry R_s x through the CG (sgv_set_rs_recurrence)
   hipEvent_t ev_sync = nullptr;   // host waits spin on this event
+  // pipelined CG (cg_loop_dev): device control state, its host mirror ring
+  // (fine-grained pinned, one slot per in-flight iteration), init staging
+  int cg_pipe = 1;
+  CgState* d_cgs = nullptr;
+  CgState* h_cgm = nullptr;       // [CG_RING]
+  CgState* h_cgi = nullptr;
+  double* d_rhonew = nullptr;
+  hipEvent_t ev_cg[4] = {nullptr, nullptr, nullptr, nullptr};
   // timers
   std::vector<hipEvent_t> evpool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
@@ -771,6 +787,142 @@ static int cg_loop(sgv_ctx* c, const CgCols& cc, double* rho, const double* atol
   return SGV_OK;
 }
 
+// spin on an event already recorded on the ctx stream
+static int event_spin(sgv_ctx* c, hipEvent_t ev) {
+  hipError_t e;
+  while ((e = hipEventQuery(ev)) == hipErrorNotReady) __builtin_ia32_pause();
+  if (e != hipSuccess) return fail(c, SGV_ERR_HIP, "event wait: %s", hipGetErrorString(e));
+  return SGV_OK;
+}
+
+// Pipelined CG: the iteration of cg_loop with the stop test, beta and alpha on
+// the device, so no host round trip sits between two iterations.  Iteration it
+// is enqueued as [k_cg_ctl (stop test of `it`, beta), p update, LD pass(es) +
+// p.q, x/r update + r.r]; the p/x/r kernels and the passes read the device
+// state and become no-ops once no column is active.  The host then waits only
+// for k_cg_ctl of `it` (the first kernel of the iteration: the wait overlaps
+// the pass) and enqueues it + 1 behind it with the columns still active after
+// that test -- so the column set of every pass is a function of the trajectory
+// alone (deterministic; a column stopping at it + 1's test rides along in that
+// pass unused).  When the test of `it` stops every column, that iteration's
+// kernels were no-ops: their pass timers and byte counts are dropped.
+static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const double* atol,
+                       int maxiter, const int* active_in, int* iters, int* info, int* passes) {
+  const int ncol = cc.ncol;
+  CgState* hi = c->h_cgi;   // the previous solve's copy has completed (its mirror was read)
+  std::memset(hi, 0, sizeof(CgState));
+  unsigned mask = 0;
+  for (int j = 0; j < ncol; ++j) {
+    hi->rho[j] = rho0[j];
+    hi->atol[j] = atol[j];
+    hi->active[j] = active_in[j] ? 1 : 0;
+    if (active_in[j]) mask |= 1u << j;
+  }
+  hi->any = mask ? 1 : 0;
+  HIPCHK(hipMemcpyAsync(c->d_cgs, hi, sizeof(CgState), hipMemcpyHostToDevice, c->st));
+  const volatile CgState* last = nullptr;
+  int executed = 0;
+  for (int it = 0; it < maxiter; ++it) {
+    const size_t np0 = c->pending.size();
+    const double cnt0[5] = {c->ld_launches, c->ld_bytes, c->dense_bytes, c->rhs_bytes,
+                            c->aux_bytes};
+    int npass = 0;
+    CgState* slot = c->h_cgm + (it % CG_RING);
+    HIPCHK(launch_cg_ctl(c->d_cgs, slot, c->d_rhonew, it, ncol, -1, c->st));
+    HIPCHK(hipEventRecord(c->ev_cg[it % CG_RING], c->st));
+    if (it > 0) {  // iterative.py:403-407
+      PArgs pa{};
+      pa.ncol = ncol;
+      pa.mask = mask;
+      pa.st = c->d_cgs;
+      for (int j = 0; j < ncol; ++j) {
+        pa.P[j] = cc.P[j];
+        pa.Rr[j] = cc.Rr[j];
+      }
+      HIPCHK(launch_cg_p(c->d_ch, c->nch, pa, c->st));
+    }
+    // q = A p (iterative.py:411): one pass per LD matrix over its columns
+    for (int ld = 0; ld < c->nld; ++ld) {
+      PassArgs pa{};
+      Map16 map = identity_map();
+      int nc = 0;
+      for (int j = 0; j < ncol; ++j) {
+        if (!(mask >> j & 1u) || cc.col_ld[j] != ld) continue;
+        pa.in[nc] = cc.P[j];
+        pa.out[nc] = cc.Q[j];
+        pa.dot[nc] = cc.P[j];
+        pa.yout[nc] = cc.RX[j] ? cc.Y[j] : nullptr;
+        pa.c1[nc] = cc.c1[j];
+        pa.c2[nc] = cc.c2[j];
+        map.d[nc] = j;
+        ++nc;
+      }
+      if (!nc) continue;
+      pa.ys1 = 1.0 - cc.s;   // Y = R_s p = (1-s) R p + s p
+      pa.ys0 = cc.s;
+      pa.run = &c->d_cgs->any;
+      CHK(ld_pass(c, ld, nc, pa));
+      CHK(reduce_dev(c, nc, ld_parts(c, ld), map, c->d_pq));
+      ++npass;
+    }
+    // alpha = rho / p.q; x += alpha p; r -= alpha q; r.r (:412-415)
+    XrArgs xa{};
+    xa.ncol = ncol;
+    xa.mask = mask;
+    xa.pq = c->d_pq;
+    xa.st = c->d_cgs;
+    for (int j = 0; j < ncol; ++j) {
+      xa.X[j] = cc.X[j];
+      xa.Rr[j] = cc.Rr[j];
+      xa.P[j] = cc.P[j];
+      xa.Q[j] = cc.Q[j];
+      xa.RX[j] = cc.RX[j];
+      xa.Y[j] = cc.Y[j];
+    }
+    HIPCHK(launch_cg_xr(c->d_ch, c->nch, xa, c->d_part, c->st));
+    CHK(reduce_dev(c, MAXC, c->d_ch_begin, identity_map(), c->d_rhonew));
+    // the stop test of `it` (its first kernel) decides whether it did any work
+    CHK(event_spin(c, c->ev_cg[it % CG_RING]));
+    last = slot;
+    if (!last->any) {
+      while (c->pending.size() > np0) {   // no-op passes: not timed, not counted
+        c->evpool.push_back(c->pending.back().first);
+        c->evpool.push_back(c->pending.back().second);
+        c->pending.pop_back();
+      }
+      c->ld_launches = cnt0[0];
+      c->ld_bytes = cnt0[1];
+      c->dense_bytes = cnt0[2];
+      c->rhs_bytes = cnt0[3];
+      c->aux_bytes = cnt0[4];
+      break;
+    }
+    ++executed;
+    if (passes) *passes += npass;
+    mask = 0;
+    for (int j = 0; j < ncol; ++j)
+      if (last->active[j]) mask |= 1u << j;
+  }
+  if (executed == maxiter) {  // for-loop exhausted (iterative.py:420-422)
+    CgState* slot = c->h_cgm + (maxiter % CG_RING);
+    HIPCHK(launch_cg_ctl(c->d_cgs, slot, c->d_rhonew, maxiter, ncol, maxiter, c->st));
+    HIPCHK(hipEventRecord(c->ev_cg[maxiter % CG_RING], c->st));
+    CHK(event_spin(c, c->ev_cg[maxiter % CG_RING]));
+    last = slot;
+  }
+  for (int j = 0; j < ncol; ++j) {
+    iters[j] = last->iters[j];
+    info[j] = last->info[j];
+  }
+  return SGV_OK;
+}
+
+static int cg_run(sgv_ctx* c, const CgCols& cc, double* rho, const double* atol, int maxiter,
+                  const int* active, int* iters, int* info, int* passes) {
+  if (c->cg_pipe) return cg_loop_dev(c, cc, rho, atol, maxiter, active, iters, info, passes);
+  return cg_loop(c, cc, rho, atol, maxiter, active, iters, info, passes);
+}
+
 // ---------------------------------------------------------------------------
 // lifetime
 // ---------------------------------------------------------------------------
@@ -914,6 +1066,13 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   CREATE_HIP(hipMalloc(&c->d_tot, sizeof(double) * 64));
   CREATE_HIP(hipMalloc(&c->d_pq, sizeof(double) * 2 * MAXC));
   CREATE_HIP(hipHostMalloc(&c->h_tot, sizeof(double) * 64, hipHostMallocCoherent));
+  CREATE_HIP(hipMalloc(&c->d_cgs, sizeof(CgState)));
+  CREATE_HIP(hipMalloc(&c->d_rhonew, sizeof(double) * MAXC));
+  CREATE_HIP(hipHostMalloc(&c->h_cgm, sizeof(CgState) * CG_RING, hipHostMallocCoherent));
+  CREATE_HIP(hipHostMalloc(&c->h_cgi, sizeof(CgState)));
+  for (int i = 0; i < CG_RING; ++i)
+    CREATE_HIP(hipEventCreateWithFlags(&c->ev_cg[i], hipEventDisableTiming));
+  c->cg_pipe = cg_pipe_default();
   c->xnz.assign(2 * K, 0);
   c->rx0_valid.assign(2 * K, 0);
 #undef CREATE_HIP
@@ -957,6 +1116,12 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   (void)hipFree(c->d_tot);
   (void)hipFree(c->d_pq);
   if (c->h_tot) (void)hipHostFree(c->h_tot);
+  if (c->d_cgs) (void)hipFree(c->d_cgs);
+  if (c->d_rhonew) (void)hipFree(c->d_rhonew);
+  if (c->h_cgm) (void)hipHostFree(c->h_cgm);
+  if (c->h_cgi) (void)hipHostFree(c->h_cgi);
+  for (hipEvent_t e : c->ev_cg)
+    if (e) (void)hipEventDestroy(e);
   if (c->d_stage) (void)hipFree(c->d_stage);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   for (auto& pr : c->pending) {
@@ -1056,6 +1221,12 @@ extern "C" int sgv_set_rs_recurrence(sgv_ctx* c, int on) {
   ENTER(c);
   c->rs_rec = on ? 1 : 0;
   std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), 0);   // re-derive R_s x0 once
+  return SGV_OK;
+}
+
+extern "C" int sgv_set_cg_pipeline(sgv_ctx* c, int on) {
+  ENTER(c);
+  c->cg_pipe = on ? 1 : 0;
   return SGV_OK;
 }
 
@@ -1533,7 +1704,7 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
     }
   }
   cc.s = s;
-  CHK(cg_loop(c, cc, rhov, atol, cg_maxit, active, iters, info, &passes));
+  CHK(cg_run(c, cc, rhov, atol, cg_maxit, active, iters, info, &passes));
 
   // damping, u.Sigma2_u, xhat2.r, x.any() (:322-323, 338, 352)
   PostArgs po{};
@@ -1771,7 +1942,7 @@ extern "C" int sgv_cg_solve(sgv_ctx* c, int ld, int ncol, const double* c1, cons
       active[j] = 0;
     }
   }
-  CHK(cg_loop(c, cc, rho, atol, maxiter, active, iters_out, info_out, nullptr));
+  CHK(cg_run(c, cc, rho, atol, maxiter, active, iters_out, info_out, nullptr));
   for (int j = 0; j < ncol; ++j) CHK(download_vec(c, cc.X[j], x + (size_t)j * c->Mloc));
   return SGV_OK;
 }

@@ -114,6 +114,10 @@ struct PassArgs {
   double c1[MAXC];
   double c2[MAXC];
   double ys1, ys0;
+  // non-null: the pass runs only if *run != 0 (device-side CG control: a pass
+  // enqueued ahead of the stop test becomes a no-op); every workgroup reads it
+  // next to its first descriptor load
+  const int* run;
 };
 
 // most values one ordered reduction carries
@@ -335,6 +339,28 @@ struct InitArgs {
 hipError_t launch_lmmse_init(const ChunkDesc* d_ch, int nch, const InitArgs& a, double* d_part,
                              hipStream_t st);
 
+// Device-side CG control (k_cg_ctl, the pipelined CG of capi.hip): per column
+// the scipy loop scalars; `any` = some column still iterating.
+struct CgState {
+  double rho[MAXC];        // r.r of the current iterate (rho_cur)
+  double rho_prev[MAXC];
+  double beta[MAXC];
+  double atol[MAXC];
+  int active[MAXC];
+  int iters[MAXC];
+  int info[MAXC];
+  int any;
+  int it;
+  int pad_[2];
+};
+// iteration `it` of the CG (iterative.py:397-407): it > 0 first takes rho_new
+// (the r.r reduction of iteration it-1) for the active columns; then the stop
+// test sqrt(rho) < atol (strict), and beta = rho / rho_prev.  final_it >= 0
+// instead marks the still-active columns as exhausted (iters = info =
+// final_it, :420-422).  The state is also copied to `mirror` (host memory).
+hipError_t launch_cg_ctl(CgState* d_st, CgState* mirror, const double* d_rho_new, int it,
+                         int ncol, int final_it, hipStream_t st);
+
 struct XrArgs {
   double* X[MAXC];
   double* Rr[MAXC];
@@ -346,6 +372,7 @@ struct XrArgs {
   const double* pq;         // device, indexed by column
   unsigned mask;
   int ncol;
+  const CgState* st;        // non-null: rho and the active columns from the device state
 };
 hipError_t launch_cg_xr(const ChunkDesc* d_ch, int nch, const XrArgs& a, double* d_part,
                         hipStream_t st);
@@ -356,6 +383,7 @@ struct PArgs {
   double beta[MAXC];
   unsigned mask;
   int ncol;
+  const CgState* st;        // non-null: beta and the active columns from the device state
 };
 hipError_t launch_cg_p(const ChunkDesc* d_ch, int nch, const PArgs& a, hipStream_t st);
 

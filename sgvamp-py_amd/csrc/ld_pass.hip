@@ -31,6 +31,7 @@ __global__ __launch_bounds__(256) void k_ld_pass(const BlkDesc* __restrict__ blk
   __shared__ double red[4][LD_RW * NC];
 
   const RowGroup rg = rgs[blockIdx.x];
+  if (pa.run && !ldg(pa.run)) return;   // no-op pass (pipelined CG past its stop test)
   const BlkDesc bd = blks[rg.blk];
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // provably wave-uniform

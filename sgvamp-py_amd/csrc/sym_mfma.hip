@@ -66,7 +66,8 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
                                                          const SymItem* __restrict__ sitems,
                                                          const double* __restrict__ pk, int ncol,
                                                          double* __restrict__ rowpart,
-                                                         double* __restrict__ colpart) {
+                                                         double* __restrict__ colpart,
+                                                         const int* __restrict__ run) {
   static_assert(NW == 4, "waves 0 and 1 own the diagonal half of a chunk");
   constexpr int WC = MF_CW / NW;   // columns per wave (128)
   constexpr int NT = WC / 32;      // 32-column steps per wave
@@ -74,6 +75,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   __shared__ double red[2][NW][256];
   __shared__ __attribute__((aligned(16))) double stg[NW][16 * MF_LDP];
   const SymStrip sp = strips[blockIdx.x];
+  if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lo = lane & 15, hi = lane >> 4, bq = (lane >> 2) & 3, n4 = lane & 3;
@@ -269,11 +271,13 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
                                                      double* __restrict__ rowpart,
-                                                     double* __restrict__ colpart) {
+                                                     double* __restrict__ colpart,
+                                                     const int* __restrict__ run) {
   constexpr int LDP = MF_LDP;
   __shared__ double red[2][4][256];
   __shared__ __attribute__((aligned(16))) double stg[4][16 * LDP];
   const SymStrip sp = strips[blockIdx.x];
+  if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lo = lane & 15, hi = lane >> 4;
@@ -413,6 +417,7 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize_strip(
     const SymPanel* __restrict__ panels, PassArgs pa, const double* __restrict__ rowpart,
     const double* __restrict__ colpart, double* __restrict__ partials) {
   const SymPanel pn = panels[blockIdx.x];
+  if (pa.run && !ldg(pa.run)) return;
   const int t = threadIdx.x & 255, q = threadIdx.x >> 8;
   const int tr = t < pn.H ? t : 0;
   double y[NC];
@@ -439,6 +444,7 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize_strip(
 // Pk[i][c] = in[c][i] for c < ncol, 0 for ncol <= c < 16 (i over the padded vector)
 __global__ __launch_bounds__(256) void k_pack16(PassArgs pa, int ncol, int64_t mpad,
                                                 double* __restrict__ pk) {
+  if (pa.run && !ldg(pa.run)) return;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= mpad * 16) return;
   const int64_t i = t >> 4;
@@ -449,9 +455,9 @@ __global__ __launch_bounds__(256) void k_pack16(PassArgs pa, int ncol, int64_t m
 template <int NG, int NW, int PD>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
-                      hipStream_t st) {
+                      const int* run, hipStream_t st) {
   hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD>), dim3(nstrips), dim3(NW * 64), 0, st, d_strips,
-                     d_sitems, d_pk, nc, rowpart, colpart);
+                     d_sitems, d_pk, nc, rowpart, colpart, run);
 }
 
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
@@ -466,11 +472,11 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
   // not come from cache): measured in DESIGN.md
   switch ((nc + 3) / 4) {
     // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
-    case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, st); break;
-    case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, st); break;
+    case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, st); break;
+    case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, st); break;
     default:
       hipLaunchKernelGGL(k_sym_mfma16, dim3(nstrips), dim3(256), 0, st, d_strips, d_sitems, d_pk,
-                         nc, rowpart, colpart);
+                         nc, rowpart, colpart, pa.run);
       break;
   }
   return hipGetLastError();

@@ -20,8 +20,8 @@
 
 namespace sgv {
 
-template <int NC, int RWI, int NSEG>
-__global__ __launch_bounds__(256) void k_sym_pass(const SymItem* __restrict__ items, PassArgs pa,
+template <int NC, int RWI, int NSEG, int OCC = 1>
+__global__ __launch_bounds__(256, OCC) void k_sym_pass(const SymItem* __restrict__ items, PassArgs pa,
                                                   double* __restrict__ rowpart,
                                                   double* __restrict__ colpart) {
   constexpr int CW = NSEG * 128;
@@ -31,6 +31,7 @@ __global__ __launch_bounds__(256) void k_sym_pass(const SymItem* __restrict__ it
   __shared__ d2 cbw[4][NC][CW / 2];
 
   const SymItem it = items[blockIdx.x];
+  if (pa.run && !ldg(pa.run)) return;   // no-op pass (pipelined CG past its stop test)
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);   // provably wave-uniform
   const double* pp[NC];
@@ -148,6 +149,7 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize(const SymPanel* __
   constexpr int PCH = 1024;   // panels staged per round
   __shared__ int s_ib[PCH];
   const SymPanel pn = panels[blockIdx.x];
+  if (pa.run && !ldg(pa.run)) return;
   const int t = threadIdx.x & 255, q = threadIdx.x >> 8;
   double y[NC];
 #pragma unroll

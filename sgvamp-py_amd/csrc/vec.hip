@@ -207,18 +207,26 @@ hipError_t launch_lmmse_init(const ChunkDesc* d_ch, int nch, const InitArgs& a, 
 __global__ __launch_bounds__(VTHREADS) void k_cg_xr(const ChunkDesc* __restrict__ chs, XrArgs a,
                                                     double* __restrict__ part) {
   const ChunkDesc ch = chs[blockIdx.x];
+  unsigned mask = a.mask;
+  if (a.st) {   // device-side control: the columns still active after this iteration's test
+    if (!a.st->any) return;   // no-op iteration (its r.r partials are never read)
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c)
+      if (c < a.ncol && !a.st->active[c]) mask &= ~(1u << c);
+  }
   double acc[MAXC];
   double alpha[MAXC];
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     acc[c] = 0.0;
-    alpha[c] = (c < a.ncol && ((a.mask >> c) & 1u)) ? a.rho[c] / a.pq[c] : 0.0;
+    const double rc = a.st ? a.st->rho[c] : a.rho[c];
+    alpha[c] = (c < a.ncol && ((mask >> c) & 1u)) ? rc / a.pq[c] : 0.0;
   }
   CHUNK_LOOP(ch) {
     const int64_t i = ch.voff + t;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c)
-      if (c < a.ncol && ((a.mask >> c) & 1u)) {
+      if (c < a.ncol && ((mask >> c) & 1u)) {
         a.X[c][i] = a.X[c][i] + alpha[c] * a.P[c][i];
         if (a.RX[c]) a.RX[c][i] = a.RX[c][i] + alpha[c] * a.Y[c][i];   // R_s x carried
         const double r = a.Rr[c][i] - alpha[c] * a.Q[c][i];
@@ -238,16 +246,83 @@ hipError_t launch_cg_xr(const ChunkDesc* d_ch, int nch, const XrArgs& a, double*
 // p = beta p + r   (iterative.py:405-407: p *= beta; p += z)
 __global__ __launch_bounds__(VTHREADS) void k_cg_p(const ChunkDesc* __restrict__ chs, PArgs a) {
   const ChunkDesc ch = chs[blockIdx.x];
+  unsigned mask = a.mask;
+  double beta[MAXC];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) beta[c] = a.beta[c];
+  if (a.st) {
+    if (!a.st->any) return;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      if (c < a.ncol && !a.st->active[c]) mask &= ~(1u << c);
+      beta[c] = a.st->beta[c];
+    }
+  }
   CHUNK_LOOP(ch) {
     const int64_t i = ch.voff + t;
 #pragma unroll
     for (int c = 0; c < MAXC; ++c)
-      if (c < a.ncol && ((a.mask >> c) & 1u)) a.P[c][i] = a.P[c][i] * a.beta[c] + a.Rr[c][i];
+      if (c < a.ncol && ((mask >> c) & 1u)) a.P[c][i] = a.P[c][i] * beta[c] + a.Rr[c][i];
   }
 }
 
 hipError_t launch_cg_p(const ChunkDesc* d_ch, int nch, const PArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_cg_p, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a);
+  return hipGetLastError();
+}
+
+// Device-side CG control, one wave (thread j = column j); same expressions
+// as the host loop (correctly rounded sqrt and division: the same decisions
+// and the same beta bit for bit).
+__global__ __launch_bounds__(WAVE) void k_cg_ctl(CgState* __restrict__ s, CgState* mirror,
+                                                const double* __restrict__ rho_new, int it, int ncol,
+                                                int final_it) {
+  const int j = threadIdx.x;
+  int act = 0;
+  if (j < ncol) {
+    act = s->active[j];
+    if (final_it >= 0) {                     // for-loop exhausted (iterative.py:420-422)
+      if (act) {
+        s->iters[j] = final_it;
+        s->info[j] = final_it;
+      }
+      act = 0;
+    } else if (act) {
+      if (it > 0) {                          // rho_prev = rho_cur; rho_cur = r.r (:412-415)
+        s->rho_prev[j] = s->rho[j];
+        s->rho[j] = rho_new[j];
+      }
+      if (sqrt(s->rho[j]) < s->atol[j]) {   // iterative.py:398 (strict <)
+        act = 0;
+        s->active[j] = 0;
+        s->iters[j] = it;
+        s->info[j] = 0;
+      } else if (it > 0) {
+        s->beta[j] = s->rho[j] / s->rho_prev[j];   // :405
+      }
+    }
+  }
+  const int any = __any(act) ? 1 : 0;
+  if (j == 0) {
+    s->any = any;
+    s->it = it;
+  }
+  if (mirror && j < MAXC) {
+    mirror->rho[j] = s->rho[j];
+    mirror->active[j] = j < ncol ? (final_it >= 0 ? 0 : s->active[j]) : 0;
+    mirror->iters[j] = s->iters[j];
+    mirror->info[j] = s->info[j];
+  }
+  if (mirror && j == 0) {
+    mirror->any = any;
+    mirror->it = it;
+  }
+}
+
+hipError_t launch_cg_ctl(CgState* d_st, CgState* mirror, const double* d_rho_new, int it, int ncol,
+                         int final_it, hipStream_t st) {
+  hipLaunchKernelGGL(k_cg_ctl, dim3(1), dim3(WAVE), 0, st, d_st, mirror, d_rho_new, it, ncol,
+                     final_it);
   return hipGetLastError();
 }
 

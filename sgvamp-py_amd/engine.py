@@ -87,6 +87,11 @@ class Engine:
         """Packed LD passes with >= nc_min right-hand sides use the f64 MFMA kernel."""
         self.ctx.sgv_set_mfma_min(int(nc_min))
 
+    def set_cg_pipeline(self, on):
+        """Device-side CG control with the next iteration enqueued ahead (default)
+        or the host-side stop test per iteration."""
+        self.ctx.sgv_set_cg_pipeline(1 if on else 0)
+
     def set_rs_recurrence(self, on):
         """Carry R_s x through the CG (default) instead of a gamw LD pass."""
         self.ctx.sgv_set_rs_recurrence(1 if on else 0)

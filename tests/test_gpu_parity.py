@@ -227,14 +227,18 @@ def read_tsv(path):
     return text, np.array(rows)
 
 
-@pytest.mark.parametrize("packing", [True, False, "valu", "direct"])
+@pytest.mark.parametrize("packing", [True, False, "valu", "direct", "hostcg"])
 @pytest.mark.parametrize("name", case_names())
-def test_vamp_matches_reference_golden(name, packing, tmp_path):
+def test_vamp_matches_reference_golden(name, packing, tmp_path, monkeypatch):
     """packing True: packed storage (MFMA pass for K >= 2, i.e. >= 3 CG columns),
     R_s x carried through the CG (default); "valu": packed storage, VALU pass
     only; False: dense storage; "direct": R_s xhat2 / R_s Sigma2_u by a separate
-    LD pass, as the reference computes them (src/sgvamp.py:352,359)."""
+    LD pass, as the reference computes them (src/sgvamp.py:352,359); "hostcg":
+    the CG's stop test on the host every iteration instead of the pipelined
+    device-side control (SGV_CG_PIPE=0)."""
     c = Case(name)
+    if packing == "hostcg":
+        monkeypatch.setenv("SGV_CG_PIPE", "0")
     if packing == "valu" and c.K == 1:
         pytest.skip("K = 1 never reaches 3 columns: same as packing=True")
     v, xh = run_vamp_case(c, tmp_path, ld_packing=bool(packing),
@@ -270,6 +274,29 @@ def test_vamp_matches_reference_golden(name, packing, tmp_path):
     assert text.splitlines()[0] == c.metrics_csv_text.splitlines()[0]
     np.testing.assert_allclose(rows, c.metrics_csv, rtol=1e-7, atol=1e-12)
     v.engine.close()
+
+
+@pytest.mark.parametrize("name", ["k1_defaults", "k1_blocks_csr_s_damp", "k2_shared",
+                                  "k4_shared_s_damp"])
+def test_cg_pipeline_matches_host_loop(name, tmp_path, monkeypatch):
+    """Pipelined CG (device-side stop test/beta, next iteration enqueued ahead)
+    vs the host-tested loop: identical CG counts; at K = 1 (VALU passes, whose
+    per-column sums do not depend on the column count) bitwise identical."""
+    c = Case(name)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("SGV_CG_PIPE", mode)
+        d = tmp_path / mode
+        d.mkdir()
+        v, xh = run_vamp_case(c, d)
+        out[mode] = (v, xh, [h["cg_iters"] for h in v.history], [h["cg_info"] for h in v.history])
+        v.engine.close()
+    assert out["0"][2] == out["1"][2] and out["0"][3] == out["1"][3]
+    for a_, b_ in zip(out["0"][1], out["1"][1]):
+        if c.K == 1:
+            np.testing.assert_array_equal(a_, b_)
+        else:
+            assert maxrel(b_, a_) < 1e-10
 
 
 def test_vamp_is_deterministic(tmp_path):
