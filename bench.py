@@ -56,6 +56,7 @@ def parse():
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     p.add_argument("--cpu-iters", type=int, default=30)   # ~10 s of CPU work on the box
     p.add_argument("--no-files", action="store_true", help="skip the per-iteration output files")
+    p.add_argument("--out-dir", default=None, help="keep the output files here (default: a temp dir)")
     p.add_argument("--share-device", action="store_true",
                    help="rehearsal: every rank on device 0 with the host exchange (RCCL refuses "
                         "two ranks on one device); timings are then not a multi-GPU result")
@@ -166,7 +167,8 @@ def main():
     eng.set_ridge(args.ridge)
     run = dict(cg_maxit=500, em_prior_maxit=100, learn_gamw=True, lmmse_damp=bool(args.lmmse_damp),
                prior_update="em", update_prior_from=1)
-    tmp = tempfile.mkdtemp(prefix="sgvamp_bench_")
+    tmp = args.out_dir or tempfile.mkdtemp(prefix="sgvamp_bench_")
+    os.makedirs(tmp, exist_ok=True)
     v = VAMP(N=N_list if K > 1 else N_list[0], Nt=Nt, M=eng.M, K=K, a=a, out_dir=tmp,
              out_name="bench", comm=comm, seed=args.seed, write_files=not args.no_files, **flags)
     x0 = beta * np.sqrt(N_list[0])                      # main.py:276-279

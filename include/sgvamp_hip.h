@@ -116,11 +116,12 @@ int sgv_set_rs_recurrence(sgv_ctx* ctx, int on);
  * cores (v_mfma_f64_16x16x4f64); fewer run on the VALU.  0 = never.  Default 3
  * (env SGV_MFMA_MIN).  Results agree to rounding, not bitwise, across the two. */
 int sgv_set_mfma_min(sgv_ctx* ctx, int nc_min);
-/* CG driver (scipy iterative.py:397-422 either way): on (default) the stop
- * test, beta and alpha run on the device and iteration i+1 is enqueued while
- * iteration i's pass runs (no host round trip between iterations); off, the
- * host tests every iteration's residual.  Same iterates and counts; env
- * SGV_CG_PIPE=0 sets the default off. */
+/* CG and EM-loop drivers (scipy iterative.py:397-422; src/sgvamp.py:250-257):
+ * on (default) the CG's stop test, beta and alpha, and the EM prior loop's
+ * update and convergence test run on the device, and iteration i+1 is enqueued
+ * while iteration i runs (no host round trip between iterations); off, the
+ * host tests every iteration.  Same iterates and counts; env SGV_CG_PIPE=0
+ * sets the default off. */
 int sgv_set_cg_pipeline(sgv_ctx* ctx, int on);
 /* Storage of LD blocks set or generated from now on: mode 1 (default) stores a
  * block that is exactly symmetric as packed upper-triangle panels (about half

@@ -173,6 +173,12 @@ struct sgv_ctx {
   CgState* h_cgi = nullptr;
   double* d_rhonew = nullptr;
   hipEvent_t ev_cg[4] = {nullptr, nullptr, nullptr, nullptr};
+  // device EM loop (sgv_em with cg_pipe on): state, mirror ring, init staging
+  EmState* d_ems = nullptr;
+  EmState* h_emm = nullptr;       // [CG_RING]
+  EmState* h_emi = nullptr;
+  double* d_emtot = nullptr;
+  hipEvent_t ev_em[4] = {nullptr, nullptr, nullptr, nullptr};
   // timers
   std::vector<hipEvent_t> evpool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
@@ -1072,6 +1078,12 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   CREATE_HIP(hipHostMalloc(&c->h_cgi, sizeof(CgState)));
   for (int i = 0; i < CG_RING; ++i)
     CREATE_HIP(hipEventCreateWithFlags(&c->ev_cg[i], hipEventDisableTiming));
+  CREATE_HIP(hipMalloc(&c->d_ems, sizeof(EmState)));
+  CREATE_HIP(hipMalloc(&c->d_emtot, sizeof(double) * MAXNV));
+  CREATE_HIP(hipHostMalloc(&c->h_emm, sizeof(EmState) * CG_RING, hipHostMallocCoherent));
+  CREATE_HIP(hipHostMalloc(&c->h_emi, sizeof(EmState)));
+  for (int i = 0; i < CG_RING; ++i)
+    CREATE_HIP(hipEventCreateWithFlags(&c->ev_em[i], hipEventDisableTiming));
   c->cg_pipe = cg_pipe_default();
   c->xnz.assign(2 * K, 0);
   c->rx0_valid.assign(2 * K, 0);
@@ -1121,6 +1133,12 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   if (c->h_cgm) (void)hipHostFree(c->h_cgm);
   if (c->h_cgi) (void)hipHostFree(c->h_cgi);
   for (hipEvent_t e : c->ev_cg)
+    if (e) (void)hipEventDestroy(e);
+  if (c->d_ems) (void)hipFree(c->d_ems);
+  if (c->d_emtot) (void)hipFree(c->d_emtot);
+  if (c->h_emm) (void)hipHostFree(c->h_emm);
+  if (c->h_emi) (void)hipHostFree(c->h_emi);
+  for (hipEvent_t e : c->ev_em)
     if (e) (void)hipEventDestroy(e);
   if (c->d_stage) (void)hipFree(c->d_stage);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
@@ -1482,6 +1500,40 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
   double lam = *lam_io;
   double om[MAXL];
   for (int l = 0; l < nslab; ++l) om[l] = omegas_io[l];
+  if (c->cg_pipe && maxit > 0) {
+    // Device loop: k_em reads lam/omegas from the device state, k_em_ctl updates
+    // it and tests convergence; step it + 1 is enqueued before the host waits
+    // for step it's test, so the GPU does not idle for a host round trip per
+    // step (one no-op step runs past the last).  Every rank enqueues the same
+    // steps (the stop decision is made from the same global sums).
+    EmState* hi = c->h_emi;   // the previous loop's init copy has completed
+    std::memset(hi, 0, sizeof(EmState));
+    hi->lam = lam;
+    for (int l = 0; l < nslab; ++l) hi->om[l] = om[l];
+    HIPCHK(hipMemcpyAsync(c->d_ems, hi, sizeof(EmState), hipMemcpyHostToDevice, c->st));
+    ea.st = c->d_ems;
+    auto enqueue = [&](int j) -> int {
+      HIPCHK(launch_em(c->d_ch, c->nch, ea, c->d_part, c->st));
+      CHK(reduce_dev(c, EM_NV, c->d_ch_begin, identity_map(), c->d_emtot));
+      HIPCHK(launch_em_ctl(c->d_ems, c->h_emm + j % CG_RING, c->d_emtot, nslab, (double)c->Mtot,
+                           j, maxit, c->st));
+      HIPCHK(hipEventRecord(c->ev_em[j % CG_RING], c->st));
+      return SGV_OK;
+    };
+    CHK(enqueue(0));
+    const volatile EmState* last = nullptr;
+    for (int it = 0; it < maxit; ++it) {
+      if (it + 1 < maxit) CHK(enqueue(it + 1));
+      CHK(event_spin(c, c->ev_em[it % CG_RING]));
+      last = c->h_emm + it % CG_RING;
+      if (last->done) break;
+    }
+    *lam_io = last->lam;
+    for (int l = 0; l < nslab; ++l) omegas_io[l] = last->om[l];
+    if (steps_out) *steps_out = last->steps;
+    if (final_err_out) *final_err_out = last->err;
+    return SGV_OK;
+  }
   double om_err = 0.0, lam_err = 0.0;
   int steps = 0;
   for (int it = 0; it < maxit; ++it) {

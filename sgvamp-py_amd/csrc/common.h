@@ -299,7 +299,17 @@ hipError_t launch_mle_minsq(const ChunkDesc* d_ch, int nch, const MleArgs& a, do
 hipError_t launch_mle_terms(const ChunkDesc* d_ch, int nch, const MleArgs& a, double* d_part,
                             hipStream_t st);
 
+// Device-side EM control (k_em_ctl, the device EM loop of sgv_em): the prior
+// scalars between steps, the last step's error and the stop flag
+struct EmState {
+  double lam;
+  double om[MAXL];
+  double err;               // max(omegas_rel_err, lam_rel_err) of the last step
+  int steps;
+  int done;                 // converged or em_prior_maxit reached: k_em is a no-op
+};
 struct EmArgs {
+  const EmState* st;        // non-null: lam and omegas from the device state
   const double* r1[MAXK];
   double a[MAXK];
   double gam1[MAXK];
@@ -311,6 +321,11 @@ struct EmArgs {
 constexpr int EM_NV = MAXL + 2;   // [0] sum_j avg_k(pi); [1..L-1] omega numerators; [nslab+1] denominator
 hipError_t launch_em(const ChunkDesc* d_ch, int nch, const EmArgs& a, double* d_part,
                      hipStream_t st);
+// one EM update from the reduced sums tot[EM_NV] (src/sgvamp.py:134-136) and the
+// loop's stop test (:252-257); it + 1 == maxit also stops.  The state is
+// copied to `mirror` (host memory).
+hipError_t launch_em_ctl(EmState* d_st, EmState* mirror, const double* d_tot, int nslab,
+                         double Mtot, int it, int maxit, hipStream_t st);
 
 struct CohortPtrs {
   const double* r[MAXK];

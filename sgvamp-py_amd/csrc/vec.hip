@@ -12,6 +12,44 @@ namespace sgv {
 #define CHUNK_LOOP(ch)                                                  \
   for (int t = threadIdx.x; t < (ch).len; t += VTHREADS)
 
+// Latency-bound vector kernels: a thread owns markers t, t + 256, t + 512,
+// t + 768 of its chunk (the CHUNK_LOOP order, so every per-thread sum adds in
+// the same order), and all of their loads are issued before the first store.
+// Pointers taken from argument structs may alias as far as the compiler
+// knows, so in a CHUNK_LOOP each store fences the next marker's loads: a chain
+// of MPT x (columns) dependent HBM round trips (~24 us for k_cg_xr whatever M).
+// Independent columns / cohorts run as grid.y, one per workgroup.
+constexpr int MPT = CHUNK / VTHREADS;
+static_assert(CHUNK % VTHREADS == 0, "markers per thread");
+
+// one value summed over the workgroup like block_reduce_store (wave butterfly,
+// waves 0..3 in order), stored by thread 0 at *out
+template <int NV>
+__device__ __forceinline__ void block_reduce_slots(double (&v)[NV], double* __restrict__ base,
+                                                   const int (&slot)[NV]) {
+  __shared__ double sm[VTHREADS / WAVE][NV];
+  const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double s = wave_sum(v[k]);
+    if (lane == 0) sm[wid][k] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+    if ((int)threadIdx.x == k) base[slot[k]] = ((sm[0][k] + sm[1][k]) + sm[2][k]) + sm[3][k];
+}
+
+// block y == 0 of a chunk zeroes the partial slots whose owner (column or
+// cohort) has no workgroup (owner >= n), as the one-workgroup-per-chunk kernels
+// did by summing zeros
+template <class F>
+__device__ __forceinline__ void zero_unowned(double* __restrict__ base, int nv, int n, F owner) {
+  if (blockIdx.y != 0) return;
+  for (int t = threadIdx.x; t < nv; t += VTHREADS)
+    if (owner(t) >= n) base[t] = 0.0;
+}
+
 // ---------------------------------------------------------------------------
 // denoiser_meta + der_denoiser_meta, src/sgvamp.py:93-114, per marker (:273,285)
 // ---------------------------------------------------------------------------
@@ -22,13 +60,29 @@ __global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restric
   double acc[MAXK];
 #pragma unroll
   for (int k = 0; k < MAXK; ++k) acc[k] = 0.0;
-  CHUNK_LOOP(ch) {
+  // loads of the thread's MPT markers first (see MPT), then the markers in order
+  double vr[MPT][MAXK], vxo[MPT];
+#pragma unroll
+  for (int j = 0; j < MPT; ++j) {
+    const int t = threadIdx.x + j * VTHREADS;
+    if (t < ch.len) {
+      const int64_t i = ch.voff + t;
+#pragma unroll
+      for (int k = 0; k < MAXK; ++k)
+        if (k < a.K) vr[j][k] = a.r1[k][i];
+      if (a.damp) vxo[j] = a.xhat1[i];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < MPT; ++j) {
+    const int t = threadIdx.x + j * VTHREADS;
+    if (t >= ch.len) continue;
     const int64_t i = ch.voff + t;
     // np.inner(rs, a*gam1s) (:96)
     double inner = 0.0;
 #pragma unroll
     for (int k = 0; k < MAXK; ++k)
-      if (k < a.K) inner = (k == 0) ? a.r1[0][i] * a.ag[0] : inner + a.r1[k][i] * a.ag[k];
+      if (k < a.K) inner = (k == 0) ? vr[j][0] * a.ag[0] : inner + vr[j][k] * a.ag[k];
     double mu[MAXL];
     int m = 0;
     double best = 0.0;
@@ -64,7 +118,7 @@ __global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restric
     const double EXP2 = exp(-0.5 * (mum * mum / s2m));   // :100
     const double Den = (1 - a.lam) * EXP2 + a.lam * sumD;
     double x = Num / Den;
-    if (a.damp) x = a.rho * x + (1 - a.rho) * a.xhat1[i];   // :275-276
+    if (a.damp) x = a.rho * x + (1 - a.rho) * vxo[j];   // :275-276
     a.xhat1[i] = x;
     // der_denoiser_meta for every cohort k (:112-114 with a[k]*gam1s[k])
 #pragma unroll
@@ -100,16 +154,35 @@ hipError_t launch_denoise(const ChunkDesc* d_ch, int nch, const DenoiseArgs& a, 
 __global__ __launch_bounds__(VTHREADS) void k_em(const ChunkDesc* __restrict__ chs, EmArgs a,
                                                  double* __restrict__ part) {
   const ChunkDesc ch = chs[blockIdx.x];
+  double lam = a.lam, om[MAXL];
+#pragma unroll
+  for (int l = 0; l < MAXL; ++l) om[l] = a.omegas[l];
+  if (a.st) {   // device EM loop
+    if (a.st->done) return;
+    lam = a.st->lam;
+#pragma unroll
+    for (int l = 0; l < MAXL; ++l) om[l] = a.st->om[l];
+  }
   double acc[EM_NV];
 #pragma unroll
   for (int v = 0; v < EM_NV; ++v) acc[v] = 0.0;
-  CHUNK_LOOP(ch) {
-    const int64_t i = ch.voff + t;
+  double vr[MPT][MAXK];
+#pragma unroll
+  for (int j = 0; j < MPT; ++j) {
+    const int t = threadIdx.x + j * VTHREADS;
+    if (t < ch.len)
+#pragma unroll
+      for (int k = 0; k < MAXK; ++k)
+        if (k < a.K) vr[j][k] = a.r1[k][ch.voff + t];
+  }
+#pragma unroll
+  for (int j = 0; j < MPT; ++j) {
+    if ((int)threadIdx.x + j * VTHREADS >= ch.len) continue;
     double avg = 0.0;   // sum_k pi_k a_k (np.average numerator, sequential over k)
 #pragma unroll
     for (int k = 0; k < MAXK; ++k)
       if (k < a.K) {
-        const double r = a.r1[k][i];
+        const double r = vr[j][k];
         const double r2 = r * r;                  // np.power(r1s, 2)
         const double ginv = 1.0 / a.gam1[k];      // gam1invs
         double tl[MAXL];
@@ -125,11 +198,11 @@ __global__ __launch_bounds__(VTHREADS) void k_em(const ChunkDesc* __restrict__ c
 #pragma unroll
         for (int l = 0; l < MAXL; ++l)
           if (l < a.nslab) {
-            xi[l] = a.lam * a.omegas[l] * exp(tl[l] - emax) / sqrt(ginv + a.sigmas[l]);   // :128
+            xi[l] = lam * om[l] * exp(tl[l] - emax) / sqrt(ginv + a.sigmas[l]);   // :128
             sum_xi = (l == 0) ? xi[l] : sum_xi + xi[l];                                   // :129
           }
         const double pi =
-            1.0 / (1.0 + (1 - a.lam) * exp(-r2 / 2 * a.gam1[k] - emax) / sqrt(ginv) / sum_xi);  // :131
+            1.0 / (1.0 + (1 - lam) * exp(-r2 / 2 * a.gam1[k] - emax) / sqrt(ginv) / sum_xi);  // :131
         const double pa = pi * a.a[k];
         avg = (k == 0) ? pa : avg + pa;
 #pragma unroll
@@ -148,55 +221,127 @@ hipError_t launch_em(const ChunkDesc* d_ch, int nch, const EmArgs& a, double* d_
   return hipGetLastError();
 }
 
+// the host loop's update and test (capi.hip sgv_em), same expressions in the
+// same order: -ffp-contract=off and correctly rounded division and sqrt give
+// the same bits, so the same step count
+__global__ __launch_bounds__(WAVE) void k_em_ctl(EmState* __restrict__ s, EmState* mirror,
+                                                const double* __restrict__ tot, int nslab,
+                                                double Mtot, int it, int maxit) {
+  if (threadIdx.x != 0) return;
+  if (!s->done) {
+    const double lam = s->lam;
+    const double lam_new = tot[0] / Mtot;                 // np.mean (:134)
+    double om_new[MAXL];
+    double dn = 0.0, on = 0.0;
+    for (int l = 0; l < nslab; ++l) {
+      om_new[l] = tot[1 + l] / tot[1 + nslab];            // :136
+      const double d = om_new[l] - s->om[l];
+      dn += d * d;
+      on += s->om[l] * s->om[l];
+    }
+    const double om_err = sqrt(dn) / sqrt(on);            // :254
+    const double lam_err = fabs(lam_new - lam) / lam_new; // :255
+    s->lam = lam_new;
+    for (int l = 0; l < nslab; ++l) s->om[l] = om_new[l];
+    s->steps = it + 1;
+    s->err = (om_err < lam_err) ? lam_err : om_err;       // std::max
+    if ((om_err < 1e-6 && lam_err < 1e-6) || it + 1 >= maxit) s->done = 1;   // :256
+  }
+  if (mirror) {
+    mirror->lam = s->lam;
+    for (int l = 0; l < MAXL; ++l) mirror->om[l] = s->om[l];
+    mirror->err = s->err;
+    mirror->steps = s->steps;
+    mirror->done = s->done;
+  }
+}
+
+hipError_t launch_em_ctl(EmState* d_st, EmState* mirror, const double* d_tot, int nslab,
+                         double Mtot, int it, int maxit, hipStream_t st) {
+  hipLaunchKernelGGL(k_em_ctl, dim3(1), dim3(WAVE), 0, st, d_st, mirror, d_tot, nslab, Mtot, it,
+                     maxit);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // LMMSE set-up, src/sgvamp.py:305-313 + scipy cg prologue (iterative.py:375-392)
 // partials: [c] = |b_c|^2, [MAXC + c] = |r0_c|^2
 // ---------------------------------------------------------------------------
 constexpr int INIT_NV = 2 * MAXC;
+// grid (nch, K): workgroup (chunk, k) does cohort k's two columns 2k, 2k + 1
 __global__ __launch_bounds__(VTHREADS) void k_lmmse_init(const ChunkDesc* __restrict__ chs,
                                                          InitArgs a,
                                                          double* __restrict__ part) {
   const ChunkDesc ch = chs[blockIdx.x];
-  double acc[INIT_NV];
+  const int k = blockIdx.y;
+  double* pb = part + (int64_t)blockIdx.x * INIT_NV;
+  zero_unowned(pb, INIT_NV, a.K, [](int t) { return (t < MAXC ? t : t - MAXC) / 2; });
+  const double* __restrict__ xh = a.xhat1;
+  const double* __restrict__ r1 = a.cp.r1[k];
+  const double* __restrict__ rk = a.cp.r[k];
+  const double* __restrict__ uk = a.cp.u[k];
+  double* __restrict__ r2o = a.cp.r2[k];
+  const double al = a.alpha1[k], gw = a.gamw[k], g2 = a.gam2[k];
+  const int c0 = 2 * k;
+  const bool w0 = a.warm[c0], w1 = a.warm[c0 + 1];
+  const bool sx = a.save_x0, sxr = sx && a.col.RXp[c0];
+  double vx[MPT], vr1[MPT], vr[MPT], vu[MPT], vrx[2][MPT], vxc[2][MPT];
 #pragma unroll
-  for (int v = 0; v < INIT_NV; ++v) acc[v] = 0.0;
-  CHUNK_LOOP(ch) {
-    const int64_t i = ch.voff + t;
-    const double x1 = a.xhat1[i];
+  for (int j = 0; j < MPT; ++j) {
+    const int t = threadIdx.x + j * VTHREADS;
+    if (t < ch.len) {
+      const int64_t i = ch.voff + t;
+      vx[j] = xh[i];
+      vr1[j] = r1[i];
+      vr[j] = rk[i];
+      vu[j] = uk[i];
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k)
-      if (k < a.K) {
-        const double r2 = (x1 - a.alpha1[k] * a.cp.r1[k][i]) / (1 - a.alpha1[k]);   // :310
-        a.cp.r2[k][i] = r2;
-        const double b1 = a.gamw[k] * a.cp.r[k][i] + a.gam2[k] * r2;               // :313
-        const double b2 = a.cp.u[k][i];                                            // :326
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int c = 2 * k + h;
-          const double b = h == 0 ? b1 : b2;
-          double r = b;
-          if (a.warm[c]) {
-            // r = b - A x0, A x0 = gamw (R_s x0) + gam2 x0 (:312; R_s x0 from the last gamw pass)
-            const double ax = a.gamw[k] * a.col.RX0[c][i] + a.gam2[k] * a.col.X[c][i];
-            r = b - ax;
-          }
-          a.col.Rr[c][i] = r;
-          a.col.P[c][i] = r;
-          acc[c] += b * b;
-          acc[MAXC + c] += r * r;
-        }
-        if (a.save_x0) {
-          a.col.X0[2 * k][i] = a.col.X[2 * k][i];
-          if (a.col.RXp[2 * k]) a.col.RXp[2 * k][i] = a.col.RX0[2 * k][i];
-        }
+      for (int h = 0; h < 2; ++h) {
+        const bool w = h ? w1 : w0;
+        vrx[h][j] = (w || (h == 0 && sxr)) ? a.col.RX0[c0 + h][i] : 0.0;
+        vxc[h][j] = (w || (h == 0 && sx)) ? a.col.X[c0 + h][i] : 0.0;
       }
+    }
   }
-  block_reduce_store<INIT_NV>(acc, part + (int64_t)blockIdx.x * INIT_NV, INIT_NV);
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};   // |b_c|^2, |b_c+1|^2, |r0_c|^2, |r0_c+1|^2
+#pragma unroll
+  for (int j = 0; j < MPT; ++j) {
+    const int t = threadIdx.x + j * VTHREADS;
+    if (t < ch.len) {
+      const int64_t i = ch.voff + t;
+      const double r2 = (vx[j] - al * vr1[j]) / (1 - al);   // :310
+      r2o[i] = r2;
+      const double b1 = gw * vr[j] + g2 * r2;               // :313
+      const double b2 = vu[j];                              // :326
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int c = c0 + h;
+        const double b = h == 0 ? b1 : b2;
+        double r = b;
+        if (h ? w1 : w0) {
+          // r = b - A x0, A x0 = gamw (R_s x0) + gam2 x0 (:312; R_s x0 carried)
+          const double ax = gw * vrx[h][j] + g2 * vxc[h][j];
+          r = b - ax;
+        }
+        a.col.Rr[c][i] = r;
+        a.col.P[c][i] = r;
+        acc[h] += b * b;
+        acc[2 + h] += r * r;
+      }
+      if (sx) {
+        a.col.X0[c0][i] = vxc[0][j];
+        if (sxr) a.col.RXp[c0][i] = vrx[0][j];
+      }
+    }
+  }
+  const int slot[4] = {c0, c0 + 1, MAXC + c0, MAXC + c0 + 1};
+  block_reduce_slots<4>(acc, pb, slot);
 }
 
 hipError_t launch_lmmse_init(const ChunkDesc* d_ch, int nch, const InitArgs& a, double* d_part,
                              hipStream_t st) {
-  hipLaunchKernelGGL(k_lmmse_init, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part);
+  if (a.K < 1 || a.K > MAXK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_lmmse_init, dim3(nch, a.K), dim3(VTHREADS), 0, st, d_ch, a, d_part);
   return hipGetLastError();
 }
 
@@ -204,70 +349,104 @@ hipError_t launch_lmmse_init(const ChunkDesc* d_ch, int nch, const InitArgs& a, 
 // CG update (iterative.py:412-415): alpha = rho / (p.q); x += alpha p;
 // r -= alpha q; partial rho_new = r.r  (partials [c], stride MAXC)
 // ---------------------------------------------------------------------------
+// grid (nch, ncol): workgroup (chunk, c) updates column c
 __global__ __launch_bounds__(VTHREADS) void k_cg_xr(const ChunkDesc* __restrict__ chs, XrArgs a,
                                                     double* __restrict__ part) {
   const ChunkDesc ch = chs[blockIdx.x];
-  unsigned mask = a.mask;
+  const int c = blockIdx.y;
+  double* pb = part + (int64_t)blockIdx.x * MAXC;
+  bool on = (a.mask >> c) & 1u;
+  double rc = a.rho[c];
   if (a.st) {   // device-side control: the columns still active after this iteration's test
-    if (!a.st->any) return;   // no-op iteration (its r.r partials are never read)
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-      if (c < a.ncol && !a.st->active[c]) mask &= ~(1u << c);
+    const int any = a.st->any, act = a.st->active[c];
+    rc = a.st->rho[c];
+    if (!any) return;   // no-op iteration (its r.r partials are never read)
+    on = on && act;
   }
-  double acc[MAXC];
-  double alpha[MAXC];
+  zero_unowned(pb, MAXC, a.ncol, [](int t) { return t; });
+  double acc[1] = {0.0};
+  if (on) {
+    const double alpha = rc / a.pq[c];
+    double* __restrict__ X = a.X[c];
+    double* __restrict__ Rr = a.Rr[c];
+    double* __restrict__ RX = a.RX[c];
+    const double* __restrict__ P = a.P[c];
+    const double* __restrict__ Q = a.Q[c];
+    const double* __restrict__ Y = a.Y[c];
+    double vx[MPT], vp[MPT], vr[MPT], vq[MPT], vrx[MPT], vy[MPT];
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
-    acc[c] = 0.0;
-    const double rc = a.st ? a.st->rho[c] : a.rho[c];
-    alpha[c] = (c < a.ncol && ((mask >> c) & 1u)) ? rc / a.pq[c] : 0.0;
-  }
-  CHUNK_LOOP(ch) {
-    const int64_t i = ch.voff + t;
-#pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-      if (c < a.ncol && ((mask >> c) & 1u)) {
-        a.X[c][i] = a.X[c][i] + alpha[c] * a.P[c][i];
-        if (a.RX[c]) a.RX[c][i] = a.RX[c][i] + alpha[c] * a.Y[c][i];   // R_s x carried
-        const double r = a.Rr[c][i] - alpha[c] * a.Q[c][i];
-        a.Rr[c][i] = r;
-        acc[c] += r * r;
+    for (int j = 0; j < MPT; ++j) {
+      const int t = threadIdx.x + j * VTHREADS;
+      if (t < ch.len) {
+        const int64_t i = ch.voff + t;
+        vx[j] = X[i];
+        vp[j] = P[i];
+        vr[j] = Rr[i];
+        vq[j] = Q[i];
+        if (RX) {
+          vrx[j] = RX[i];
+          vy[j] = Y[i];
+        }
       }
+    }
+#pragma unroll
+    for (int j = 0; j < MPT; ++j) {
+      const int t = threadIdx.x + j * VTHREADS;
+      if (t < ch.len) {
+        const int64_t i = ch.voff + t;
+        X[i] = vx[j] + alpha * vp[j];
+        if (RX) RX[i] = vrx[j] + alpha * vy[j];   // R_s x carried
+        const double r = vr[j] - alpha * vq[j];
+        Rr[i] = r;
+        acc[0] += r * r;
+      }
+    }
   }
-  block_reduce_store<MAXC>(acc, part + (int64_t)blockIdx.x * MAXC, MAXC);
+  const int slot[1] = {c};
+  block_reduce_slots<1>(acc, pb, slot);
 }
 
 hipError_t launch_cg_xr(const ChunkDesc* d_ch, int nch, const XrArgs& a, double* d_part,
                         hipStream_t st) {
-  hipLaunchKernelGGL(k_cg_xr, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part);
+  if (a.ncol < 1 || a.ncol > MAXC) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_cg_xr, dim3(nch, a.ncol), dim3(VTHREADS), 0, st, d_ch, a, d_part);
   return hipGetLastError();
 }
 
-// p = beta p + r   (iterative.py:405-407: p *= beta; p += z)
+// p = beta p + r   (iterative.py:405-407: p *= beta; p += z); grid (nch, ncol)
 __global__ __launch_bounds__(VTHREADS) void k_cg_p(const ChunkDesc* __restrict__ chs, PArgs a) {
   const ChunkDesc ch = chs[blockIdx.x];
-  unsigned mask = a.mask;
-  double beta[MAXC];
-#pragma unroll
-  for (int c = 0; c < MAXC; ++c) beta[c] = a.beta[c];
+  const int c = blockIdx.y;
+  bool on = (a.mask >> c) & 1u;
+  double beta = a.beta[c];
   if (a.st) {
-    if (!a.st->any) return;
+    const int any = a.st->any, act = a.st->active[c];
+    beta = a.st->beta[c];
+    if (!any) return;
+    on = on && act;
+  }
+  if (!on) return;
+  double* __restrict__ P = a.P[c];
+  const double* __restrict__ Rr = a.Rr[c];
+  double vp[MPT], vr[MPT];
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c) {
-      if (c < a.ncol && !a.st->active[c]) mask &= ~(1u << c);
-      beta[c] = a.st->beta[c];
+  for (int j = 0; j < MPT; ++j) {
+    const int t = threadIdx.x + j * VTHREADS;
+    if (t < ch.len) {
+      vp[j] = P[ch.voff + t];
+      vr[j] = Rr[ch.voff + t];
     }
   }
-  CHUNK_LOOP(ch) {
-    const int64_t i = ch.voff + t;
 #pragma unroll
-    for (int c = 0; c < MAXC; ++c)
-      if (c < a.ncol && ((mask >> c) & 1u)) a.P[c][i] = a.P[c][i] * beta[c] + a.Rr[c][i];
+  for (int j = 0; j < MPT; ++j) {
+    const int t = threadIdx.x + j * VTHREADS;
+    if (t < ch.len) P[ch.voff + t] = vp[j] * beta + vr[j];
   }
 }
 
 hipError_t launch_cg_p(const ChunkDesc* d_ch, int nch, const PArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(k_cg_p, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a);
+  if (a.ncol < 1 || a.ncol > MAXC) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_cg_p, dim3(nch, a.ncol), dim3(VTHREADS), 0, st, d_ch, a);
   return hipGetLastError();
 }
 
@@ -335,63 +514,114 @@ hipError_t launch_cg_ctl(CgState* d_st, CgState* mirror, const double* d_rho_new
 // ---------------------------------------------------------------------------
 constexpr int POST_NV = 4 * MAXK + MAXC;
 static_assert(POST_NV <= MAXNV, "post partials");
+// grid (nch, K): workgroup (chunk, k) does cohort k
 __global__ __launch_bounds__(VTHREADS) void k_lmmse_post(const ChunkDesc* __restrict__ chs,
                                                          PostArgs a,
                                                          double* __restrict__ part) {
   const ChunkDesc ch = chs[blockIdx.x];
-  double acc[POST_NV];
+  const int k = blockIdx.y;
+  double* pb = part + (int64_t)blockIdx.x * POST_NV;
+  zero_unowned(pb, POST_NV, a.K, [](int t) {
+    return t < 2 * MAXK ? t % MAXK : t < 2 * MAXK + MAXC ? (t - 2 * MAXK) / 2 : (t - 2 * MAXK - MAXC) % MAXK;
+  });
+  double* __restrict__ X0 = a.X[2 * k];
+  const double* __restrict__ X1 = a.X[2 * k + 1];
+  const double* __restrict__ Xp = a.X0[2 * k];
+  double* __restrict__ RX0 = a.RX[2 * k];
+  const double* __restrict__ RX1 = a.RX[2 * k + 1];
+  const double* __restrict__ RXp = a.RXp[2 * k];
+  const double* __restrict__ U = a.u[k];
+  const double* __restrict__ Rk = a.r[k];
+  const bool damp = a.damp, rs = a.rs;
+  const double rho = a.rho;
+  double vx[MPT], vxp[MPT], vs[MPT], vu[MPT], vr[MPT], vrx[MPT], vrxp[MPT], vrx1[MPT];
 #pragma unroll
-  for (int v = 0; v < POST_NV; ++v) acc[v] = 0.0;
-  CHUNK_LOOP(ch) {
-    const int64_t i = ch.voff + t;
-#pragma unroll
-    for (int k = 0; k < MAXK; ++k)
-      if (k < a.K) {
-        double x2 = a.X[2 * k][i];
-        if (a.damp) {
-          x2 = a.rho * x2 + (1 - a.rho) * a.X0[2 * k][i];   // :322-323
-          a.X[2 * k][i] = x2;
-        }
-        const double s2u = a.X[2 * k + 1][i];
-        const double uk = a.u[k][i];
-        acc[k] += uk * s2u;                                 // :338
-        acc[MAXK + k] += x2 * a.r[k][i];                    // :352
-        if (a.rs) {
-          double rx = a.RX[2 * k][i];
-          if (a.damp) {                                     // R_s is linear: damp with x
-            rx = a.rho * rx + (1 - a.rho) * a.RXp[2 * k][i];
-            a.RX[2 * k][i] = rx;
-          }
-          acc[2 * MAXK + MAXC + k] += x2 * rx;              // :352 xhat2^T R_s xhat2
-          acc[3 * MAXK + MAXC + k] += uk * a.RX[2 * k + 1][i];   // :359 u^T R_s Sigma2_u
-        }
-        acc[2 * MAXK + 2 * k] += (x2 != 0.0) ? 1.0 : 0.0;
-        acc[2 * MAXK + 2 * k + 1] += (s2u != 0.0) ? 1.0 : 0.0;
+  for (int j = 0; j < MPT; ++j) {
+    const int t = threadIdx.x + j * VTHREADS;
+    if (t < ch.len) {
+      const int64_t i = ch.voff + t;
+      vx[j] = X0[i];
+      vs[j] = X1[i];
+      vu[j] = U[i];
+      vr[j] = Rk[i];
+      if (damp) vxp[j] = Xp[i];
+      if (rs) {
+        vrx[j] = RX0[i];
+        vrx1[j] = RX1[i];
+        if (damp) vrxp[j] = RXp[i];
       }
+    }
   }
-  block_reduce_store<POST_NV>(acc, part + (int64_t)blockIdx.x * POST_NV, POST_NV);
+  // [u.S2u, x2.r, nnz x2, nnz S2u, x2.R_s x2, u.R_s S2u]
+  double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int j = 0; j < MPT; ++j) {
+    const int t = threadIdx.x + j * VTHREADS;
+    if (t < ch.len) {
+      const int64_t i = ch.voff + t;
+      double x2 = vx[j];
+      if (damp) {
+        x2 = rho * x2 + (1 - rho) * vxp[j];   // :322-323
+        X0[i] = x2;
+      }
+      const double s2u = vs[j];
+      const double uk = vu[j];
+      acc[0] += uk * s2u;                       // :338
+      acc[1] += x2 * vr[j];                     // :352
+      if (rs) {
+        double rx = vrx[j];
+        if (damp) {                             // R_s is linear: damp with x
+          rx = rho * rx + (1 - rho) * vrxp[j];
+          RX0[i] = rx;
+        }
+        acc[4] += x2 * rx;                      // :352 xhat2^T R_s xhat2
+        acc[5] += uk * vrx1[j];                 // :359 u^T R_s Sigma2_u
+      }
+      acc[2] += (x2 != 0.0) ? 1.0 : 0.0;
+      acc[3] += (s2u != 0.0) ? 1.0 : 0.0;
+    }
+  }
+  const int slot[6] = {k, MAXK + k, 2 * MAXK + 2 * k, 2 * MAXK + 2 * k + 1, 2 * MAXK + MAXC + k,
+                       3 * MAXK + MAXC + k};
+  block_reduce_slots<6>(acc, pb, slot);
 }
 
 hipError_t launch_lmmse_post(const ChunkDesc* d_ch, int nch, const PostArgs& a, double* d_part,
                              hipStream_t st) {
-  hipLaunchKernelGGL(k_lmmse_post, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part);
+  if (a.K < 1 || a.K > MAXK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_lmmse_post, dim3(nch, a.K), dim3(VTHREADS), 0, st, d_ch, a, d_part);
   return hipGetLastError();
 }
 
 // r1 = (xhat2 - alpha2 r2) / (1 - alpha2)   (src/sgvamp.py:348)
+// grid (nch, K)
 __global__ __launch_bounds__(VTHREADS) void k_r1_update(const ChunkDesc* __restrict__ chs,
                                                         R1Args a) {
   const ChunkDesc ch = chs[blockIdx.x];
-  CHUNK_LOOP(ch) {
-    const int64_t i = ch.voff + t;
+  const int k = blockIdx.y;
+  const double* __restrict__ X = a.X[k];
+  const double* __restrict__ r2 = a.r2[k];
+  double* __restrict__ r1 = a.r1[k];
+  const double al = a.alpha2[k];
+  double vx[MPT], vr[MPT];
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k)
-      if (k < a.K) a.r1[k][i] = (a.X[k][i] - a.alpha2[k] * a.r2[k][i]) / (1 - a.alpha2[k]);
+  for (int j = 0; j < MPT; ++j) {
+    const int t = threadIdx.x + j * VTHREADS;
+    if (t < ch.len) {
+      vx[j] = X[ch.voff + t];
+      vr[j] = r2[ch.voff + t];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < MPT; ++j) {
+    const int t = threadIdx.x + j * VTHREADS;
+    if (t < ch.len) r1[ch.voff + t] = (vx[j] - al * vr[j]) / (1 - al);
   }
 }
 
 hipError_t launch_r1_update(const ChunkDesc* d_ch, int nch, const R1Args& a, hipStream_t st) {
-  hipLaunchKernelGGL(k_r1_update, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a);
+  if (a.K < 1 || a.K > MAXK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_r1_update, dim3(nch, a.K), dim3(VTHREADS), 0, st, d_ch, a);
   return hipGetLastError();
 }
 
@@ -401,14 +631,26 @@ __global__ __launch_bounds__(VTHREADS) void k_metrics(const ChunkDesc* __restric
                                                       const double* __restrict__ x0,
                                                       double* __restrict__ part) {
   const ChunkDesc ch = chs[blockIdx.x];
+  double va[MPT], vb[MPT];
+#pragma unroll
+  for (int j = 0; j < MPT; ++j) {
+    const int t = threadIdx.x + j * VTHREADS;
+    if (t < ch.len) {
+      va[j] = x[ch.voff + t];
+      vb[j] = x0[ch.voff + t];
+    }
+  }
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  CHUNK_LOOP(ch) {
-    const int64_t i = ch.voff + t;
-    const double a = x[i], b = x0[i], d = a - b;
-    acc[0] += a * b;
-    acc[1] += a * a;
-    acc[2] += d * d;
-    acc[3] += b * b;
+#pragma unroll
+  for (int j = 0; j < MPT; ++j) {
+    const int t = threadIdx.x + j * VTHREADS;
+    if (t < ch.len) {
+      const double a = va[j], b = vb[j], d = a - b;
+      acc[0] += a * b;
+      acc[1] += a * a;
+      acc[2] += d * d;
+      acc[3] += b * b;
+    }
   }
   block_reduce_store<4>(acc, part + (int64_t)blockIdx.x * 4, 4);
 }

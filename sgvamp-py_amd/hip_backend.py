@@ -10,7 +10,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsgvamp_hip.so")
+# SGV_LIB: another build of the same library (same-box A/B runs in tools/)
+LIB_PATH = os.environ.get("SGV_LIB") or os.path.join(HERE, "libsgvamp_hip.so")
 
 SGV_OK = 0
 VEC_R, VEC_R1, VEC_XHAT1, VEC_XHAT2, VEC_SIG2U, VEC_X0 = range(6)

@@ -276,12 +276,13 @@ def test_vamp_matches_reference_golden(name, packing, tmp_path, monkeypatch):
     v.engine.close()
 
 
-@pytest.mark.parametrize("name", ["k1_defaults", "k1_blocks_csr_s_damp", "k2_shared",
+@pytest.mark.parametrize("name", ["k1_defaults", "k1_L3", "k1_blocks_csr_s_damp", "k2_shared",
                                   "k4_shared_s_damp"])
 def test_cg_pipeline_matches_host_loop(name, tmp_path, monkeypatch):
     """Pipelined CG (device-side stop test/beta, next iteration enqueued ahead)
-    vs the host-tested loop: identical CG counts; at K = 1 (VALU passes, whose
-    per-column sums do not depend on the column count) bitwise identical."""
+    and device EM loop (k_em_ctl) vs the host-tested loops: identical CG and EM
+    step counts; at K = 1 (VALU passes, whose per-column sums do not depend on
+    the column count) bitwise identical trajectories and CSV files."""
     c = Case(name)
     out = {}
     for mode in ("0", "1"):
@@ -289,9 +290,14 @@ def test_cg_pipeline_matches_host_loop(name, tmp_path, monkeypatch):
         d = tmp_path / mode
         d.mkdir()
         v, xh = run_vamp_case(c, d)
-        out[mode] = (v, xh, [h["cg_iters"] for h in v.history], [h["cg_info"] for h in v.history])
+        out[mode] = (v, xh, [h["cg_iters"] for h in v.history], [h["cg_info"] for h in v.history],
+                     [h.get("em_steps") for h in v.history],
+                     [(d / ("%s_cohort_%d.csv" % (name, k + 1))).read_text() for k in range(c.K)])
         v.engine.close()
     assert out["0"][2] == out["1"][2] and out["0"][3] == out["1"][3]
+    assert out["0"][4] == out["1"][4]
+    if c.K == 1:
+        assert out["0"][5] == out["1"][5]
     for a_, b_ in zip(out["0"][1], out["1"][1]):
         if c.K == 1:
             np.testing.assert_array_equal(a_, b_)
