@@ -155,6 +155,15 @@ int sgv_synth_ld_g(sgv_ctx* ctx, int ld, uint64_t geno_seed, int64_t marker0, in
 int sgv_synth_r(sgv_ctx* ctx, int k, uint64_t geno_seed, int64_t marker0, int Nsamp,
                 const double* y);
 
+/* ---- Hutchinson probes (host only, no device) ----------------------------
+ * src/sgvamp.py:326 u = np.random.binomial(p=1/2, n=1, size=n)*2-1 from a legacy
+ * numpy RandomState (MT19937) whose state is key[624], *pos (as
+ * RandomState.get_state() returns them): advances the stream by n samples and
+ * writes the +-1 values of samples [lo, hi) to out[0 .. hi-lo).  Bit for bit
+ * numpy's stream and values; replaces the draw each reference rank makes. */
+int sgv_probe_draw(uint32_t* key, int32_t* pos, int64_t n, int64_t lo, int64_t hi,
+                   int8_t* out);
+
 /* ---- the hot path -------------------------------------------------------- */
 
 /* Meta denoiser + derivative over all markers: src/sgvamp.py:93-114 applied at

@@ -68,6 +68,8 @@ _SIGS = {
     "sgv_cg_solve": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, _c_dbl_p, _c_dbl_p, _c_dbl_p,
                      ctypes.c_int, ctypes.c_double, _c_int_p, _c_int_p],
     "sgv_timers": [_vp, _c_dbl_p, ctypes.c_int],
+    "sgv_probe_draw": [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32),
+                       ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _c_i8_p],
     "sgv_sync": [_vp],
 }
 _RESTYPES = {"sgv_destroy": None, "sgv_last_error": ctypes.c_char_p}
@@ -90,6 +92,8 @@ def load(path=LIB_PATH):
                        "`make -C sgvamp-py_amd/csrc` (there is no CPU fallback)" % path)
     lib = ctypes.CDLL(path)
     for name, args in _SIGS.items():
+        if os.environ.get("SGV_LIB") and not hasattr(lib, name):
+            continue   # A/B run against an older build (tools/gpu_ab_bitwise.sh)
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, ctypes.c_int)
@@ -154,6 +158,35 @@ class Context:
             self.check(fn(self.h, *args), name)
 
         return call
+
+
+class ProbeStream:
+    """One cohort's Hutchinson probe stream (src/sgvamp.py:326): the legacy
+    RandomState `rs`'s binomial(p=1/2, n=1) draws, advanced and sliced in C
+    (sgv_probe_draw, bit for bit numpy's stream).  `rs` is not advanced."""
+
+    def __init__(self, rs):
+        name, key, pos = rs.get_state()[:3]
+        if name != "MT19937":
+            raise HipError("probe stream: %s is not a legacy MT19937 RandomState" % name)
+        self.key = np.ascontiguousarray(key, dtype=np.uint32).copy()
+        self.pos = np.array([pos], dtype=np.int32)
+        self.lib = load()
+        # A/B runs against an older build without sgv_probe_draw draw with numpy
+        self.rs = rs if os.environ.get("SGV_LIB") and not hasattr(self.lib, "sgv_probe_draw") \
+            else None
+
+    def draw(self, n, lo, hi):
+        """Advance by n samples; return u[lo:hi] as int8 +-1."""
+        if self.rs is not None:
+            return (self.rs.binomial(p=1 / 2, n=1, size=n) * 2 - 1)[lo:hi].astype(np.int8)
+        out = np.empty(max(hi - lo, 1), dtype=np.int8)
+        rc = self.lib.sgv_probe_draw(self.key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                     self.pos.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                     int(n), int(lo), int(hi), out.ctypes.data_as(_c_i8_p))
+        if rc != SGV_OK:
+            raise HipError("sgv_probe_draw failed (%d)" % rc)
+        return out[:hi - lo]
 
 
 # int fn(void* user, const double* send, double* recv, int64_t count)

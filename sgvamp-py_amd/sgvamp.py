@@ -283,7 +283,8 @@ class VAMP:
         K = self.K
         self._st = dict(gam1=[self.gam1] * K, gamw=[self.gamw] * K, alpha1=[0] * K,
                         alpha2=[0] * K, gamws=[[] for _ in range(K)], xhat1s=[],
-                        probes=self._probe_streams(), cg_maxit=cg_maxit,
+                        probes=[hb.ProbeStream(rs) for rs in self._probe_streams()],
+                        cg_maxit=cg_maxit,
                         em_prior_maxit=em_prior_maxit, learn_gamw=learn_gamw,
                         lmmse_damp=lmmse_damp, prior_update=prior_update,
                         update_prior_from=update_prior_from, return_xhat=return_xhat)
@@ -312,10 +313,10 @@ class VAMP:
             logging.debug(f"a = {self.a}")
 
     def _draw_probe(self, k):
-        """u_k = binomial(p=1/2, n=1, size=M)*2-1 (src/sgvamp.py:326), local slice."""
-        eng = self.engine
-        return (self._st["probes"][k].binomial(p=1 / 2, n=1, size=self.M) * 2 - 1)[eng.sl] \
-            .astype(np.int8)
+        """u_k = binomial(p=1/2, n=1, size=M)*2-1 (src/sgvamp.py:326), local slice:
+        the cohort's RandomState stream, drawn in C (hip_backend.ProbeStream)."""
+        sl = self.engine.sl
+        return self._st["probes"][k].draw(self.M, sl.start, sl.stop)
 
     def _submit_probes(self):
         # each cohort's stream is drawn in its own task; the next iteration's draws

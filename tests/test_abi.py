@@ -84,3 +84,33 @@ def test_product_does_not_import_oracle():
     for p in glob.glob(os.path.join(PKG, "*.py")):
         src = open(p).read()
         assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, flags=re.M), p
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2025, 987654321])
+def test_probe_stream_matches_numpy_binomial(seed):
+    """sgv_probe_draw (host only) reproduces src/sgvamp.py:326's
+    RandomState.binomial(p=1/2, n=1, size=M)*2-1 bit for bit, stream position
+    included: whole draws, rank slices, empty slices, successive iterations."""
+    import numpy as np
+    import hip_backend as hb
+
+    rs = np.random.RandomState(seed)
+    ps = hb.ProbeStream(np.random.RandomState(seed))
+    for n, lo, hi in [(200000, 0, 200000), (12345, 100, 9000), (1, 0, 1), (0, 0, 0),
+                      (77777, 77777, 77777), (5000, 0, 0), (3001, 1, 3000), (100000, 60000, 100000)]:
+        ref = (rs.binomial(p=1 / 2, n=1, size=n) * 2 - 1).astype(np.int8)[lo:hi]
+        np.testing.assert_array_equal(ps.draw(n, lo, hi), ref)
+
+
+def test_probe_stream_odd_position():
+    """A stream left at an odd 32-bit position (a 32-bit draw made before)."""
+    import numpy as np
+    import hip_backend as hb
+
+    rs = np.random.RandomState(5)
+    rs.randint(0, 10, dtype=np.int32)   # one 32-bit output
+    ps = hb.ProbeStream(rs)
+    assert ps.pos[0] % 2 == 1
+    for n in (5000, 1248, 3):
+        ref = (rs.binomial(p=1 / 2, n=1, size=n) * 2 - 1).astype(np.int8)
+        np.testing.assert_array_equal(ps.draw(n, 0, n), ref)
