@@ -166,6 +166,42 @@ int sgv_probe_draw(uint32_t* key, int32_t* pos, int64_t n, int64_t lo, int64_t h
 
 /* ---- the hot path -------------------------------------------------------- */
 
+/* One VAMP outer iteration, src/sgvamp.py:222-387 without the output files and
+ * logs, with no return to the caller between its phases:
+ *   flags & SGV_STEP_EM:  sgv_em (lam_io, omegas_io updated; ires[0] = steps,
+ *                         res[0] = final error);
+ *   sgv_denoise (damping iff SGV_STEP_DENOISE_DAMP);
+ *   out_slot 0/1:        sgv_outputs_begin(out_slot) (xhat1, r1 for the files);
+ *   SGV_STEP_METRICS:    sgv_metrics_begin (read with sgv_metrics_end);
+ *   alpha1 = der_sum / M_total, damped with alpha1_prev iff SGV_STEP_ALPHA1_DAMP
+ *   (:285-291), gam2 = gam1 (1 - alpha1) / alpha1 (:305): res[1 + k], res[1 + K + k];
+ *   sgv_lmmse (damping iff SGV_STEP_LMMSE_DAMP, gamw learning iff
+ *   SGV_STEP_LEARN_GAMW): out, cg_out as sgv_lmmse; ires[1] = LD passes.
+ * res holds 1 + 2K doubles, ires 2 ints. */
+#define SGV_STEP_EM 1
+#define SGV_STEP_DENOISE_DAMP 2
+#define SGV_STEP_ALPHA1_DAMP 4
+#define SGV_STEP_LMMSE_DAMP 8
+#define SGV_STEP_LEARN_GAMW 16
+#define SGV_STEP_METRICS 32
+int sgv_step(sgv_ctx* ctx, int it, int flags, int em_maxit, int nslab, const double* sigmas,
+             const double* a, double* lam_io, double* omegas_io, const double* gam1s,
+             double rho, const double* gamw, const double* alpha1_prev,
+             const double* alpha2_prev, const int8_t* probes, int cg_maxit, double rtol,
+             int out_slot, double* res, int* ires, double* out, int* cg_out);
+/* sgv_step on the context's host worker thread: returns at once; the caller may
+ * run host work (files, logs, the next probes) that does not touch the context
+ * (sgv_outputs_wait excepted) until sgv_step_end, which waits and returns
+ * sgv_step's status.  lam_io, omegas_io, probes and the outputs must stay valid
+ * until then; the other arrays are copied. */
+int sgv_step_begin(sgv_ctx* ctx, int it, int flags, int em_maxit, int nslab,
+                   const double* sigmas, const double* a, double* lam_io, double* omegas_io,
+                   const double* gam1s, double rho, const double* gamw,
+                   const double* alpha1_prev, const double* alpha2_prev, const int8_t* probes,
+                   int cg_maxit, double rtol, int out_slot, double* res, int* ires, double* out,
+                   int* cg_out);
+int sgv_step_end(sgv_ctx* ctx);
+
 /* Meta denoiser + derivative over all markers: src/sgvamp.py:93-114 applied at
  * :270-291.  xhat1 <- denoiser_meta(r1s, gam1s); if damp: xhat1 <- rho*xhat1 +
  * (1-rho)*xhat1_prev.  der_sum_out[k] = sum_j der_denoiser_meta_k(r1s[:, j])

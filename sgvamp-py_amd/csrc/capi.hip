@@ -12,6 +12,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <limits>
 #include <cmath>
 #include <cstdarg>
@@ -122,10 +126,26 @@ struct sgv_ctx {
   int8_t* d_probe = nullptr;
   size_t probe_cap = 0;
   int probe_slot = 0;
+  hipEvent_t ev_unpk[2] = {nullptr, nullptr};   // the slot's probes consumed (ctx stream)
+  int pref_slot = -1;                           // probes prefetched by sgv_step
+  const int8_t* pref_src = nullptr;
+  // copies between host and device run on their own stream, behind events: a
+  // DMA copy queued on the ctx stream stalls the kernels behind it for its
+  // start-up latency (~50-110 us measured per copy)
+  hipStream_t st_copy = nullptr;
+  hipEvent_t ev_pack[2] = {nullptr, nullptr};
   // metrics queued behind the denoiser, read at the end of the iteration
   double* h_met = nullptr;        // fine-grained pinned [4]
   hipEvent_t ev_met = nullptr;
   int met_pending = 0;
+  // sgv_step_begin/end: one host worker thread runs queued steps
+  std::thread worker;
+  std::mutex wmu;
+  std::condition_variable wcv;
+  std::function<int()> job;
+  int job_state = 0;      // 0 idle, 1 queued, 2 running, 3 done
+  int job_rc = 0;
+  bool worker_quit = false;
   size_t pk_cap = 0;
   // chunk / row-group layouts
   int nch = 0;
@@ -334,29 +354,35 @@ static int h2d(sgv_ctx* c, const void* host, size_t bytes) {
   return stream_wait(c);
 }
 
-// K x Mloc int8 probes -> d_probe, queued on the stream without a host wait
-static int upload_probes(sgv_ctx* c, const int8_t* probes) {
+// K x Mloc int8 probes -> d_probe slot, copied on the copy stream (no host wait);
+// returns the slot.  A slot's device half is consumed by the unpack kernels of
+// its step (ev_unpk) and reused two uploads later.
+static int probe_upload(sgv_ctx* c, const int8_t* probes, int* slot_out) {
   const size_t bytes = std::max<size_t>((size_t)c->K * c->Mloc, 8);
   if (bytes > c->probe_cap) {
     CHK(stream_wait(c));
+    HIPCHK(hipStreamSynchronize(c->st_copy));
     for (int i = 0; i < 2; ++i) {
       if (c->h_probe[i]) HIPCHK(hipHostFree(c->h_probe[i]));
       c->h_probe[i] = nullptr;
       HIPCHK(hipHostMalloc(&c->h_probe[i], bytes));
       if (!c->ev_probe[i]) HIPCHK(hipEventCreateWithFlags(&c->ev_probe[i], hipEventDisableTiming));
+      if (!c->ev_unpk[i]) HIPCHK(hipEventCreateWithFlags(&c->ev_unpk[i], hipEventDisableTiming));
     }
     if (c->d_probe) HIPCHK(hipFree(c->d_probe));
     c->d_probe = nullptr;
-    HIPCHK(hipMalloc(&c->d_probe, bytes));
+    HIPCHK(hipMalloc(&c->d_probe, 2 * bytes));
     c->probe_cap = bytes;
   }
   const int slot = c->probe_slot;
   c->probe_slot ^= 1;
   HIPCHK(hipEventSynchronize(c->ev_probe[slot]));   // this slot's previous copy (long done)
   std::memcpy(c->h_probe[slot], probes, (size_t)c->K * c->Mloc);
-  HIPCHK(hipMemcpyAsync(c->d_probe, c->h_probe[slot], (size_t)c->K * c->Mloc,
-                        hipMemcpyHostToDevice, c->st));
-  HIPCHK(hipEventRecord(c->ev_probe[slot], c->st));
+  HIPCHK(hipStreamWaitEvent(c->st_copy, c->ev_unpk[slot], 0));   // its previous unpack
+  HIPCHK(hipMemcpyAsync(c->d_probe + slot * c->probe_cap, c->h_probe[slot],
+                        (size_t)c->K * c->Mloc, hipMemcpyHostToDevice, c->st_copy));
+  HIPCHK(hipEventRecord(c->ev_probe[slot], c->st_copy));
+  *slot_out = slot;
   return SGV_OK;
 }
 
@@ -976,6 +1002,8 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
     return cleanup(fail(nullptr, SGV_ERR_HIP, "hipEventCreate"));
   if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail(nullptr, SGV_ERR_HIP, "hipStreamCreate"));
+  if (hipStreamCreateWithFlags(&c->st_copy, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(nullptr, SGV_ERR_HIP, "hipStreamCreate"));
 
   // marker layout
   int64_t off = 0, voff = 0;
@@ -1095,6 +1123,15 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
 
 extern "C" void sgv_destroy(sgv_ctx* c) {
   if (!c) return;
+  if (c->worker.joinable()) {
+    {
+      std::unique_lock<std::mutex> lk(c->wmu);
+      c->wcv.wait(lk, [c] { return c->job_state != 1 && c->job_state != 2; });
+      c->worker_quit = true;
+    }
+    c->wcv.notify_all();
+    c->worker.join();
+  }
   (void)hipSetDevice(c->dev);
   if (c->st) (void)hipStreamSynchronize(c->st);
   if (c->comm) (void)ncclCommDestroy(c->comm);
@@ -1148,6 +1185,12 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   }
   for (hipEvent_t e : c->evpool) (void)hipEventDestroy(e);
   if (c->ev_sync) (void)hipEventDestroy(c->ev_sync);
+  if (c->st_copy) (void)hipStreamSynchronize(c->st_copy);
+  for (int i = 0; i < 2; ++i) {
+    if (c->ev_unpk[i]) (void)hipEventDestroy(c->ev_unpk[i]);
+    if (c->ev_pack[i]) (void)hipEventDestroy(c->ev_pack[i]);
+  }
+  if (c->st_copy) (void)hipStreamDestroy(c->st_copy);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
 }
@@ -1630,19 +1673,25 @@ extern "C" int sgv_outputs_begin(sgv_ctx* c, int slot) {
   if (slot < 0 || slot > 1) return fail(c, SGV_ERR_ARG, "slot must be 0 or 1");
   const size_t n = (size_t)std::max<int64_t>(c->Mloc, 1);
   const size_t bytes = sizeof(double) * n * (c->K + 1);
-  if (!c->d_out) {
-    HIPCHK(hipMalloc(&c->d_out, bytes));
+  if (!c->d_out) {   // a device staging half and a pinned buffer per slot
+    HIPCHK(hipMalloc(&c->d_out, 2 * bytes));
     for (int i = 0; i < 2; ++i) {
       HIPCHK(hipHostMalloc(&c->h_out[i], bytes));
       HIPCHK(hipEventCreateWithFlags(&c->ev_out[i], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&c->ev_pack[i], hipEventDisableTiming));
     }
   }
-  HIPCHK(launch_pack(c->d_ch, c->nch, c->d_ch_doff, c->xhat1, c->d_out, c->st));
+  double* dst = c->d_out + (size_t)slot * n * (c->K + 1);
+  HIPCHK(hipStreamWaitEvent(c->st, c->ev_out[slot], 0));   // the slot's previous copy
+  HIPCHK(launch_pack(c->d_ch, c->nch, c->d_ch_doff, c->xhat1, dst, c->st));
   for (int k = 0; k < c->K; ++k)
-    HIPCHK(launch_pack(c->d_ch, c->nch, c->d_ch_doff, c->r1[k], c->d_out + n * (k + 1), c->st));
-  HIPCHK(hipMemcpyAsync(c->h_out[slot], c->d_out, sizeof(double) * n * (c->K + 1),
-                        hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipEventRecord(c->ev_out[slot], c->st));
+    HIPCHK(launch_pack(c->d_ch, c->nch, c->d_ch_doff, c->r1[k], dst + n * (k + 1), c->st));
+  // the copy runs on the copy stream: the ctx stream goes on with the step
+  HIPCHK(hipEventRecord(c->ev_pack[slot], c->st));
+  HIPCHK(hipStreamWaitEvent(c->st_copy, c->ev_pack[slot], 0));
+  HIPCHK(hipMemcpyAsync(c->h_out[slot], dst, sizeof(double) * n * (c->K + 1),
+                        hipMemcpyDeviceToHost, c->st_copy));
+  HIPCHK(hipEventRecord(c->ev_out[slot], c->st_copy));
   return SGV_OK;
 }
 
@@ -1671,11 +1720,16 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
   const double s = c->s;
   int passes = 0;
 
-  // probes u_k (:326), int8 +-1 -> f64
-  CHK(upload_probes(c, probes));
+  // probes u_k (:326), int8 +-1 -> f64; uploaded at the start of sgv_step, or now
+  int ps = c->pref_slot;
+  if (ps < 0 || c->pref_src != probes) CHK(probe_upload(c, probes, &ps));
+  c->pref_slot = -1;
+  c->pref_src = nullptr;
+  HIPCHK(hipStreamWaitEvent(c->st, c->ev_probe[ps], 0));
   for (int k = 0; k < K; ++k)
-    HIPCHK(launch_unpack_i8(c->d_ch, c->nch, c->d_ch_doff, c->d_probe + (size_t)k * c->Mloc,
-                            c->U[k], c->st));
+    HIPCHK(launch_unpack_i8(c->d_ch, c->nch, c->d_ch_doff,
+                            c->d_probe + ps * c->probe_cap + (size_t)k * c->Mloc, c->U[k], c->st));
+  HIPCHK(hipEventRecord(c->ev_unpk[ps], c->st));
 
   // warm start needs R_s x0: carried from the previous iteration (rs_rec), or the
   // previous gamw pass; a pass only when X was set from outside
@@ -2022,4 +2076,106 @@ extern "C" int sgv_sync(sgv_ctx* c) {
   CHK(stream_wait(c));
   resolve_timers(c);
   return SGV_OK;
+}
+
+// ---------------------------------------------------------------------------
+// one outer iteration in the shim (src/sgvamp.py:222-387 minus the files and
+// logs): the host returns to the caller once, not between the phases
+// ---------------------------------------------------------------------------
+extern "C" int sgv_step(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
+                        const double* sigmas, const double* a, double* lam_io, double* omegas_io,
+                        const double* gam1s, double rho, const double* gamw,
+                        const double* alpha1_prev, const double* alpha2_prev,
+                        const int8_t* probes, int cg_maxit, double rtol, int out_slot,
+                        double* res, int* ires, double* out, int* cg_out) {
+  ENTER(c);
+  if (!sigmas || !a || !lam_io || !omegas_io || !gam1s || !gamw || !alpha1_prev ||
+      !alpha2_prev || !probes || !res || !ires || !out || !cg_out || out_slot > 1)
+    return fail(c, SGV_ERR_ARG, "sgv_step: bad arguments");
+  const int K = c->K;
+  res[0] = 0.0;
+  ires[0] = 0;
+  // this step's probes go up now, behind nothing: the copy overlaps EM/denoiser
+  CHK(probe_upload(c, probes, &c->pref_slot));
+  c->pref_src = probes;
+  if (flags & SGV_STEP_EM) {   // :250-257
+    CHK(sgv_em(c, gam1s, a, nslab, sigmas, em_maxit, lam_io, omegas_io, &ires[0], &res[0]));
+  }
+  double der[MAXK];
+  CHK(sgv_denoise(c, gam1s, a, *lam_io, nslab, omegas_io, sigmas, rho,
+                  (flags & SGV_STEP_DENOISE_DAMP) ? 1 : 0, der));   // :270-291
+  if (out_slot >= 0) CHK(sgv_outputs_begin(c, out_slot));           // :281-283 (files)
+  if (flags & SGV_STEP_METRICS) CHK(sgv_metrics_begin(c));          // :379-387
+  double alpha1[MAXK], gam2[MAXK];
+  for (int k = 0; k < K; ++k) {
+    double a1 = der[k] / (double)c->Mtot;                           // np.mean (:285)
+    if (flags & SGV_STEP_ALPHA1_DAMP) a1 = rho * a1 + (1 - rho) * alpha1_prev[k];   // :290-291
+    alpha1[k] = a1;
+    gam2[k] = gam1s[k] * (1 - a1) / a1;                             // :305
+    res[1 + k] = a1;
+    res[1 + K + k] = gam2[k];
+  }
+  int passes = 0;
+  CHK(sgv_lmmse(c, it, gamw, gam2, alpha1, alpha2_prev, probes, cg_maxit, rtol,
+                (flags & SGV_STEP_LMMSE_DAMP) ? 1 : 0, rho, (flags & SGV_STEP_LEARN_GAMW) ? 1 : 0,
+                out, cg_out, &passes));
+  ires[1] = passes;
+  return SGV_OK;
+}
+
+static void worker_main(sgv_ctx* c) {
+  (void)hipSetDevice(c->dev);
+  std::unique_lock<std::mutex> lk(c->wmu);
+  for (;;) {
+    c->wcv.wait(lk, [c] { return c->job_state == 1 || c->worker_quit; });
+    if (c->job_state != 1) return;   // quit
+    c->job_state = 2;
+    std::function<int()> job = std::move(c->job);
+    lk.unlock();
+    const int rc = job();
+    lk.lock();
+    c->job_rc = rc;
+    c->job_state = 3;
+    c->wcv.notify_all();
+  }
+}
+
+extern "C" int sgv_step_begin(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
+                              const double* sigmas, const double* a, double* lam_io,
+                              double* omegas_io, const double* gam1s, double rho,
+                              const double* gamw, const double* alpha1_prev,
+                              const double* alpha2_prev, const int8_t* probes, int cg_maxit,
+                              double rtol, int out_slot, double* res, int* ires, double* out,
+                              int* cg_out) {
+  if (!c) return fail(nullptr, SGV_ERR_ARG, "null context");
+  if (nslab < 1 || nslab > MAXL || !sigmas || !a || !gam1s || !gamw || !alpha1_prev ||
+      !alpha2_prev)
+    return fail(c, SGV_ERR_ARG, "sgv_step_begin: bad arguments");
+  std::unique_lock<std::mutex> lk(c->wmu);
+  if (c->job_state == 1 || c->job_state == 2)
+    return fail(c, SGV_ERR_ARG, "sgv_step_begin: a step is already running");
+  // the K- and L-length inputs are copied; lam/omegas, probes and the outputs
+  // stay the caller's (valid until sgv_step_end)
+  const int K = c->K;
+  std::vector<double> v_sig(sigmas, sigmas + nslab), v_a(a, a + K), v_g1(gam1s, gam1s + K),
+      v_gw(gamw, gamw + K), v_a1(alpha1_prev, alpha1_prev + K), v_a2(alpha2_prev, alpha2_prev + K);
+  c->job = [=]() {
+    return sgv_step(c, it, flags, em_maxit, nslab, v_sig.data(), v_a.data(), lam_io, omegas_io,
+                    v_g1.data(), rho, v_gw.data(), v_a1.data(), v_a2.data(), probes, cg_maxit, rtol,
+                    out_slot, res, ires, out, cg_out);
+  };
+  c->job_state = 1;
+  if (!c->worker.joinable()) c->worker = std::thread(worker_main, c);
+  lk.unlock();
+  c->wcv.notify_all();
+  return SGV_OK;
+}
+
+extern "C" int sgv_step_end(sgv_ctx* c) {
+  if (!c) return fail(nullptr, SGV_ERR_ARG, "null context");
+  std::unique_lock<std::mutex> lk(c->wmu);
+  if (c->job_state == 0) return fail(c, SGV_ERR_ARG, "sgv_step_end without sgv_step_begin");
+  c->wcv.wait(lk, [c] { return c->job_state == 3; });
+  c->job_state = 0;
+  return c->job_rc;
 }

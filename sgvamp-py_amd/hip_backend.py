@@ -17,6 +17,8 @@ SGV_OK = 0
 VEC_R, VEC_R1, VEC_XHAT1, VEC_XHAT2, VEC_SIG2U, VEC_X0 = range(6)
 LMMSE_NOUT = 8
 O_TRSIGMA2, O_ALPHA2, O_GAM1, O_Z, O_TRRSIGMA2, O_GAMW, O_XR, O_XRX = range(8)
+STEP_EM, STEP_DENOISE_DAMP, STEP_ALPHA1_DAMP, STEP_LMMSE_DAMP, STEP_LEARN_GAMW, STEP_METRICS = \
+    1, 2, 4, 8, 16, 32
 MAX_COHORTS = 8
 MAX_SLABS = 8
 
@@ -68,6 +70,15 @@ _SIGS = {
     "sgv_cg_solve": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, _c_dbl_p, _c_dbl_p, _c_dbl_p,
                      ctypes.c_int, ctypes.c_double, _c_int_p, _c_int_p],
     "sgv_timers": [_vp, _c_dbl_p, ctypes.c_int],
+    "sgv_step": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dbl_p, _c_dbl_p,
+                 _c_dbl_p, _c_dbl_p, _c_dbl_p, ctypes.c_double, _c_dbl_p, _c_dbl_p, _c_dbl_p,
+                 _c_i8_p, ctypes.c_int, ctypes.c_double, ctypes.c_int, _c_dbl_p, _c_int_p,
+                 _c_dbl_p, _c_int_p],
+    "sgv_step_begin": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dbl_p,
+                       _c_dbl_p, _c_dbl_p, _c_dbl_p, _c_dbl_p, ctypes.c_double, _c_dbl_p,
+                       _c_dbl_p, _c_dbl_p, _c_i8_p, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                       _c_dbl_p, _c_int_p, _c_dbl_p, _c_int_p],
+    "sgv_step_end": [_vp],
     "sgv_probe_draw": [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32),
                        ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _c_i8_p],
     "sgv_sync": [_vp],

@@ -305,6 +305,7 @@ class VAMP:
         self._csv_rows = []
         self._next_probes = self._submit_probes()
         self._pending_write = None
+        self._last_out = None
         # everything allocated so far (imports, LD upload) lives for the whole run:
         # keep it out of the cyclic collector's scans, whose full passes otherwise
         # stall an iteration for milliseconds at a time
@@ -359,6 +360,11 @@ class VAMP:
         """Wait for every output of the finished iterations: .bin files and CSV rows."""
         self._submit_csv()
         self.flush()
+        last = getattr(self, "_last_out", None)
+        if last is not None:   # step() starts an iteration's writer during the next step
+            self._last_out = None
+            self._pending_write = self._out_pool.submit(self._write_outputs, last, last % 2)
+            self.flush()
         for f in getattr(self, "_csv_futs", []):
             f.result()                    # re-raise a failed append
         self._csv_futs = []
@@ -371,7 +377,137 @@ class VAMP:
                 setattr(self, pool, None)
 
     def step(self, it):
-        """One outer iteration, src/sgvamp.py:222-387."""
+        """One outer iteration, src/sgvamp.py:222-387.  The device phases (EM
+        loop, denoiser, LMMSE) run as one sgv_step on the library's worker
+        thread; meanwhile this thread draws nothing on the GPU's critical path:
+        it submits the next probes, waits for the previous iteration's files and
+        hands the previous CSV rows to their writer.  Logs follow the step in the
+        reference's order."""
+        if os.environ.get("SGV_STEP") == "phases":
+            return self._step_phases(it)
+        st = self._st
+        eng = self.engine
+        K, M, Nt, rho, rank = self.K, self.M, self.Nt, self.rho, self.rank
+        gam1, gamw, alpha1, alpha2 = st["gam1"], st["gamw"], st["alpha1"], st["alpha2"]
+        t_it = time.perf_counter()
+        rec = dict(it=it)
+        # lazy %-arguments: nothing is formatted unless the level is enabled
+        if rank == 0:
+            logging.info("\n -----ITERATION %s -----", it)
+        gam1s = np.array(gam1, dtype=np.float64)                      # :228-233
+        if rank == 0:
+            logging.debug("gam1s=%s", gam1s)
+            logging.info("...Data from all ranks collected")
+
+        flags = 0
+        if it >= st["update_prior_from"]:                             # :242-259
+            if st["prior_update"] == "mle":
+                if rank == 0:
+                    logging.info("...Updating prior parameters using MLE")
+                warn = self.prior_update_mle(gam1s)
+                if warn:
+                    rec["mle_warning"] = warn
+            elif st["prior_update"] == "em":
+                flags |= hb.STEP_EM
+        if it > 0:
+            flags |= hb.STEP_DENOISE_DAMP | hb.STEP_ALPHA1_DAMP       # :275-276, 290-291
+        if st["lmmse_damp"]:
+            flags |= hb.STEP_LMMSE_DAMP
+        if st["learn_gamw"]:
+            flags |= hb.STEP_LEARN_GAMW
+        if self._has_x0:
+            flags |= hb.STEP_METRICS                                  # :379-387
+        t0 = time.perf_counter()
+        u = self._next_probes[0].result()[None] if K == 1 else \
+            np.stack([f.result() for f in self._next_probes])         # :326
+        rec["wait_probes_ms"] = (time.perf_counter() - t0) * 1e3
+        if self.write_files:
+            # pinned slot it % 2 was last read by the writer of it - 2 (started
+            # during the previous step): normally long done
+            t0 = time.perf_counter()
+            self.flush()
+            rec["wait_write_ms"] = (time.perf_counter() - t0) * 1e3
+        h = eng.step_begin(it, flags, st["em_prior_maxit"], self.sigmas, self.a, self.lam,
+                           self.omegas, gam1s, rho, gamw, alpha1, alpha2, u, st["cg_maxit"],
+                           it % 2 if self.write_files else -1)
+        # host work overlapping the step (touches no device state): the next
+        # probes, the previous iteration's files and CSV rows
+        self._next_probes = self._submit_probes()
+        if self.write_files and it > 0 and self._last_out == it - 1:
+            self._pending_write = self._out_pool.submit(self._write_outputs, it - 1, (it - 1) % 2)
+        self._submit_csv()
+        r = eng.step_end(h)
+        if self.write_files:
+            self._last_out = it
+
+        if flags & hb.STEP_EM:
+            self.lam, self.omegas = r["lam"], r["omegas"]
+            rec["em_steps"] = r["em_steps"]
+            if rank == 0:
+                logging.info("...Updating prior parameters using EM")
+                logging.info("... prior-learning EM algorithm performed %s steps "
+                             "and had final relative error = %0.9f", r["em_steps"], r["em_err"])
+        if rank == 0:
+            logging.debug("lam=%s", self.lam)
+            logging.debug("omegas=%s", self.omegas)
+            logging.debug("sigmas=%s", self.sigmas)
+            logging.info("...Denoising")
+        if st["return_xhat"]:
+            xhat_loc = eng.get_vector(hb.VEC_XHAT1)    # LMMSE leaves xhat1 as denoised
+            full = xhat_loc
+            if self.comm.Get_size() > 1:
+                full = np.concatenate(self.comm.allgather(xhat_loc))
+            st["xhat1s"].append(full.reshape((M, 1)))
+        gam2 = r["gam2"]
+        for k in range(K):
+            alpha1[k] = r["alpha1"][k]
+        if rank == 0:
+            logging.debug("[rank = %s] alpha1 = %s", rank, alpha1[0])
+            logging.debug("[rank = %s] gam2 = %s", rank, gam2[0])
+        for k in range(K):
+            logging.info("...LMMSE cohort %s", k)
+        out, cg, passes = r["out"], r["cg"], r["passes"]
+        rec.update(cg_iters=cg[:, [0, 2]].tolist(), cg_info=cg[:, [1, 3]].tolist(),
+                   ld_passes=passes)
+        for k in range(K):
+            if cg[k, 1] > 0:
+                logging.info("Rank %s WARNING: CG 1 convergence after %s "
+                             "iterations not achieved!", k, cg[k, 1])
+            if cg[k, 3] > 0:
+                logging.info("Rank %s WARNING: CG 2 convergence after %s "
+                             "iterations not achieved!", k, cg[k, 3])
+            alpha2[k] = out[k, hb.O_ALPHA2]
+            gam1[k] = out[k, hb.O_GAM1]
+            if st["learn_gamw"]:
+                gamw[k] = float(out[k, hb.O_GAMW])                    # :363-364
+        if rank == 0:
+            logging.debug("[rank = %s] alpha2 = %s", rank, alpha2[0])
+            logging.debug("gamw = %0.9f \n", gamw[0])
+        for k in range(K):
+            st["gamws"][k].append(gamw[k])                            # :373
+            gamw[k] = max(gamw[k], 1.0)                               # :374
+            if rank == 0 and self.write_files:
+                self._queue_csv(self.write_params_to_file,
+                                [it, gamw[k], gam1[k], gam2[k], alpha1[k], alpha2[k],
+                                 self.lam], k)                        # :377
+        if self._has_x0:                                              # :379-387
+            s = eng.metrics_end()
+            alignment = s[0] / np.sqrt(s[1]) / np.sqrt(s[3])
+            l2 = np.sqrt(s[2]) / np.sqrt(s[3])
+            rec["metrics"] = (alignment, l2)
+            if rank == 0:
+                logging.debug("Alignment(xhat1, x0) = %0.9f \n", alignment)
+                logging.debug("L2_error(xhat1, x0) = %0.9f \n", l2)
+                if self.write_files:
+                    self._queue_csv(self.write_metrics_to_file, [it, alignment, l2])
+        rec.update(gamw=list(gamw), gam1=list(gam1), gam2=gam2, alpha1=list(alpha1),
+                   alpha2=list(alpha2), lam=self.lam, wall_s=time.perf_counter() - t_it)
+        self.history.append(rec)
+        return rec
+
+    def _step_phases(self, it):
+        """One outer iteration, src/sgvamp.py:222-387, one host call per phase
+        (SGV_STEP=phases: the A/B reference for step(); same results)."""
         st = self._st
         eng = self.engine
         K, M, Nt, rho, rank = self.K, self.M, self.Nt, self.rho, self.rank

@@ -10,8 +10,8 @@ rc=0
 run() {   # name args...
   local n=$1; shift
   for side in A B; do
-    if [ $side = A ]; then lib=tools/ab/base.so; else lib=; fi
-    SGV_LIB=$lib timeout -k 10 200 python bench.py --cpu-baseline off --out-dir $W/$n$side "$@" \
+    if [ $side = A ]; then lib=${AB_LIB_A-tools/ab/base.so}; stp=${AB_STEP_A:-}; else lib=; stp=; fi
+    SGV_STEP=$stp SGV_LIB=$lib timeout -k 10 200 python bench.py --cpu-baseline off --out-dir $W/$n$side "$@" \
       > gpurun_out/ab_$n$side.log 2>&1 || { echo "[$n$side] bench failed rc=$?"; tail -5 gpurun_out/ab_$n$side.log; exit 3; }
   done
   if diff -r -q $W/${n}A $W/${n}B > /dev/null; then
