@@ -12,6 +12,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -143,9 +145,9 @@ struct sgv_ctx {
   std::mutex wmu;
   std::condition_variable wcv;
   std::function<int()> job;
-  int job_state = 0;      // 0 idle, 1 queued, 2 running, 3 done
+  std::atomic<int> job_state{0};   // 0 idle, 1 queued, 2 running, 3 done
   int job_rc = 0;
-  bool worker_quit = false;
+  std::atomic<bool> worker_quit{false};
   size_t pk_cap = 0;
   // chunk / row-group layouts
   int nch = 0;
@@ -199,6 +201,7 @@ struct sgv_ctx {
   EmState* h_emi = nullptr;
   double* d_emtot = nullptr;
   hipEvent_t ev_em[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_den = nullptr;    // sgv_step: the denoiser's sums are in h_tot
   // timers
   std::vector<hipEvent_t> evpool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
@@ -841,17 +844,23 @@ static int event_spin(sgv_ctx* c, hipEvent_t ev) {
 static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const double* atol,
                        int maxiter, const int* active_in, int* iters, int* info, int* passes) {
   const int ncol = cc.ncol;
-  CgState* hi = c->h_cgi;   // the previous solve's copy has completed (its mirror was read)
-  std::memset(hi, 0, sizeof(CgState));
   unsigned mask = 0;
-  for (int j = 0; j < ncol; ++j) {
-    hi->rho[j] = rho0[j];
-    hi->atol[j] = atol[j];
-    hi->active[j] = active_in[j] ? 1 : 0;
-    if (active_in[j]) mask |= 1u << j;
+  if (rho0) {
+    CgState* hi = c->h_cgi;   // the previous solve's copy has completed (its mirror was read)
+    std::memset(hi, 0, sizeof(CgState));
+    for (int j = 0; j < ncol; ++j) {
+      hi->rho[j] = rho0[j];
+      hi->atol[j] = atol[j];
+      hi->active[j] = active_in[j] ? 1 : 0;
+      if (active_in[j]) mask |= 1u << j;
+    }
+    hi->any = mask ? 1 : 0;
+    HIPCHK(hipMemcpyAsync(c->d_cgs, hi, sizeof(CgState), hipMemcpyHostToDevice, c->st));
+  } else {
+    // state set by k_cg_init on the stream; a |b| == 0 column is inactive there
+    // and rides along unused in the first pass (its result is never read)
+    mask = ncol >= 32 ? ~0u : (1u << ncol) - 1u;
   }
-  hi->any = mask ? 1 : 0;
-  HIPCHK(hipMemcpyAsync(c->d_cgs, hi, sizeof(CgState), hipMemcpyHostToDevice, c->st));
   const volatile CgState* last = nullptr;
   int executed = 0;
   for (int it = 0; it < maxiter; ++it) {
@@ -1106,6 +1115,7 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   CREATE_HIP(hipHostMalloc(&c->h_cgi, sizeof(CgState)));
   for (int i = 0; i < CG_RING; ++i)
     CREATE_HIP(hipEventCreateWithFlags(&c->ev_cg[i], hipEventDisableTiming));
+  CREATE_HIP(hipEventCreateWithFlags(&c->ev_den, hipEventDisableTiming));
   CREATE_HIP(hipMalloc(&c->d_ems, sizeof(EmState)));
   CREATE_HIP(hipMalloc(&c->d_emtot, sizeof(double) * MAXNV));
   CREATE_HIP(hipHostMalloc(&c->h_emm, sizeof(EmState) * CG_RING, hipHostMallocCoherent));
@@ -1124,9 +1134,9 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
 extern "C" void sgv_destroy(sgv_ctx* c) {
   if (!c) return;
   if (c->worker.joinable()) {
+    while (c->job_state.load() == 1 || c->job_state.load() == 2) __builtin_ia32_pause();
     {
-      std::unique_lock<std::mutex> lk(c->wmu);
-      c->wcv.wait(lk, [c] { return c->job_state != 1 && c->job_state != 2; });
+      std::lock_guard<std::mutex> lk(c->wmu);
       c->worker_quit = true;
     }
     c->wcv.notify_all();
@@ -1177,6 +1187,7 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   if (c->h_emi) (void)hipHostFree(c->h_emi);
   for (hipEvent_t e : c->ev_em)
     if (e) (void)hipEventDestroy(e);
+  if (c->ev_den) (void)hipEventDestroy(c->ev_den);
   if (c->d_stage) (void)hipFree(c->d_stage);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   for (auto& pr : c->pending) {
@@ -1488,12 +1499,10 @@ extern "C" int sgv_synth_r(sgv_ctx* c, int k, uint64_t seed, int64_t marker0, in
 // ---------------------------------------------------------------------------
 // denoiser (src/sgvamp.py:93-114, 270-291)
 // ---------------------------------------------------------------------------
-extern "C" int sgv_denoise(sgv_ctx* c, const double* gam1s, const double* a, double lam,
+// denoiser kernel + the ordered reduction of its derivative sums into h_tot[0..K)
+static int denoise_enqueue(sgv_ctx* c, const double* gam1s, const double* a, double lam,
                            int nslab, const double* omegas, const double* sigmas, double rho,
-                           int damp, double* der_sum) {
-  ENTER(c);
-  if (nslab < 1 || nslab > MAXL || !gam1s || !a || !omegas || !sigmas || !der_sum)
-    return fail(c, SGV_ERR_ARG, "sgv_denoise: bad arguments (nslab=%d)", nslab);
+                           int damp) {
   DenoiseArgs da{};
   da.xhat1 = c->xhat1;
   da.K = c->K;
@@ -1515,9 +1524,20 @@ extern "C" int sgv_denoise(sgv_ctx* c, const double* gam1s, const double* a, dou
     da.sq[l] = std::sqrt(da.s2[l] / sigmas[l]);         // np.sqrt(sigma2_meta / sigmas)
   }
   HIPCHK(launch_denoise(c->d_ch, c->nch, da, c->d_part, c->st));
-  double tot[MAXK];
-  CHK(reduce_host(c, MAXK, c->d_ch_begin, tot));
-  for (int k = 0; k < c->K; ++k) der_sum[k] = tot[k];
+  CHK(reduce_dev(c, MAXK, c->d_ch_begin, identity_map(), c->h_tot));
+  return SGV_OK;
+}
+
+extern "C" int sgv_denoise(sgv_ctx* c, const double* gam1s, const double* a, double lam,
+                           int nslab, const double* omegas, const double* sigmas, double rho,
+                           int damp, double* der_sum) {
+  ENTER(c);
+  if (nslab < 1 || nslab > MAXL || !gam1s || !a || !omegas || !sigmas || !der_sum)
+    return fail(c, SGV_ERR_ARG, "sgv_denoise: bad arguments (nslab=%d)", nslab);
+  CHK(denoise_enqueue(c, gam1s, a, lam, nslab, omegas, sigmas, rho, damp));
+  CHK(stream_wait(c));
+  resolve_timers(c);
+  for (int k = 0; k < c->K; ++k) der_sum[k] = c->h_tot[k];
   return SGV_OK;
 }
 
@@ -1778,7 +1798,14 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
   }
   HIPCHK(launch_lmmse_init(c->d_ch, c->nch, ia, c->d_part, c->st));
   double tot[2 * MAXC];
-  CHK(reduce_host(c, 2 * MAXC, c->d_ch_begin, tot));
+  const bool dev_init = c->cg_pipe;   // CG prologue on the device: no host round trip
+  if (dev_init) {
+    CHK(reduce_dev(c, 2 * MAXC, c->d_ch_begin, identity_map(), c->d_tot));
+    HIPCHK(launch_cg_init(c->d_cgs, c->d_tot, rtol, ncol, c->d_ch, c->nch, c->X.data(),
+                          c->RX0.data(), c->st));
+  } else {
+    CHK(reduce_host(c, 2 * MAXC, c->d_ch_begin, tot));
+  }
   // carried: RX0 follows X through the CG; otherwise the gamw pass refreshes it
   std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), c->rs_rec ? 1 : 0);
 
@@ -1799,10 +1826,11 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
       cc.RX[j] = c->RX0[j];
       cc.Y[j] = c->Y[j];
     }
+    active[j] = 1;
+    if (dev_init) continue;                   // k_cg_init
     const double bn = std::sqrt(tot[j]);      // bnrm2 (iterative.py:376)
     atol[j] = std::max(0.0, rtol * bn);
     rhov[j] = tot[MAXC + j];
-    active[j] = 1;
     if (bn == 0.0) {                          // iterative.py:380-381: return b
       HIPCHK(hipMemsetAsync(c->X[j], 0, sizeof(double) * c->Mpad, c->st));
       HIPCHK(hipMemsetAsync(c->RX0[j], 0, sizeof(double) * c->Mpad, c->st));   // R_s 0
@@ -1810,7 +1838,8 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
     }
   }
   cc.s = s;
-  CHK(cg_run(c, cc, rhov, atol, cg_maxit, active, iters, info, &passes));
+  CHK(dev_init ? cg_loop_dev(c, cc, nullptr, nullptr, cg_maxit, active, iters, info, &passes)
+               : cg_run(c, cc, rhov, atol, cg_maxit, active, iters, info, &passes));
 
   // damping, u.Sigma2_u, xhat2.r, x.any() (:322-323, 338, 352)
   PostArgs po{};
@@ -1830,11 +1859,33 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
   }
   HIPCHK(launch_lmmse_post(c->d_ch, c->nch, po, c->d_part, c->st));
   double pt[4 * MAXK + MAXC];
-  CHK(reduce_host(c, 4 * MAXK + MAXC, c->d_ch_begin, pt));
-  for (int j = 0; j < ncol; ++j) c->xnz[j] = pt[2 * MAXK + j] > 0.0;
-
   R1Args ra{};
   ra.K = K;
+  if (dev_init) {
+    // r1 takes alpha2 from the device-reduced Tr(Sigma2): the update is queued
+    // before the host reads the sums (which it computes alpha2 from as well)
+    CHK(reduce_dev(c, 4 * MAXK + MAXC, c->d_ch_begin, identity_map(), c->d_tot));
+    ra.trs = c->d_tot;
+    ra.Mtot = (double)c->Mtot;
+    ra.rho = rho;
+    ra.damp = lmmse_damp;
+    for (int k = 0; k < K; ++k) {
+      ra.X[k] = c->X[2 * k];
+      ra.r2[k] = c->r2[k];
+      ra.r1[k] = c->r1[k];
+      ra.gam2[k] = gam2[k];
+      ra.alpha2_prev[k] = alpha2_prev[k];
+    }
+    HIPCHK(launch_r1_update(c->d_ch, c->nch, ra, c->st));   // :348
+    HIPCHK(launch_copy_f64(c->h_tot, c->d_tot, 4 * MAXK + MAXC, c->st));
+    CHK(stream_wait(c));
+    resolve_timers(c);
+    std::memcpy(pt, c->h_tot, sizeof(pt));
+  } else {
+    CHK(reduce_host(c, 4 * MAXK + MAXC, c->d_ch_begin, pt));
+  }
+  for (int j = 0; j < ncol; ++j) c->xnz[j] = pt[2 * MAXK + j] > 0.0;
+
   for (int k = 0; k < K; ++k) {
     const double TrSigma2 = pt[k];
     double a2 = gam2[k] * TrSigma2 / (double)c->Mtot;              // :340
@@ -1858,7 +1909,7 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
     cg_out[4 * k + 2] = iters[2 * k + 1];
     cg_out[4 * k + 3] = info[2 * k + 1];
   }
-  HIPCHK(launch_r1_update(c->d_ch, c->nch, ra, c->st));   // :348
+  if (!dev_init) HIPCHK(launch_r1_update(c->d_ch, c->nch, ra, c->st));   // :348
 
   if (learn_gamw && c->rs_rec) {  // :350-363 from the carried products: no pass
     for (int k = 0; k < K; ++k) {
@@ -2101,11 +2152,17 @@ extern "C" int sgv_step(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
   if (flags & SGV_STEP_EM) {   // :250-257
     CHK(sgv_em(c, gam1s, a, nslab, sigmas, em_maxit, lam_io, omegas_io, &ires[0], &res[0]));
   }
+  if (nslab < 1 || nslab > MAXL) return fail(c, SGV_ERR_ARG, "sgv_step: nslab=%d", nslab);
+  // denoiser (:270-291); the output copies and metrics (:281-283, 379-387) are
+  // queued behind it before the host waits for the derivative sums
+  CHK(denoise_enqueue(c, gam1s, a, *lam_io, nslab, omegas_io, sigmas, rho,
+                      (flags & SGV_STEP_DENOISE_DAMP) ? 1 : 0));
+  HIPCHK(hipEventRecord(c->ev_den, c->st));
+  if (out_slot >= 0) CHK(sgv_outputs_begin(c, out_slot));
+  if (flags & SGV_STEP_METRICS) CHK(sgv_metrics_begin(c));
+  CHK(event_spin(c, c->ev_den));
   double der[MAXK];
-  CHK(sgv_denoise(c, gam1s, a, *lam_io, nslab, omegas_io, sigmas, rho,
-                  (flags & SGV_STEP_DENOISE_DAMP) ? 1 : 0, der));   // :270-291
-  if (out_slot >= 0) CHK(sgv_outputs_begin(c, out_slot));           // :281-283 (files)
-  if (flags & SGV_STEP_METRICS) CHK(sgv_metrics_begin(c));          // :379-387
+  for (int k = 0; k < K; ++k) der[k] = c->h_tot[k];
   double alpha1[MAXK], gam2[MAXK];
   for (int k = 0; k < K; ++k) {
     double a1 = der[k] / (double)c->Mtot;                           // np.mean (:285)
@@ -2123,20 +2180,25 @@ extern "C" int sgv_step(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
   return SGV_OK;
 }
 
+// Hand-offs spin (a futex wake costs tens of microseconds, the GPU idles for
+// it): the worker spins up to ~2 ms for the next step before it blocks, and
+// sgv_step_end spins for the step it waits on.
 static void worker_main(sgv_ctx* c) {
   (void)hipSetDevice(c->dev);
-  std::unique_lock<std::mutex> lk(c->wmu);
   for (;;) {
-    c->wcv.wait(lk, [c] { return c->job_state == 1 || c->worker_quit; });
-    if (c->job_state != 1) return;   // quit
-    c->job_state = 2;
-    std::function<int()> job = std::move(c->job);
-    lk.unlock();
-    const int rc = job();
-    lk.lock();
+    const auto t0 = std::chrono::steady_clock::now();
+    while (c->job_state.load(std::memory_order_acquire) != 1 && !c->worker_quit.load()) {
+      __builtin_ia32_pause();
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
+        std::unique_lock<std::mutex> lk(c->wmu);
+        c->wcv.wait(lk, [c] { return c->job_state.load() == 1 || c->worker_quit.load(); });
+      }
+    }
+    if (c->job_state.load(std::memory_order_acquire) != 1) return;   // quit
+    c->job_state.store(2);
+    const int rc = c->job();
     c->job_rc = rc;
-    c->job_state = 3;
-    c->wcv.notify_all();
+    c->job_state.store(3, std::memory_order_release);
   }
 }
 
@@ -2151,8 +2213,7 @@ extern "C" int sgv_step_begin(sgv_ctx* c, int it, int flags, int em_maxit, int n
   if (nslab < 1 || nslab > MAXL || !sigmas || !a || !gam1s || !gamw || !alpha1_prev ||
       !alpha2_prev)
     return fail(c, SGV_ERR_ARG, "sgv_step_begin: bad arguments");
-  std::unique_lock<std::mutex> lk(c->wmu);
-  if (c->job_state == 1 || c->job_state == 2)
+  if (c->job_state.load() == 1 || c->job_state.load() == 2)
     return fail(c, SGV_ERR_ARG, "sgv_step_begin: a step is already running");
   // the K- and L-length inputs are copied; lam/omegas, probes and the outputs
   // stay the caller's (valid until sgv_step_end)
@@ -2164,18 +2225,20 @@ extern "C" int sgv_step_begin(sgv_ctx* c, int it, int flags, int em_maxit, int n
                     v_g1.data(), rho, v_gw.data(), v_a1.data(), v_a2.data(), probes, cg_maxit, rtol,
                     out_slot, res, ires, out, cg_out);
   };
-  c->job_state = 1;
+  {
+    std::lock_guard<std::mutex> lk(c->wmu);   // a worker about to block sees the job
+    c->job_state.store(1, std::memory_order_release);
+  }
   if (!c->worker.joinable()) c->worker = std::thread(worker_main, c);
-  lk.unlock();
   c->wcv.notify_all();
   return SGV_OK;
 }
 
 extern "C" int sgv_step_end(sgv_ctx* c) {
   if (!c) return fail(nullptr, SGV_ERR_ARG, "null context");
-  std::unique_lock<std::mutex> lk(c->wmu);
-  if (c->job_state == 0) return fail(c, SGV_ERR_ARG, "sgv_step_end without sgv_step_begin");
-  c->wcv.wait(lk, [c] { return c->job_state == 3; });
-  c->job_state = 0;
+  if (c->job_state.load() == 0) return fail(c, SGV_ERR_ARG, "sgv_step_end without sgv_step_begin");
+  while (c->job_state.load(std::memory_order_acquire) != 3) __builtin_ia32_pause();
+  c->job = nullptr;
+  c->job_state.store(0);
   return c->job_rc;
 }

@@ -366,7 +366,7 @@ struct CgState {
   int info[MAXC];
   int any;
   int it;
-  int pad_[2];
+  int zero[MAXC];          // bnrm2 == 0 at the start: x = b = 0 (iterative.py:380-381)
 };
 // iteration `it` of the CG (iterative.py:397-407): it > 0 first takes rho_new
 // (the r.r reduction of iteration it-1) for the active columns; then the stop
@@ -375,6 +375,13 @@ struct CgState {
 // final_it, :420-422).  The state is also copied to `mirror` (host memory).
 hipError_t launch_cg_ctl(CgState* d_st, CgState* mirror, const double* d_rho_new, int it,
                          int ncol, int final_it, hipStream_t st);
+// the CG prologue's scalars from the device-reduced |b|^2 (tot[c]) and |r0|^2
+// (tot[MAXC + c]) (iterative.py:376-392): rho, atol = max(0, rtol |b|), active
+// unless |b| == 0; then X and R_s X of the |b| == 0 columns are zeroed
+hipError_t launch_cg_init(CgState* d_st, const double* d_tot, double rtol, int ncol,
+                          const ChunkDesc* d_ch, int nch, double* const* X, double* const* RX,
+                          hipStream_t st);
+hipError_t launch_copy_f64(double* dst, const double* src, int n, hipStream_t st);
 
 struct XrArgs {
   double* X[MAXC];
@@ -423,6 +430,12 @@ struct R1Args {
   double* r1[MAXK];
   double alpha2[MAXK];
   int K;
+  // non-null: alpha2 from the device-reduced Tr(Sigma2) trs[k] (:340, 345-346):
+  // alpha2 = gam2 trs / Mtot, damped with alpha2_prev
+  const double* trs;
+  double gam2[MAXK], alpha2_prev[MAXK];
+  double Mtot, rho;
+  int damp;
 };
 hipError_t launch_r1_update(const ChunkDesc* d_ch, int nch, const R1Args& a, hipStream_t st);
 

@@ -498,6 +498,78 @@ __global__ __launch_bounds__(WAVE) void k_cg_ctl(CgState* __restrict__ s, CgStat
   }
 }
 
+__global__ __launch_bounds__(WAVE) void k_cg_init(CgState* __restrict__ s,
+                                                 const double* __restrict__ tot, double rtol,
+                                                 int ncol) {
+  const int j = threadIdx.x;
+  int act = 0;
+  if (j < MAXC) {
+    double rho = 0.0, atol = 0.0;
+    int zero = 0;
+    if (j < ncol) {
+      const double bn = sqrt(tot[j]);        // bnrm2 (iterative.py:376)
+      const double v = rtol * bn;
+      atol = (0.0 < v) ? v : 0.0;            // std::max(0.0, v)
+      rho = tot[MAXC + j];
+      zero = bn == 0.0;
+      act = !zero;
+    }
+    s->rho[j] = rho;
+    s->rho_prev[j] = 0.0;
+    s->beta[j] = 0.0;
+    s->atol[j] = atol;
+    s->active[j] = act;
+    s->iters[j] = 0;
+    s->info[j] = 0;
+    s->zero[j] = zero;
+  }
+  const int any = __any(act) ? 1 : 0;
+  if (j == 0) {
+    s->any = any;
+    s->it = 0;
+  }
+}
+
+struct ZeroCols {
+  double* X[MAXC];
+  double* RX[MAXC];
+};
+// grid (nch, ncol): X[c] = 0 and R_s X[c] = 0 where the state says |b_c| == 0
+__global__ __launch_bounds__(VTHREADS) void k_cg_zero(const ChunkDesc* __restrict__ chs,
+                                                     const CgState* __restrict__ s, ZeroCols z) {
+  const int c = blockIdx.y;
+  if (!s->zero[c]) return;
+  const ChunkDesc ch = chs[blockIdx.x];
+  CHUNK_LOOP(ch) {
+    z.X[c][ch.voff + t] = 0.0;
+    if (z.RX[c]) z.RX[c][ch.voff + t] = 0.0;
+  }
+}
+
+hipError_t launch_cg_init(CgState* d_st, const double* d_tot, double rtol, int ncol,
+                          const ChunkDesc* d_ch, int nch, double* const* X, double* const* RX,
+                          hipStream_t st) {
+  if (ncol < 1 || ncol > MAXC) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_cg_init, dim3(1), dim3(WAVE), 0, st, d_st, d_tot, rtol, ncol);
+  ZeroCols z{};
+  for (int j = 0; j < ncol; ++j) {
+    z.X[j] = X[j];
+    z.RX[j] = RX[j];
+  }
+  hipLaunchKernelGGL(k_cg_zero, dim3(nch, ncol), dim3(VTHREADS), 0, st, d_ch, d_st, z);
+  return hipGetLastError();
+}
+
+__global__ void k_copy_f64(double* dst, const double* __restrict__ src, int n) {
+  const int t = threadIdx.x;
+  if (t < n) dst[t] = src[t];
+}
+hipError_t launch_copy_f64(double* dst, const double* src, int n, hipStream_t st) {
+  if (n < 1 || n > 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_copy_f64, dim3(1), dim3(n), 0, st, dst, src, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_cg_ctl(CgState* d_st, CgState* mirror, const double* d_rho_new, int it, int ncol,
                          int final_it, hipStream_t st) {
   hipLaunchKernelGGL(k_cg_ctl, dim3(1), dim3(WAVE), 0, st, d_st, mirror, d_rho_new, it, ncol,
@@ -602,7 +674,11 @@ __global__ __launch_bounds__(VTHREADS) void k_r1_update(const ChunkDesc* __restr
   const double* __restrict__ X = a.X[k];
   const double* __restrict__ r2 = a.r2[k];
   double* __restrict__ r1 = a.r1[k];
-  const double al = a.alpha2[k];
+  double al = a.alpha2[k];
+  if (a.trs) {   // same expressions as the host's (capi.hip sgv_lmmse)
+    al = a.gam2[k] * a.trs[k] / a.Mtot;                                   // :340
+    if (a.damp) al = a.rho * al + (1 - a.rho) * a.alpha2_prev[k];         // :345-346
+  }
   double vx[MPT], vr[MPT];
 #pragma unroll
   for (int j = 0; j < MPT; ++j) {
