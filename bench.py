@@ -173,7 +173,9 @@ def main():
              out_name="bench", comm=comm, seed=args.seed, write_files=not args.no_files, **flags)
     x0 = beta * np.sqrt(N_list[0])                      # main.py:276-279
     v.attach_engine(eng, x0=x0)
-    v.begin(x0=x0, return_xhat=False, **run)
+    # the warm-up steps queue no step past their last: the timers are reset
+    # between the two loops while no step runs
+    v.begin(x0=x0, return_xhat=False, iterations=args.warmup, **run)
     eng.sync()
     comm.barrier()
     log("[bench] setup (device data generation) %.1f s, M=%d, blocks=%d x %d, N=%d, K=%d, ranks=%d"
@@ -186,6 +188,7 @@ def main():
                                                               rec["wall_s"] * 1e3))
     eng.timers(reset=True)
     eng.sync()
+    v.set_iterations(args.warmup + args.steps)
     comm.barrier()
     t0 = time.perf_counter()
     recs = []

@@ -171,29 +171,35 @@ int sgv_probe_draw(uint32_t* key, int32_t* pos, int64_t n, int64_t lo, int64_t h
  *   flags & SGV_STEP_EM:  sgv_em (lam_io, omegas_io updated; ires[0] = steps,
  *                         res[0] = final error);
  *   sgv_denoise (damping iff SGV_STEP_DENOISE_DAMP);
- *   out_slot 0/1:        sgv_outputs_begin(out_slot) (xhat1, r1 for the files);
- *   SGV_STEP_METRICS:    sgv_metrics_begin (read with sgv_metrics_end);
+ *   out_slot 0/1/2:      sgv_outputs_begin(out_slot) (xhat1, r1 for the files);
+ *   SGV_STEP_METRICS:    the metric sums of xhat1 (:381-382) in res[1 + 2K .. + 4);
  *   alpha1 = der_sum / M_total, damped with alpha1_prev iff SGV_STEP_ALPHA1_DAMP
  *   (:285-291), gam2 = gam1 (1 - alpha1) / alpha1 (:305): res[1 + k], res[1 + K + k];
  *   sgv_lmmse (damping iff SGV_STEP_LMMSE_DAMP, gamw learning iff
  *   SGV_STEP_LEARN_GAMW): out, cg_out as sgv_lmmse; ires[1] = LD passes.
- * res holds 1 + 2K doubles, ires 2 ints. */
+ * res holds 1 + 2K + 4 doubles, ires 2 ints.
+ * SGV_STEP_CHAIN (sgv_step_begin only): gam1s, gamw (clamped to >= 1, :374),
+ * alpha1_prev, alpha2_prev, *lam_io and omegas_io are taken, when the step
+ * starts, from the results of the step queued before it -- so a step can be
+ * queued while the previous one runs. */
 #define SGV_STEP_EM 1
 #define SGV_STEP_DENOISE_DAMP 2
 #define SGV_STEP_ALPHA1_DAMP 4
 #define SGV_STEP_LMMSE_DAMP 8
 #define SGV_STEP_LEARN_GAMW 16
 #define SGV_STEP_METRICS 32
+#define SGV_STEP_CHAIN 64
 int sgv_step(sgv_ctx* ctx, int it, int flags, int em_maxit, int nslab, const double* sigmas,
              const double* a, double* lam_io, double* omegas_io, const double* gam1s,
              double rho, const double* gamw, const double* alpha1_prev,
              const double* alpha2_prev, const int8_t* probes, int cg_maxit, double rtol,
              int out_slot, double* res, int* ires, double* out, int* cg_out);
-/* sgv_step on the context's host worker thread: returns at once; the caller may
- * run host work (files, logs, the next probes) that does not touch the context
- * (sgv_outputs_wait excepted) until sgv_step_end, which waits and returns
- * sgv_step's status.  lam_io, omegas_io, probes and the outputs must stay valid
- * until then; the other arrays are copied. */
+/* sgv_step on the context's host worker thread: returns at once; at most two
+ * steps are queued and they run in order.  The caller may run host work
+ * (files, logs, the next probes) that does not touch the context
+ * (sgv_outputs_wait excepted) until sgv_step_end, which waits for the oldest
+ * queued step and returns its status.  lam_io, omegas_io, probes and the
+ * outputs must stay valid until then; the other arrays are copied. */
 int sgv_step_begin(sgv_ctx* ctx, int it, int flags, int em_maxit, int nslab,
                    const double* sigmas, const double* a, double* lam_io, double* omegas_io,
                    const double* gam1s, double rho, const double* gamw,
@@ -246,7 +252,7 @@ int sgv_mle_terms(sgv_ctx* ctx, const double* a /* K */, const double* gam1s /* 
 
 /* The per-iteration output vectors without a host wait (src/sgvamp.py:281,283):
  * sgv_outputs_begin queues this rank's slices of xhat1 and r1[0..K-1] (unscaled,
- * marker order) into pinned slot 0 or 1; sgv_outputs_wait -- callable from a
+ * marker order) into pinned slot 0, 1 or 2; sgv_outputs_wait -- callable from a
  * writer thread -- waits for that copy and returns the slot's buffer
  * [(K + 1) x M_local] doubles, valid until the slot is begun again. */
 int sgv_outputs_begin(sgv_ctx* ctx, int slot);

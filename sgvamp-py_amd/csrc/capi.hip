@@ -89,6 +89,7 @@ static int cg_pipe_default() {
   return (e && e[0] == '0') ? 0 : 1;
 }
 constexpr int CG_RING = 4;   // mirror slots of the pipelined CG
+constexpr int NOUT_SLOTS = 3;   // pinned output slots (a writer reads one while two steps run)
 
 static int sym_class_nc(int cls) { return std::min(16, 2 << (cls + 1)); }   // widest NC using cls
 
@@ -119,8 +120,8 @@ struct sgv_ctx {
   // asynchronous per-iteration outputs (xhat1, r1[k]): device pack buffer and two
   // pinned host slots, each with its completion event (sgv_outputs_begin/wait)
   double* d_out = nullptr;
-  double* h_out[2] = {nullptr, nullptr};
-  hipEvent_t ev_out[2] = {nullptr, nullptr};
+  double* h_out[NOUT_SLOTS] = {};
+  hipEvent_t ev_out[NOUT_SLOTS] = {};
   // probe upload: two pinned slots used alternately, stream-ordered copy into
   // d_probe (no host wait; a slot is reused two iterations later)
   int8_t* h_probe[2] = {nullptr, nullptr};
@@ -135,7 +136,7 @@ struct sgv_ctx {
   // DMA copy queued on the ctx stream stalls the kernels behind it for its
   // start-up latency (~50-110 us measured per copy)
   hipStream_t st_copy = nullptr;
-  hipEvent_t ev_pack[2] = {nullptr, nullptr};
+  hipEvent_t ev_pack[NOUT_SLOTS] = {};
   // metrics queued behind the denoiser, read at the end of the iteration
   double* h_met = nullptr;        // fine-grained pinned [4]
   hipEvent_t ev_met = nullptr;
@@ -144,10 +145,19 @@ struct sgv_ctx {
   std::thread worker;
   std::mutex wmu;
   std::condition_variable wcv;
-  std::function<int()> job;
-  std::atomic<int> job_state{0};   // 0 idle, 1 queued, 2 running, 3 done
-  int job_rc = 0;
+  struct Job {
+    std::function<int()> fn;
+    std::atomic<int> state{0};   // 0 free, 1 queued, 2 running, 3 done
+    int rc = 0;
+  };
+  Job jobs[2];                   // at most two steps in flight, run in order
+  uint64_t job_begun = 0, job_ended = 0, job_run = 0;
   std::atomic<bool> worker_quit{false};
+  // the last completed sgv_step's results, the inputs of a chained step
+  struct Chain {
+    int valid = 0;
+    double gam1[MAXK], gamw[MAXK], alpha1[MAXK], alpha2[MAXK], lam, om[MAXL];
+  } chain;
   size_t pk_cap = 0;
   // chunk / row-group layouts
   int nch = 0;
@@ -1134,7 +1144,8 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
 extern "C" void sgv_destroy(sgv_ctx* c) {
   if (!c) return;
   if (c->worker.joinable()) {
-    while (c->job_state.load() == 1 || c->job_state.load() == 2) __builtin_ia32_pause();
+    for (auto& j : c->jobs)
+      while (j.state.load() == 1 || j.state.load() == 2) __builtin_ia32_pause();
     {
       std::lock_guard<std::mutex> lk(c->wmu);
       c->worker_quit = true;
@@ -1155,8 +1166,7 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   if (c->d_pk) (void)hipFree(c->d_pk);
   if (c->d_out) (void)hipFree(c->d_out);
   for (int i = 0; i < 2; ++i) {
-    if (c->h_out[i]) (void)hipHostFree(c->h_out[i]);
-    if (c->ev_out[i]) (void)hipEventDestroy(c->ev_out[i]);
+
     if (c->h_probe[i]) (void)hipHostFree(c->h_probe[i]);
     if (c->ev_probe[i]) (void)hipEventDestroy(c->ev_probe[i]);
   }
@@ -1199,6 +1209,11 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   if (c->st_copy) (void)hipStreamSynchronize(c->st_copy);
   for (int i = 0; i < 2; ++i) {
     if (c->ev_unpk[i]) (void)hipEventDestroy(c->ev_unpk[i]);
+
+  }
+  for (int i = 0; i < NOUT_SLOTS; ++i) {
+    if (c->h_out[i]) (void)hipHostFree(c->h_out[i]);
+    if (c->ev_out[i]) (void)hipEventDestroy(c->ev_out[i]);
     if (c->ev_pack[i]) (void)hipEventDestroy(c->ev_pack[i]);
   }
   if (c->st_copy) (void)hipStreamDestroy(c->st_copy);
@@ -1690,12 +1705,12 @@ extern "C" int sgv_mle_terms(sgv_ctx* c, const double* a, const double* gam1s, i
 // ---------------------------------------------------------------------------
 extern "C" int sgv_outputs_begin(sgv_ctx* c, int slot) {
   ENTER(c);
-  if (slot < 0 || slot > 1) return fail(c, SGV_ERR_ARG, "slot must be 0 or 1");
+  if (slot < 0 || slot >= NOUT_SLOTS) return fail(c, SGV_ERR_ARG, "slot must be 0, 1 or 2");
   const size_t n = (size_t)std::max<int64_t>(c->Mloc, 1);
   const size_t bytes = sizeof(double) * n * (c->K + 1);
   if (!c->d_out) {   // a device staging half and a pinned buffer per slot
-    HIPCHK(hipMalloc(&c->d_out, 2 * bytes));
-    for (int i = 0; i < 2; ++i) {
+    HIPCHK(hipMalloc(&c->d_out, NOUT_SLOTS * bytes));
+    for (int i = 0; i < NOUT_SLOTS; ++i) {
       HIPCHK(hipHostMalloc(&c->h_out[i], bytes));
       HIPCHK(hipEventCreateWithFlags(&c->ev_out[i], hipEventDisableTiming));
       HIPCHK(hipEventCreateWithFlags(&c->ev_pack[i], hipEventDisableTiming));
@@ -1719,7 +1734,7 @@ extern "C" int sgv_outputs_begin(sgv_ctx* c, int slot) {
 // only waits on the slot's event and returns the pinned buffer (valid until the
 // slot's next sgv_outputs_begin).
 extern "C" int sgv_outputs_wait(sgv_ctx* c, int slot, double** data) {
-  if (!c || slot < 0 || slot > 1 || !data || !c->ev_out[slot]) return SGV_ERR_ARG;
+  if (!c || slot < 0 || slot >= NOUT_SLOTS || !data || !c->ev_out[slot]) return SGV_ERR_ARG;
   if (hipSetDevice(c->dev) != hipSuccess) return SGV_ERR_HIP;
   hipError_t e;
   while ((e = hipEventQuery(c->ev_out[slot])) == hipErrorNotReady) __builtin_ia32_pause();
@@ -2141,7 +2156,7 @@ extern "C" int sgv_step(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
                         double* res, int* ires, double* out, int* cg_out) {
   ENTER(c);
   if (!sigmas || !a || !lam_io || !omegas_io || !gam1s || !gamw || !alpha1_prev ||
-      !alpha2_prev || !probes || !res || !ires || !out || !cg_out || out_slot > 1)
+      !alpha2_prev || !probes || !res || !ires || !out || !cg_out || out_slot >= NOUT_SLOTS)
     return fail(c, SGV_ERR_ARG, "sgv_step: bad arguments");
   const int K = c->K;
   res[0] = 0.0;
@@ -2177,28 +2192,44 @@ extern "C" int sgv_step(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
                 (flags & SGV_STEP_LMMSE_DAMP) ? 1 : 0, rho, (flags & SGV_STEP_LEARN_GAMW) ? 1 : 0,
                 out, cg_out, &passes));
   ires[1] = passes;
+  if (flags & SGV_STEP_METRICS) CHK(sgv_metrics_end(c, res + 1 + 2 * K));   // long done
+  // inputs of a chained next step: src/sgvamp.py:347, 363-374 (gamw clamped to
+  // >= 1 after it is logged, as Python's max(gamw, 1.0))
+  sgv_ctx::Chain& ch = c->chain;
+  for (int k = 0; k < K; ++k) {
+    const double* o = out + (size_t)k * SGV_LMMSE_NOUT;
+    ch.gam1[k] = o[SGV_O_GAM1];
+    const double gw = (flags & SGV_STEP_LEARN_GAMW) ? o[SGV_O_GAMW] : gamw[k];
+    ch.gamw[k] = (1.0 > gw) ? 1.0 : gw;
+    ch.alpha1[k] = alpha1[k];
+    ch.alpha2[k] = o[SGV_O_ALPHA2];
+  }
+  ch.lam = *lam_io;
+  for (int l = 0; l < nslab; ++l) ch.om[l] = omegas_io[l];
+  ch.valid = 1;
   return SGV_OK;
 }
 
 // Hand-offs spin (a futex wake costs tens of microseconds, the GPU idles for
 // it): the worker spins up to ~2 ms for the next step before it blocks, and
-// sgv_step_end spins for the step it waits on.
+// sgv_step_end spins for the step it waits on.  Steps run in begin order.
 static void worker_main(sgv_ctx* c) {
   (void)hipSetDevice(c->dev);
   for (;;) {
+    sgv_ctx::Job& j = c->jobs[c->job_run % 2];
     const auto t0 = std::chrono::steady_clock::now();
-    while (c->job_state.load(std::memory_order_acquire) != 1 && !c->worker_quit.load()) {
+    while (j.state.load(std::memory_order_acquire) != 1 && !c->worker_quit.load()) {
       __builtin_ia32_pause();
       if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) {
         std::unique_lock<std::mutex> lk(c->wmu);
-        c->wcv.wait(lk, [c] { return c->job_state.load() == 1 || c->worker_quit.load(); });
+        c->wcv.wait(lk, [&] { return j.state.load() == 1 || c->worker_quit.load(); });
       }
     }
-    if (c->job_state.load(std::memory_order_acquire) != 1) return;   // quit
-    c->job_state.store(2);
-    const int rc = c->job();
-    c->job_rc = rc;
-    c->job_state.store(3, std::memory_order_release);
+    if (j.state.load(std::memory_order_acquire) != 1) return;   // quit
+    j.state.store(2);
+    j.rc = j.fn();
+    ++c->job_run;
+    j.state.store(3, std::memory_order_release);
   }
 }
 
@@ -2211,24 +2242,38 @@ extern "C" int sgv_step_begin(sgv_ctx* c, int it, int flags, int em_maxit, int n
                               int* cg_out) {
   if (!c) return fail(nullptr, SGV_ERR_ARG, "null context");
   if (nslab < 1 || nslab > MAXL || !sigmas || !a || !gam1s || !gamw || !alpha1_prev ||
-      !alpha2_prev)
+      !alpha2_prev || !lam_io || !omegas_io)
     return fail(c, SGV_ERR_ARG, "sgv_step_begin: bad arguments");
-  if (c->job_state.load() == 1 || c->job_state.load() == 2)
-    return fail(c, SGV_ERR_ARG, "sgv_step_begin: a step is already running");
-  // the K- and L-length inputs are copied; lam/omegas, probes and the outputs
-  // stay the caller's (valid until sgv_step_end)
+  sgv_ctx::Job& j = c->jobs[c->job_begun % 2];
+  if (j.state.load() != 0) return fail(c, SGV_ERR_ARG, "sgv_step_begin: two steps already queued");
+  // the K- and L-length inputs are copied (a chained step takes gam1, gamw,
+  // alpha1, alpha2, lam and omegas from the step before it when it starts);
+  // lam_io/omegas_io, probes and the outputs stay the caller's until sgv_step_end
   const int K = c->K;
   std::vector<double> v_sig(sigmas, sigmas + nslab), v_a(a, a + K), v_g1(gam1s, gam1s + K),
       v_gw(gamw, gamw + K), v_a1(alpha1_prev, alpha1_prev + K), v_a2(alpha2_prev, alpha2_prev + K);
-  c->job = [=]() {
-    return sgv_step(c, it, flags, em_maxit, nslab, v_sig.data(), v_a.data(), lam_io, omegas_io,
-                    v_g1.data(), rho, v_gw.data(), v_a1.data(), v_a2.data(), probes, cg_maxit, rtol,
-                    out_slot, res, ires, out, cg_out);
+  j.fn = [=]() mutable {
+    if (flags & SGV_STEP_CHAIN) {
+      const sgv_ctx::Chain& ch = c->chain;
+      if (!ch.valid) return fail(c, SGV_ERR_ARG, "chained step without a completed step");
+      for (int k = 0; k < K; ++k) {
+        v_g1[k] = ch.gam1[k];
+        v_gw[k] = ch.gamw[k];
+        v_a1[k] = ch.alpha1[k];
+        v_a2[k] = ch.alpha2[k];
+      }
+      *lam_io = ch.lam;
+      for (int l = 0; l < nslab; ++l) omegas_io[l] = ch.om[l];
+    }
+    return sgv_step(c, it, flags & ~SGV_STEP_CHAIN, em_maxit, nslab, v_sig.data(), v_a.data(),
+                    lam_io, omegas_io, v_g1.data(), rho, v_gw.data(), v_a1.data(), v_a2.data(),
+                    probes, cg_maxit, rtol, out_slot, res, ires, out, cg_out);
   };
   {
     std::lock_guard<std::mutex> lk(c->wmu);   // a worker about to block sees the job
-    c->job_state.store(1, std::memory_order_release);
+    j.state.store(1, std::memory_order_release);
   }
+  ++c->job_begun;
   if (!c->worker.joinable()) c->worker = std::thread(worker_main, c);
   c->wcv.notify_all();
   return SGV_OK;
@@ -2236,9 +2281,12 @@ extern "C" int sgv_step_begin(sgv_ctx* c, int it, int flags, int em_maxit, int n
 
 extern "C" int sgv_step_end(sgv_ctx* c) {
   if (!c) return fail(nullptr, SGV_ERR_ARG, "null context");
-  if (c->job_state.load() == 0) return fail(c, SGV_ERR_ARG, "sgv_step_end without sgv_step_begin");
-  while (c->job_state.load(std::memory_order_acquire) != 3) __builtin_ia32_pause();
-  c->job = nullptr;
-  c->job_state.store(0);
-  return c->job_rc;
+  if (c->job_ended == c->job_begun) return fail(c, SGV_ERR_ARG, "sgv_step_end without sgv_step_begin");
+  sgv_ctx::Job& j = c->jobs[c->job_ended % 2];
+  while (j.state.load(std::memory_order_acquire) != 3) __builtin_ia32_pause();
+  const int rc = j.rc;
+  j.fn = nullptr;
+  j.state.store(0);
+  ++c->job_ended;
+  return rc;
 }

@@ -195,7 +195,8 @@ class Engine:
                    alpha1_prev, alpha2_prev, probes_local, cg_maxit, out_slot, rtol=1e-5):
         """One outer iteration (sgv_step) on the library's worker thread; returns a
         handle for step_end.  Until then only host work that does not touch the
-        context may run (outputs_wait excepted)."""
+        context may run (outputs_wait excepted).  With hb.STEP_CHAIN in flags the
+        scalar inputs come from the step queued before this one."""
         K = self.K
         sg = hb.f64(sigmas)
         pr = np.ascontiguousarray(probes_local, dtype=np.int8)
@@ -203,7 +204,7 @@ class Engine:
             raise ValueError("probes must be (K, Mloc) int8")
         h = dict(lam=np.array([lam], dtype=np.float64),
                  om=np.array(omegas, dtype=np.float64).copy(),
-                 pr=pr, res=np.zeros(1 + 2 * K), ires=np.zeros(2, dtype=np.int32),
+                 pr=pr, res=np.zeros(1 + 2 * K + 4), ires=np.zeros(2, dtype=np.int32),
                  out=np.zeros((K, hb.LMMSE_NOUT)), cg=np.zeros((K, 4), dtype=np.int32))
         self.ctx.sgv_step_begin(int(it), int(flags), int(em_maxit), len(sg), hb.dptr(sg),
                                 hb.dptr(hb.f64(a)), hb.dptr(h["lam"]), hb.dptr(h["om"]),
@@ -215,14 +216,14 @@ class Engine:
         return h
 
     def step_end(self, h):
-        """Wait for the step; returns dict(lam, omegas, em_steps, em_err, alpha1,
-        gam2, out, cg, passes) (see sgv_step)."""
+        """Wait for the oldest queued step; returns dict(lam, omegas, em_steps,
+        em_err, alpha1, gam2, metrics, out, cg, passes) (see sgv_step)."""
         self.ctx.sgv_step_end()
         K = self.K
         return dict(lam=float(h["lam"][0]), omegas=h["om"], em_steps=int(h["ires"][0]),
                     em_err=float(h["res"][0]), alpha1=h["res"][1:1 + K].tolist(),
-                    gam2=h["res"][1 + K:1 + 2 * K].tolist(), out=h["out"], cg=h["cg"],
-                    passes=int(h["ires"][1]))
+                    gam2=h["res"][1 + K:1 + 2 * K].tolist(), metrics=h["res"][1 + 2 * K:],
+                    out=h["out"], cg=h["cg"], passes=int(h["ires"][1]))
 
     def metrics(self):
         out = np.zeros(4)

@@ -17,8 +17,9 @@ SGV_OK = 0
 VEC_R, VEC_R1, VEC_XHAT1, VEC_XHAT2, VEC_SIG2U, VEC_X0 = range(6)
 LMMSE_NOUT = 8
 O_TRSIGMA2, O_ALPHA2, O_GAM1, O_Z, O_TRRSIGMA2, O_GAMW, O_XR, O_XRX = range(8)
-STEP_EM, STEP_DENOISE_DAMP, STEP_ALPHA1_DAMP, STEP_LMMSE_DAMP, STEP_LEARN_GAMW, STEP_METRICS = \
-    1, 2, 4, 8, 16, 32
+STEP_EM, STEP_DENOISE_DAMP, STEP_ALPHA1_DAMP, STEP_LMMSE_DAMP, STEP_LEARN_GAMW, STEP_METRICS, \
+    STEP_CHAIN = 1, 2, 4, 8, 16, 32, 64
+OUT_SLOTS = 3
 MAX_COHORTS = 8
 MAX_SLABS = 8
 

@@ -266,7 +266,8 @@ class VAMP:
               lmmse_damp=True, prior_update=None, update_prior_from=1, return_xhat=True):
         self.begin(R, r, x0, cg_maxit=cg_maxit, em_prior_maxit=em_prior_maxit,
                    learn_gamw=learn_gamw, lmmse_damp=lmmse_damp, prior_update=prior_update,
-                   update_prior_from=update_prior_from, return_xhat=return_xhat)
+                   update_prior_from=update_prior_from, return_xhat=return_xhat,
+                   iterations=iterations)
         for it in range(iterations):
             self.step(it)
         self.finish()
@@ -274,9 +275,16 @@ class VAMP:
         return self._st["xhat1s"]
 
     def begin(self, R=None, r=None, x0=None, cg_maxit=500, em_prior_maxit=100, learn_gamw=True,
-              lmmse_damp=True, prior_update=None, update_prior_from=1, return_xhat=True):
+              lmmse_damp=True, prior_update=None, update_prior_from=1, return_xhat=True,
+              iterations=None):
         """Initialisation of src/sgvamp.py:198-220 (uploads R, r, x0 unless an
-        engine was attached)."""
+        engine was attached).  `iterations`: the number of step() calls that will
+        follow (0, 1, ...); when known, step(it) queues step it + 1 behind it."""
+        self._n_iter = iterations
+        self._queued = None
+        self._xhat_loc = {}        # iteration -> local xhat1 (return_xhat with files)
+        self._writes = []          # (iteration, future) of the output-file writers
+        self._unwritten = []       # finished iterations whose files are not started
         if self.engine is None:
             self._setup(R, r, x0)
             self._has_x0 = x0 is not None
@@ -305,7 +313,6 @@ class VAMP:
         self._csv_rows = []
         self._next_probes = self._submit_probes()
         self._pending_write = None
-        self._last_out = None
         # everything allocated so far (imports, LD upload) lives for the whole run:
         # keep it out of the cyclic collector's scans, whose full passes otherwise
         # stall an iteration for milliseconds at a time
@@ -329,6 +336,8 @@ class VAMP:
         sgv_outputs_begin, then write xhat1 and every r1, one file per task."""
         Nt = self.Nt
         out = self.engine.outputs_wait(slot)
+        if self._st["return_xhat"] and not os.environ.get("SGV_STEP") == "phases":
+            self._xhat_loc[it] = out[0].copy()   # gathered in order by drain()
         futs = [self._write_pool.submit(lambda: self.write_xhat_to_file(
             it, out[0] / np.sqrt(Nt)))]                                              # :281
         for k in range(self.K):
@@ -342,6 +351,11 @@ class VAMP:
         if getattr(self, "_pending_write", None) is not None:
             self._pending_write.result()
             self._pending_write = None
+        if getattr(self, "_unwritten", None):
+            self._submit_writers()
+        for _, f in getattr(self, "_writes", []):
+            f.result()
+        self._writes = []
 
     def _queue_csv(self, fn, *args):
         if getattr(self, "_csv_pool", None) is None:
@@ -353,18 +367,30 @@ class VAMP:
         if not getattr(self, "_csv_rows", None):
             return
         rows, self._csv_rows = self._csv_rows, []
-        self._csv_futs = [f for f in self._csv_futs if not f.done() or f.result() is not None]
+        keep = []
+        for f in self._csv_futs:   # finished appends: re-raise a failure, then drop
+            if f.done():
+                f.result()
+            else:
+                keep.append(f)
+        self._csv_futs = keep
         self._csv_futs.append(self._csv_pool.submit(lambda: [fn(*a) for fn, a in rows]))
 
     def drain(self):
         """Wait for every output of the finished iterations: .bin files and CSV rows."""
+        if getattr(self, "_queued", None) is not None:   # a step queued past the last call
+            self.engine.step_end(self._queued["h"])
+            self._queued = None
         self._submit_csv()
         self.flush()
-        last = getattr(self, "_last_out", None)
-        if last is not None:   # step() starts an iteration's writer during the next step
-            self._last_out = None
-            self._pending_write = self._out_pool.submit(self._write_outputs, last, last % 2)
-            self.flush()
+        xl = getattr(self, "_xhat_loc", None)
+        if xl:                         # return_xhat with files: xhat1 of every iteration
+            for it in sorted(xl):
+                full = xl[it]
+                if self.comm.Get_size() > 1:
+                    full = np.concatenate(self.comm.allgather(full))
+                self._st["xhat1s"].append(full.reshape((self.M, 1)))
+            xl.clear()
         for f in getattr(self, "_csv_futs", []):
             f.result()                    # re-raise a failed append
         self._csv_futs = []
@@ -376,13 +402,87 @@ class VAMP:
                 getattr(self, pool).shutdown(wait=True)
                 setattr(self, pool, None)
 
+    def set_iterations(self, iterations):
+        """Change the iteration horizon (see begin); call between steps."""
+        self._n_iter = iterations
+
+    def _flags(self, it, gam1s, rec):
+        """sgv_step flags of iteration it; runs the MLE prior update (host fsolve on
+        device sums, src/sgvamp.py:244-247) when it is due."""
+        st = self._st
+        flags = 0
+        if it >= st["update_prior_from"]:                             # :242-259
+            if st["prior_update"] == "mle":
+                if self.rank == 0:
+                    logging.info("...Updating prior parameters using MLE")
+                warn = self.prior_update_mle(gam1s)
+                if warn:
+                    rec["mle_warning"] = warn
+            elif st["prior_update"] == "em":
+                flags |= hb.STEP_EM
+        if it > 0:
+            flags |= hb.STEP_DENOISE_DAMP | hb.STEP_ALPHA1_DAMP       # :275-276, 290-291
+        if st["lmmse_damp"]:
+            flags |= hb.STEP_LMMSE_DAMP
+        if st["learn_gamw"]:
+            flags |= hb.STEP_LEARN_GAMW
+        if self._has_x0:
+            flags |= hb.STEP_METRICS                                  # :379-387
+        return flags
+
+    def _take_probes(self, rec):
+        """This step's probes (drawn in the background, stream order); the next
+        step's draws are submitted."""
+        t0 = time.perf_counter()
+        fs = self._next_probes
+        u = fs[0].result()[None] if self.K == 1 else np.stack([f.result() for f in fs])   # :326
+        rec["wait_probes_ms"] = (time.perf_counter() - t0) * 1e3
+        self._next_probes = self._submit_probes()
+        return u
+
+    def _flush_until(self, last, rec=None):
+        """Wait for the file writers of iterations <= last (their pinned output
+        slot is reused by iteration last + OUT_SLOTS)."""
+        t0 = time.perf_counter()
+        keep = []
+        for i, f in self._writes:
+            if i <= last:
+                f.result()
+            else:
+                keep.append((i, f))
+        self._writes = keep
+        if rec is not None:
+            rec["wait_write_ms"] = rec.get("wait_write_ms", 0.0) + (time.perf_counter() - t0) * 1e3
+
+    def _submit_writers(self):
+        for i in self._unwritten:
+            self._writes.append((i, self._out_pool.submit(self._write_outputs, i,
+                                                          i % hb.OUT_SLOTS)))
+        self._unwritten = []
+
+    def _can_chain(self, nxt):
+        st = self._st
+        return (self._n_iter is not None and nxt < self._n_iter
+                and not (st["return_xhat"] and not self.write_files)
+                and not (st["prior_update"] == "mle" and nxt >= st["update_prior_from"])
+                and os.environ.get("SGV_STEP") != "nochain")
+
+    def _begin_step(self, it, flags, u, chain):
+        st = self._st
+        return self.engine.step_begin(
+            it, flags | (hb.STEP_CHAIN if chain else 0), st["em_prior_maxit"], self.sigmas,
+            self.a, self.lam, self.omegas, np.array(st["gam1"], dtype=np.float64), self.rho,
+            st["gamw"], st["alpha1"], st["alpha2"], u, st["cg_maxit"],
+            it % hb.OUT_SLOTS if self.write_files else -1)
+
     def step(self, it):
         """One outer iteration, src/sgvamp.py:222-387.  The device phases (EM
         loop, denoiser, LMMSE) run as one sgv_step on the library's worker
-        thread; meanwhile this thread draws nothing on the GPU's critical path:
-        it submits the next probes, waits for the previous iteration's files and
-        hands the previous CSV rows to their writer.  Logs follow the step in the
-        reference's order."""
+        thread.  While it runs this thread queues the next iteration's step behind
+        it (sgv_step's inputs chained from this one's results, when the iteration
+        count is known), starts the file writers of finished iterations and hands
+        the CSV rows to their writer -- so the GPU does not wait for Python
+        between iterations.  Logs follow the step in the reference's order."""
         if os.environ.get("SGV_STEP") == "phases":
             return self._step_phases(it)
         st = self._st
@@ -399,46 +499,33 @@ class VAMP:
             logging.debug("gam1s=%s", gam1s)
             logging.info("...Data from all ranks collected")
 
-        flags = 0
-        if it >= st["update_prior_from"]:                             # :242-259
-            if st["prior_update"] == "mle":
-                if rank == 0:
-                    logging.info("...Updating prior parameters using MLE")
-                warn = self.prior_update_mle(gam1s)
-                if warn:
-                    rec["mle_warning"] = warn
-            elif st["prior_update"] == "em":
-                flags |= hb.STEP_EM
-        if it > 0:
-            flags |= hb.STEP_DENOISE_DAMP | hb.STEP_ALPHA1_DAMP       # :275-276, 290-291
-        if st["lmmse_damp"]:
-            flags |= hb.STEP_LMMSE_DAMP
-        if st["learn_gamw"]:
-            flags |= hb.STEP_LEARN_GAMW
-        if self._has_x0:
-            flags |= hb.STEP_METRICS                                  # :379-387
-        t0 = time.perf_counter()
-        u = self._next_probes[0].result()[None] if K == 1 else \
-            np.stack([f.result() for f in self._next_probes])         # :326
-        rec["wait_probes_ms"] = (time.perf_counter() - t0) * 1e3
-        if self.write_files:
-            # pinned slot it % 2 was last read by the writer of it - 2 (started
-            # during the previous step): normally long done
-            t0 = time.perf_counter()
-            self.flush()
-            rec["wait_write_ms"] = (time.perf_counter() - t0) * 1e3
-        h = eng.step_begin(it, flags, st["em_prior_maxit"], self.sigmas, self.a, self.lam,
-                           self.omegas, gam1s, rho, gamw, alpha1, alpha2, u, st["cg_maxit"],
-                           it % 2 if self.write_files else -1)
-        # host work overlapping the step (touches no device state): the next
-        # probes, the previous iteration's files and CSV rows
-        self._next_probes = self._submit_probes()
-        if self.write_files and it > 0 and self._last_out == it - 1:
-            self._pending_write = self._out_pool.submit(self._write_outputs, it - 1, (it - 1) % 2)
-        self._submit_csv()
+        q = self._queued
+        if q is not None:             # queued by the previous step(), already running
+            if q["it"] != it:
+                raise RuntimeError("step(%d) called, step(%d) was queued" % (it, q["it"]))
+            self._queued = None
+            h, flags = q["h"], q["flags"]
+            rec.update(q["rec"])
+        else:
+            flags = self._flags(it, gam1s, rec)
+            u = self._take_probes(rec)
+            if self.write_files:
+                self._flush_until(it - hb.OUT_SLOTS, rec)
+            h = self._begin_step(it, flags, u, chain=False)
+        # host work overlapping the step (touches no device state)
+        self._submit_writers()
+        self._submit_csv()            # previous iterations' rows
+        if self._can_chain(it + 1):
+            rec1 = {}
+            flags1 = self._flags(it + 1, None, rec1)
+            u1 = self._take_probes(rec1)
+            if self.write_files:
+                self._flush_until(it + 1 - hb.OUT_SLOTS, rec1)
+            self._queued = dict(it=it + 1, h=self._begin_step(it + 1, flags1, u1, chain=True),
+                                flags=flags1, rec=rec1)
         r = eng.step_end(h)
         if self.write_files:
-            self._last_out = it
+            self._unwritten.append(it)
 
         if flags & hb.STEP_EM:
             self.lam, self.omegas = r["lam"], r["omegas"]
@@ -452,12 +539,13 @@ class VAMP:
             logging.debug("omegas=%s", self.omegas)
             logging.debug("sigmas=%s", self.sigmas)
             logging.info("...Denoising")
-        if st["return_xhat"]:
+        if st["return_xhat"] and not self.write_files:
             xhat_loc = eng.get_vector(hb.VEC_XHAT1)    # LMMSE leaves xhat1 as denoised
             full = xhat_loc
             if self.comm.Get_size() > 1:
                 full = np.concatenate(self.comm.allgather(xhat_loc))
             st["xhat1s"].append(full.reshape((M, 1)))
+        # (with files, the writer keeps xhat1 from the output copy: see _write_outputs)
         gam2 = r["gam2"]
         for k in range(K):
             alpha1[k] = r["alpha1"][k]
@@ -491,7 +579,7 @@ class VAMP:
                                 [it, gamw[k], gam1[k], gam2[k], alpha1[k], alpha2[k],
                                  self.lam], k)                        # :377
         if self._has_x0:                                              # :379-387
-            s = eng.metrics_end()
+            s = r["metrics"]
             alignment = s[0] / np.sqrt(s[1]) / np.sqrt(s[3])
             l2 = np.sqrt(s[2]) / np.sqrt(s[3])
             rec["metrics"] = (alignment, l2)
