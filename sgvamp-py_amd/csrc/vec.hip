@@ -869,33 +869,50 @@ __global__ void k_reduce_total(const double* __restrict__ bsum_all, int nranks, 
 // block's sum exactly as k_reduce_blocks does (same lane stride, same
 // wave_sum) and folds them in block order exactly as k_reduce_total does, so
 // the result is bitwise the two-kernel one.
-__global__ __launch_bounds__(WAVE) void k_reduce_local(const double* __restrict__ part, int nv,
-                                                       const int* __restrict__ begin, int nblk,
-                                                       Map16 map, double* __restrict__ dst,
-                                                       int op) {
-  const int v = blockIdx.x, lane = threadIdx.x;
+// one rank: per-block sums (each by one wave, lanes strided over the block's
+// parts, butterfly -- the order k_reduce_blocks uses) computed by 16 waves in
+// parallel, then added in block order by one thread: the same sums as a
+// single wave walking the blocks one after another, without its chain of
+// nblk dependent loads (~42 us at 64 blocks)
+constexpr int RL_WAVES = 16;
+constexpr int RL_BATCH = 1024;
+__global__ __launch_bounds__(WAVE * RL_WAVES) void k_reduce_local(
+    const double* __restrict__ part, int nv, const int* __restrict__ begin, int nblk, Map16 map,
+    double* __restrict__ dst, int op) {
+  __shared__ double bs[RL_BATCH];
+  const int v = blockIdx.x, lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   double tot = 0.0;
-  for (int b = 0; b < nblk; ++b) {
-    const int p0 = begin[b], p1 = begin[b + 1];
-    double s;
-    if (op == 0) {
-      s = 0.0;
-      for (int p = p0 + lane; p < p1; p += WAVE) s += part[(int64_t)p * nv + v];
-      s = wave_sum(s);
-    } else {
-      s = __builtin_inf();
-      for (int p = p0 + lane; p < p1; p += WAVE) s = fmin(s, part[(int64_t)p * nv + v]);
-      for (int o = 32; o > 0; o >>= 1) s = fmin(s, __shfl_xor(s, o, WAVE));
+  for (int b0 = 0; b0 < nblk; b0 += RL_BATCH) {
+    const int nb = min(RL_BATCH, nblk - b0);
+    for (int bb = w; bb < nb; bb += RL_WAVES) {
+      const int p0 = begin[b0 + bb], p1 = begin[b0 + bb + 1];
+      double s;
+      if (op == 0) {
+        s = 0.0;
+        for (int p = p0 + lane; p < p1; p += WAVE) s += part[(int64_t)p * nv + v];
+        s = wave_sum(s);
+      } else {
+        s = __builtin_inf();
+        for (int p = p0 + lane; p < p1; p += WAVE) s = fmin(s, part[(int64_t)p * nv + v]);
+        for (int o = 32; o > 0; o >>= 1) s = fmin(s, __shfl_xor(s, o, WAVE));
+      }
+      if (lane == 0) bs[bb] = s;
     }
-    tot = (b == 0) ? s : (op == 0 ? tot + s : fmin(tot, s));
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int bb = 0; bb < nb; ++bb) {
+        const double s = bs[bb];
+        tot = (b0 + bb == 0) ? s : (op == 0 ? tot + s : fmin(tot, s));
+      }
+    __syncthreads();
   }
-  if (lane == 0) dst[map.d[v]] = tot;
+  if (threadIdx.x == 0) dst[map.d[v]] = tot;
 }
 
 hipError_t launch_reduce_local(const double* d_part, int nv, const int* d_begin, int nblk,
                                const Map16& map, double* d_dst, hipStream_t st, int op) {
-  hipLaunchKernelGGL(k_reduce_local, dim3(nv), dim3(WAVE), 0, st, d_part, nv, d_begin, nblk, map,
-                     d_dst, op);
+  hipLaunchKernelGGL(k_reduce_local, dim3(nv), dim3(WAVE * RL_WAVES), 0, st, d_part, nv, d_begin,
+                     nblk, map, d_dst, op);
   return hipGetLastError();
 }
 
