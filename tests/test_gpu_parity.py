@@ -305,6 +305,36 @@ def test_cg_pipeline_matches_host_loop(name, tmp_path, monkeypatch):
             assert maxrel(b_, a_) < 1e-10
 
 
+@pytest.mark.parametrize("name", ["k1_defaults", "k1_L3", "k2_shared", "k4_shared_s_damp",
+                                  "k2_mle_L3", "k1_blocks_csr_s_damp"])
+def test_step_driver_matches_phases(name, tmp_path, monkeypatch):
+    """VAMP.step through sgv_step on the library's worker thread -- chained (the
+    next step queued behind the running one, its scalars taken from it on the
+    device side) and unchained -- against one host call per phase
+    (SGV_STEP=phases): every output file byte-identical, same CG/EM counts."""
+    c = Case(name)
+    res = {}
+    for mode in ("phases", "nochain", ""):
+        monkeypatch.setenv("SGV_STEP", mode)
+        d = tmp_path / (mode or "chain")
+        d.mkdir()
+        v, xh = run_vamp_case(c, d)
+        files = sorted(p.name for p in d.iterdir())
+        res[mode] = ({f: (d / f).read_bytes() for f in files},
+                     [(h["cg_iters"], h["cg_info"], h.get("em_steps")) for h in v.history],
+                     [np.asarray(x) for x in xh])
+        v.engine.close()
+    ref = res["phases"]
+    assert len(ref[0]) >= c.flags["iterations"]
+    for mode in ("nochain", ""):
+        assert res[mode][0].keys() == ref[0].keys()
+        for f, b in ref[0].items():
+            assert res[mode][0][f] == b, (mode, f)
+        assert res[mode][1] == ref[1]
+        for a_, b_ in zip(res[mode][2], ref[2]):
+            np.testing.assert_array_equal(a_, b_)
+
+
 def test_vamp_is_deterministic(tmp_path):
     c = Case("k2_shared")
     (tmp_path / "a").mkdir()
