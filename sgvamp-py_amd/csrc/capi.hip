@@ -91,6 +91,14 @@ static int cg_pipe_default() {
 constexpr int CG_RING = 4;   // mirror slots of the pipelined CG
 constexpr int NOUT_SLOTS = 3;   // pinned output slots (a writer reads one while two steps run)
 
+// SGV_EM_FUSE=0: the device EM loop keeps three launches per step at one rank (A/B)
+static bool em_fuse_default() {
+  static const bool v = [] {
+    const char* e = std::getenv("SGV_EM_FUSE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
 static int sym_class_nc(int cls) { return std::min(16, 2 << (cls + 1)); }   // widest NC using cls
 
 struct sgv_ctx {
@@ -1590,7 +1598,18 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
     for (int l = 0; l < nslab; ++l) hi->om[l] = om[l];
     HIPCHK(hipMemcpyAsync(c->d_ems, hi, sizeof(EmState), hipMemcpyHostToDevice, c->st));
     ea.st = c->d_ems;
+    // one rank: reduction + control in one launch (k_em_reduce_ctl, same bits);
+    // SGV_EM_FUSE=0 A/B
+    const bool fuse = !c->comm && !c->host_ag && c->nblk <= EM_CTL_MAXBLK && em_fuse_default();
     auto enqueue = [&](int j) -> int {
+      if (fuse) {
+        HIPCHK(launch_em(c->d_ch, c->nch, ea, c->d_part, c->st));
+        const EmCtl f{c->d_ch_begin, c->nblk, nslab, c->h_emm + j % CG_RING, (double)c->Mtot, j,
+                      maxit};
+        HIPCHK(launch_em_reduce_ctl(c->d_part, c->d_ems, f, c->st));
+        HIPCHK(hipEventRecord(c->ev_em[j % CG_RING], c->st));
+        return SGV_OK;
+      }
       HIPCHK(launch_em(c->d_ch, c->nch, ea, c->d_part, c->st));
       CHK(reduce_dev(c, EM_NV, c->d_ch_begin, identity_map(), c->d_emtot));
       HIPCHK(launch_em_ctl(c->d_ems, c->h_emm + j % CG_RING, c->d_emtot, nslab, (double)c->Mtot,

@@ -326,6 +326,18 @@ hipError_t launch_em(const ChunkDesc* d_ch, int nch, const EmArgs& a, double* d_
 // copied to `mirror` (host memory).
 hipError_t launch_em_ctl(EmState* d_st, EmState* mirror, const double* d_tot, int nslab,
                          double Mtot, int it, int maxit, hipStream_t st);
+// k_em_reduce_ctl (one rank): the ordered reduction of k_em's partials and the
+// k_em_ctl update in one single-workgroup launch (same bits)
+constexpr int EM_CTL_MAXBLK = 128;   // LD blocks per rank
+struct EmCtl {
+  const int* begin;         // parts of LD block b: [begin[b], begin[b + 1])
+  int nblk, nslab;
+  EmState* mirror;
+  double Mtot;
+  int it, maxit;
+};
+hipError_t launch_em_reduce_ctl(const double* d_part, EmState* d_st, const EmCtl& f,
+                                hipStream_t st);
 
 struct CohortPtrs {
   const double* r[MAXK];

@@ -151,14 +151,22 @@ hipError_t launch_denoise(const ChunkDesc* d_ch, int nch, const DenoiseArgs& a, 
 // ---------------------------------------------------------------------------
 // prior_update_em, src/sgvamp.py:116-136 (one EM step)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(VTHREADS) void k_em(const ChunkDesc* __restrict__ chs, EmArgs a,
-                                                 double* __restrict__ part) {
+// One workgroup per chunk with one marker per thread (EM_THREADS = CHUNK): the
+// step is latency-bound (exp, sqrt and divisions per marker and slab), and
+// four markers in sequence per thread made it 13-16 us at any M.  A thread's
+// sums take its marker's K cohorts in order; the workgroup adds them by wave
+// butterfly, then the 16 waves in order.  false: the device loop has stopped
+// (no-op step; uniform over the grid).
+constexpr int EM_THREADS = CHUNK;
+template <int KM, int LM>
+__device__ __forceinline__ bool em_partials(const ChunkDesc* __restrict__ chs, const EmArgs& a,
+                                            double* __restrict__ part) {
   const ChunkDesc ch = chs[blockIdx.x];
   double lam = a.lam, om[MAXL];
 #pragma unroll
   for (int l = 0; l < MAXL; ++l) om[l] = a.omegas[l];
   if (a.st) {   // device EM loop
-    if (a.st->done) return;
+    if (a.st->done) return false;
     lam = a.st->lam;
 #pragma unroll
     for (int l = 0; l < MAXL; ++l) om[l] = a.st->om[l];
@@ -166,37 +174,31 @@ __global__ __launch_bounds__(VTHREADS) void k_em(const ChunkDesc* __restrict__ c
   double acc[EM_NV];
 #pragma unroll
   for (int v = 0; v < EM_NV; ++v) acc[v] = 0.0;
-  double vr[MPT][MAXK];
+  const int t = threadIdx.x;
+  if (t < ch.len) {
+    double vr[KM];
 #pragma unroll
-  for (int j = 0; j < MPT; ++j) {
-    const int t = threadIdx.x + j * VTHREADS;
-    if (t < ch.len)
-#pragma unroll
-      for (int k = 0; k < MAXK; ++k)
-        if (k < a.K) vr[j][k] = a.r1[k][ch.voff + t];
-  }
-#pragma unroll
-  for (int j = 0; j < MPT; ++j) {
-    if ((int)threadIdx.x + j * VTHREADS >= ch.len) continue;
+    for (int k = 0; k < KM; ++k)
+      if (k < a.K) vr[k] = a.r1[k][ch.voff + t];
     double avg = 0.0;   // sum_k pi_k a_k (np.average numerator, sequential over k)
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k)
+    for (int k = 0; k < KM; ++k)
       if (k < a.K) {
-        const double r = vr[j][k];
+        const double r = vr[k];
         const double r2 = r * r;                  // np.power(r1s, 2)
         const double ginv = 1.0 / a.gam1[k];      // gam1invs
-        double tl[MAXL];
+        double tl[LM];
         double emax = 0.0;
 #pragma unroll
-        for (int l = 0; l < MAXL; ++l)
+        for (int l = 0; l < LM; ++l)
           if (l < a.nslab) {
             tl[l] = -r2 / 2 / (a.sigmas[l] + ginv);          // :127
             emax = (l == 0 || tl[l] > emax) ? tl[l] : emax;
           }
-        double xi[MAXL];
+        double xi[LM];
         double sum_xi = 0.0;
 #pragma unroll
-        for (int l = 0; l < MAXL; ++l)
+        for (int l = 0; l < LM; ++l)
           if (l < a.nslab) {
             xi[l] = lam * om[l] * exp(tl[l] - emax) / sqrt(ginv + a.sigmas[l]);   // :128
             sum_xi = (l == 0) ? xi[l] : sum_xi + xi[l];                                   // :129
@@ -205,29 +207,68 @@ __global__ __launch_bounds__(VTHREADS) void k_em(const ChunkDesc* __restrict__ c
             1.0 / (1.0 + (1 - lam) * exp(-r2 / 2 * a.gam1[k] - emax) / sqrt(ginv) / sum_xi);  // :131
         const double pa = pi * a.a[k];
         avg = (k == 0) ? pa : avg + pa;
+        // compile-time accumulator indices (a runtime acc[1 + nslab] puts the
+        // array in scratch memory)
 #pragma unroll
-        for (int l = 0; l < MAXL; ++l)
-          if (l < a.nslab) acc[1 + l] += pi * (xi[l] / sum_xi) * a.a[k];   // :136 numerator
-        acc[1 + a.nslab] += pa;                                           // :136 denominator
+        for (int v = 1; v < LM + 2; ++v) {
+          const int l = v - 1;
+          if (l < a.nslab)
+            acc[v] += pi * (xi[l] / sum_xi) * a.a[k];   // :136 numerator
+          else if (l == a.nslab)
+            acc[v] += pa;                               // :136 denominator
+        }
       }
     acc[0] += avg / a.scl;   // np.average(pi, axis=0, weights=a)  (:134)
   }
-  block_reduce_store<EM_NV>(acc, part + (int64_t)blockIdx.x * EM_NV, EM_NV);
+  __shared__ double sm[EM_THREADS / WAVE][EM_NV];
+  const int lane = t & (WAVE - 1), w = t / WAVE;
+#pragma unroll
+  for (int v = 0; v < EM_NV; ++v) {
+    const double x = wave_sum(acc[v]);
+    if (lane == 0) sm[w][v] = x;
+  }
+  __syncthreads();
+  if (t < EM_NV) {
+    double x = sm[0][t];
+#pragma unroll
+    for (int q = 1; q < EM_THREADS / WAVE; ++q) x += sm[q][t];
+    part[(int64_t)blockIdx.x * EM_NV + t] = x;
+  }
+  return true;
 }
+
+template <int KM, int LM>
+__global__ __launch_bounds__(EM_THREADS) void k_em(const ChunkDesc* __restrict__ chs, EmArgs a,
+                                                   double* __restrict__ part) {
+  em_partials<KM, LM>(chs, a, part);
+}
+
+// instantiations by cohort / slab count (registers: the fully unrolled
+// MAXK x MAXL body spills at 1024 threads)
+#define EM_DISPATCH(K, L, LAUNCH)                                             \
+  do {                                                                        \
+    if ((K) <= 1 && (L) <= 2) { LAUNCH(1, 2); }                               \
+    else if ((K) <= 4 && (L) <= 2) { LAUNCH(4, 2); }                          \
+    else if ((K) <= 8 && (L) <= 2) { LAUNCH(8, 2); }                          \
+    else if ((K) <= 4) { LAUNCH(4, MAXL); }                                   \
+    else { LAUNCH(MAXK, MAXL); }                                              \
+  } while (0)
 
 hipError_t launch_em(const ChunkDesc* d_ch, int nch, const EmArgs& a, double* d_part,
                      hipStream_t st) {
-  hipLaunchKernelGGL(k_em, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part);
+#define L_EM(KM, LM) \
+  hipLaunchKernelGGL((k_em<KM, LM>), dim3(nch), dim3(EM_THREADS), 0, st, d_ch, a, d_part)
+  EM_DISPATCH(a.K, a.nslab, L_EM);
+#undef L_EM
   return hipGetLastError();
 }
 
 // the host loop's update and test (capi.hip sgv_em), same expressions in the
 // same order: -ffp-contract=off and correctly rounded division and sqrt give
-// the same bits, so the same step count
-__global__ __launch_bounds__(WAVE) void k_em_ctl(EmState* __restrict__ s, EmState* mirror,
-                                                const double* __restrict__ tot, int nslab,
-                                                double Mtot, int it, int maxit) {
-  if (threadIdx.x != 0) return;
+// the same bits, so the same step count.  One thread.
+__device__ void em_ctl_update(EmState* __restrict__ s, EmState* mirror,
+                              const double* __restrict__ tot, int nslab, double Mtot, int it,
+                              int maxit) {
   if (!s->done) {
     const double lam = s->lam;
     const double lam_new = tot[0] / Mtot;                 // np.mean (:134)
@@ -256,10 +297,78 @@ __global__ __launch_bounds__(WAVE) void k_em_ctl(EmState* __restrict__ s, EmStat
   }
 }
 
+__global__ __launch_bounds__(WAVE) void k_em_ctl(EmState* __restrict__ s, EmState* mirror,
+                                                const double* __restrict__ tot, int nslab,
+                                                double Mtot, int it, int maxit) {
+  if (threadIdx.x == 0) em_ctl_update(s, mirror, tot, nslab, Mtot, it, maxit);
+}
+
 hipError_t launch_em_ctl(EmState* d_st, EmState* mirror, const double* d_tot, int nslab,
                          double Mtot, int it, int maxit, hipStream_t st) {
   hipLaunchKernelGGL(k_em_ctl, dim3(1), dim3(WAVE), 0, st, d_st, mirror, d_tot, nslab, Mtot, it,
                      maxit);
+  return hipGetLastError();
+}
+
+// ---- one-workgroup reduction + EM control (one rank) -----------------------
+// k_reduce_local (nv workgroups) followed by k_em_ctl (one wave) cost two
+// launches per EM step; here one 1024-thread workgroup forms all EM_NV totals
+// exactly as k_reduce_local does -- per LD block b, lane l adds parts
+// begin[b] + l, + 64, ... in order, wave butterfly; then the blocks in order --
+// and applies the update and stop test.  Same bits, one launch less per step.
+// (A last-workgroup-done epilogue in k_em itself was measured slower: each
+// workgroup's device-scope release fence writes back the XCD's L2.)
+// Waves take the (block, value) pairs LB_U at a time, all their loads first.
+constexpr int LB_U = 8;
+
+__device__ void lb_reduce(const double* __restrict__ part, int nv, const int* __restrict__ begin,
+                          int nblk, double* bs /* LDS, nv * nblk */, double* tot /* LDS, nv */) {
+  const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
+  const int nw = blockDim.x / WAVE, npairs = nv * nblk;
+  for (int q0 = w * LB_U; q0 < npairs; q0 += nw * LB_U) {
+    double s[LB_U];
+#pragma unroll
+    for (int u = 0; u < LB_U; ++u) {
+      s[u] = 0.0;
+      const int q = q0 + u;
+      if (q < npairs) {
+        const int b = q / nv, v = q - b * nv;
+        const int p1 = begin[b + 1];
+        for (int p = begin[b] + lane; p < p1; p += WAVE) s[u] += part[(int64_t)p * nv + v];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < LB_U; ++u) {
+      const double t = wave_sum(s[u]);
+      if (lane == 0 && q0 + u < npairs) bs[q0 + u] = t;
+    }
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nv) {
+    const int v = threadIdx.x;
+    double t = 0.0;
+    for (int b = 0; b < nblk; ++b) t = (b == 0) ? bs[v] : t + bs[b * nv + v];
+    tot[v] = t;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void k_em_reduce_ctl(const double* __restrict__ part,
+                                                        EmState* __restrict__ s, EmCtl f) {
+  __shared__ double bs[EM_CTL_MAXBLK * EM_NV];
+  __shared__ double tot[EM_NV];
+  if (s->done) {   // past the stop (k_em was a no-op): mirror the state only
+    if (threadIdx.x == 0) em_ctl_update(s, f.mirror, nullptr, f.nslab, f.Mtot, f.it, f.maxit);
+    return;
+  }
+  lb_reduce(part, EM_NV, f.begin, f.nblk, bs, tot);
+  if (threadIdx.x == 0) em_ctl_update(s, f.mirror, tot, f.nslab, f.Mtot, f.it, f.maxit);
+}
+
+hipError_t launch_em_reduce_ctl(const double* d_part, EmState* d_st, const EmCtl& f,
+                                hipStream_t st) {
+  if (f.nblk < 1 || f.nblk > EM_CTL_MAXBLK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_em_reduce_ctl, dim3(1), dim3(1024), 0, st, d_part, d_st, f);
   return hipGetLastError();
 }
 
