@@ -881,14 +881,19 @@ static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const d
   }
   const volatile CgState* last = nullptr;
   int executed = 0;
+  // one rank: iteration it's r.r reduction and the control of it + 1 are one
+  // launch (k_cg_reduce_ctl), enqueued at the end of it; SGV_EM_FUSE=0 A/B
+  const bool fuse = !c->comm && !c->host_ag && c->nblk <= EM_CTL_MAXBLK && em_fuse_default();
   for (int it = 0; it < maxiter; ++it) {
     const size_t np0 = c->pending.size();
     const double cnt0[5] = {c->ld_launches, c->ld_bytes, c->dense_bytes, c->rhs_bytes,
                             c->aux_bytes};
     int npass = 0;
     CgState* slot = c->h_cgm + (it % CG_RING);
-    HIPCHK(launch_cg_ctl(c->d_cgs, slot, c->d_rhonew, it, ncol, -1, c->st));
-    HIPCHK(hipEventRecord(c->ev_cg[it % CG_RING], c->st));
+    if (it == 0 || !fuse) {
+      HIPCHK(launch_cg_ctl(c->d_cgs, slot, c->d_rhonew, it, ncol, -1, c->st));
+      HIPCHK(hipEventRecord(c->ev_cg[it % CG_RING], c->st));
+    }
     if (it > 0) {  // iterative.py:403-407
       PArgs pa{};
       pa.ncol = ncol;
@@ -939,7 +944,13 @@ static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const d
       xa.Y[j] = cc.Y[j];
     }
     HIPCHK(launch_cg_xr(c->d_ch, c->nch, xa, c->d_part, c->st));
-    CHK(reduce_dev(c, MAXC, c->d_ch_begin, identity_map(), c->d_rhonew));
+    if (fuse && it + 1 < maxiter) {
+      HIPCHK(launch_cg_reduce_ctl(c->d_part, c->d_ch_begin, c->nblk, c->d_cgs,
+                                  c->h_cgm + ((it + 1) % CG_RING), it + 1, ncol, c->st));
+      HIPCHK(hipEventRecord(c->ev_cg[(it + 1) % CG_RING], c->st));
+    } else {
+      CHK(reduce_dev(c, MAXC, c->d_ch_begin, identity_map(), c->d_rhonew));
+    }
     // the stop test of `it` (its first kernel) decides whether it did any work
     CHK(event_spin(c, c->ev_cg[it % CG_RING]));
     last = slot;

@@ -387,6 +387,11 @@ struct CgState {
 // final_it, :420-422).  The state is also copied to `mirror` (host memory).
 hipError_t launch_cg_ctl(CgState* d_st, CgState* mirror, const double* d_rho_new, int it,
                          int ncol, int final_it, hipStream_t st);
+// one rank: k_reduce_local of k_cg_xr's r.r partials (iteration it - 1) + the
+// control of iteration it (it >= 1) in one launch, same bits
+hipError_t launch_cg_reduce_ctl(const double* d_part, const int* d_begin, int nblk,
+                                CgState* d_st, CgState* mirror, int it, int ncol,
+                                hipStream_t st);
 // the CG prologue's scalars from the device-reduced |b|^2 (tot[c]) and |r0|^2
 // (tot[MAXC + c]) (iterative.py:376-392): rho, atol = max(0, rtol |b|), active
 // unless |b| == 0; then X and R_s X of the |b| == 0 columns are zeroed

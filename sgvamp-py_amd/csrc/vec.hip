@@ -562,9 +562,9 @@ hipError_t launch_cg_p(const ChunkDesc* d_ch, int nch, const PArgs& a, hipStream
 // Device-side CG control, one wave (thread j = column j); same expressions
 // as the host loop (correctly rounded sqrt and division: the same decisions
 // and the same beta bit for bit).
-__global__ __launch_bounds__(WAVE) void k_cg_ctl(CgState* __restrict__ s, CgState* mirror,
-                                                const double* __restrict__ rho_new, int it, int ncol,
-                                                int final_it) {
+// by one wave (lane j = column j)
+__device__ __forceinline__ void cg_ctl_body(CgState* __restrict__ s, CgState* mirror,
+                                            const double* rho_new, int it, int ncol, int final_it) {
   const int j = threadIdx.x;
   int act = 0;
   if (j < ncol) {
@@ -605,6 +605,34 @@ __global__ __launch_bounds__(WAVE) void k_cg_ctl(CgState* __restrict__ s, CgStat
     mirror->any = any;
     mirror->it = it;
   }
+}
+
+__global__ __launch_bounds__(WAVE) void k_cg_ctl(CgState* __restrict__ s, CgState* mirror,
+                                                const double* __restrict__ rho_new, int it, int ncol,
+                                                int final_it) {
+  cg_ctl_body(s, mirror, rho_new, it, ncol, final_it);
+}
+
+// One rank: the r.r reduction of iteration it - 1 (k_cg_xr's partials, formed
+// as k_reduce_local forms them) and the control of iteration it in one
+// single-workgroup launch -- same bits as k_reduce_local + k_cg_ctl.
+__global__ __launch_bounds__(1024) void k_cg_reduce_ctl(const double* __restrict__ part,
+                                                        const int* __restrict__ begin, int nblk,
+                                                        CgState* __restrict__ s, CgState* mirror,
+                                                        int it, int ncol) {
+  __shared__ double bs[EM_CTL_MAXBLK * MAXC];
+  __shared__ double tot[MAXC];
+  lb_reduce(part, MAXC, begin, nblk, bs, tot);
+  if (threadIdx.x < WAVE) cg_ctl_body(s, mirror, tot, it, ncol, -1);
+}
+
+hipError_t launch_cg_reduce_ctl(const double* d_part, const int* d_begin, int nblk,
+                                CgState* d_st, CgState* mirror, int it, int ncol,
+                                hipStream_t st) {
+  if (nblk < 1 || nblk > EM_CTL_MAXBLK || it < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_cg_reduce_ctl, dim3(1), dim3(1024), 0, st, d_part, d_begin, nblk, d_st,
+                     mirror, it, ncol);
+  return hipGetLastError();
 }
 
 __global__ __launch_bounds__(WAVE) void k_cg_init(CgState* __restrict__ s,
