@@ -215,6 +215,21 @@ struct sgv_ctx {
   hipEvent_t ev_cg[4] = {nullptr, nullptr, nullptr, nullptr};
   // device EM loop (sgv_em with cg_pipe on): state, mirror ring, init staging
   EmState* d_ems = nullptr;
+  // replicated EM (with a communicator): every rank's r1 is all-gathered once per
+  // EM loop and the loop runs over all markers on every rank with one-rank
+  // reductions -- the reference's r1 all-gather + redundant EM (sgvamp.py:228-259)
+  // instead of one exchange per EM step.  Global chunk table in global block
+  // order (the same sums as one rank); gathered r1 as [nranks][K][mpad_max].
+  bool em_rep = false;
+  int nchg = 0, nblkg = 0;
+  int64_t mpad_max = 0;
+  ChunkDesc* d_chg = nullptr;
+  int* d_chg_begin = nullptr;
+  double* d_partg = nullptr;
+  double* d_r1send = nullptr;   // [K][mpad_max]
+  double* d_r1g = nullptr;      // [nranks][K][mpad_max]
+  double* h_r1send = nullptr;   // host exchange staging
+  double* h_r1g = nullptr;
   EmState* h_emm = nullptr;       // [CG_RING]
   EmState* h_emi = nullptr;
   double* d_emtot = nullptr;
@@ -1211,6 +1226,13 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   for (hipEvent_t e : c->ev_cg)
     if (e) (void)hipEventDestroy(e);
   if (c->d_ems) (void)hipFree(c->d_ems);
+  if (c->d_chg) (void)hipFree(c->d_chg);
+  if (c->d_chg_begin) (void)hipFree(c->d_chg_begin);
+  if (c->d_partg) (void)hipFree(c->d_partg);
+  if (c->d_r1send) (void)hipFree(c->d_r1send);
+  if (c->d_r1g) (void)hipFree(c->d_r1g);
+  if (c->h_r1send) (void)hipHostFree(c->h_r1send);
+  if (c->h_r1g) (void)hipHostFree(c->h_r1g);
   if (c->d_emtot) (void)hipFree(c->d_emtot);
   if (c->h_emm) (void)hipHostFree(c->h_emm);
   if (c->h_emi) (void)hipHostFree(c->h_emi);
@@ -1284,6 +1306,116 @@ static int comm_args(sgv_ctx* c, int nranks, int rank, const int* nblk_per_rank)
   return SGV_OK;
 }
 
+// all-gather of cnt doubles per rank (device buffers), RCCL or the host callback
+static int gather_f64(sgv_ctx* c, const double* d_send, double* d_recv, size_t cnt,
+                      double* h_send, double* h_recv) {
+  if (c->comm) {
+    NCCLCHK(ncclAllGather(d_send, d_recv, cnt, ncclDouble, c->comm, c->st));
+    return SGV_OK;
+  }
+  HIPCHK(hipMemcpyAsync(h_send, d_send, sizeof(double) * cnt, hipMemcpyDeviceToHost, c->st));
+  CHK(stream_wait(c));
+  if (c->host_ag(c->host_ag_user, h_send, h_recv, (int64_t)cnt) != 0)
+    return fail(c, SGV_ERR_RCCL, "host all-gather callback failed");
+  HIPCHK(hipMemcpyAsync(d_recv, h_recv, sizeof(double) * cnt * c->nranks, hipMemcpyHostToDevice,
+                        c->st));
+  return SGV_OK;
+}
+
+// SGV_EM_REP=0: with a communicator, one exchange per EM step instead (A/B)
+static bool em_rep_default() {
+  static const bool v = [] {
+    const char* e = std::getenv("SGV_EM_REP");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// replicated EM tables: every rank's block sizes (gathered), the global chunk
+// table and the gathered-r1 buffers
+static int em_rep_setup(sgv_ctx* c, const int* nblk_per_rank) {
+  if (!em_rep_default()) return SGV_OK;
+  int nbg = 0;
+  for (int r = 0; r < c->nranks; ++r) nbg += nblk_per_rank[r];
+  if (nbg > EM_CTL_MAXBLK) return SGV_OK;   // one-workgroup reduction cap: per-step exchange
+  const size_t nb = (size_t)c->nbmax;
+  double *d_s = nullptr, *d_r = nullptr;
+  std::vector<double> hs(nb, 0.0), hr(nb * c->nranks, 0.0);
+  for (int b = 0; b < c->nblk; ++b) hs[b] = (double)c->bn[b];
+  double *h_s = nullptr, *h_r = nullptr;
+  int rc = SGV_OK;
+  if (hipMalloc(&d_s, sizeof(double) * nb) != hipSuccess ||
+      hipMalloc(&d_r, sizeof(double) * nb * c->nranks) != hipSuccess ||
+      hipHostMalloc(&h_s, sizeof(double) * nb) != hipSuccess ||
+      hipHostMalloc(&h_r, sizeof(double) * nb * c->nranks) != hipSuccess)
+    rc = fail(c, SGV_ERR_HIP, "em_rep_setup: allocation failed");
+  if (rc == SGV_OK && hipMemcpy(d_s, hs.data(), sizeof(double) * nb, hipMemcpyHostToDevice) != hipSuccess)
+    rc = fail(c, SGV_ERR_HIP, "em_rep_setup: copy failed");
+  if (rc == SGV_OK) rc = gather_f64(c, d_s, d_r, nb, h_s, h_r);
+  if (rc == SGV_OK && hipStreamSynchronize(c->st) != hipSuccess)
+    rc = fail(c, SGV_ERR_HIP, "em_rep_setup: sync failed");
+  if (rc == SGV_OK && hipMemcpy(hr.data(), d_r, sizeof(double) * nb * c->nranks, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(c, SGV_ERR_HIP, "em_rep_setup: copy failed");
+  if (d_s) (void)hipFree(d_s);
+  if (d_r) (void)hipFree(d_r);
+  if (h_s) (void)hipHostFree(h_s);
+  if (h_r) (void)hipHostFree(h_r);
+  CHK(rc);
+  // per-rank padded layouts (the rule of sgv_create), then the global chunks
+  std::vector<std::vector<int64_t>> bv(c->nranks);
+  int64_t mpmax = PADV;
+  for (int r = 0; r < c->nranks; ++r) {
+    int64_t v = 0;
+    for (int b = 0; b < nblk_per_rank[r]; ++b) {
+      const int64_t n = (int64_t)hr[(size_t)r * nb + b];
+      if (n < 1) return fail(c, SGV_ERR_ARG, "em_rep_setup: rank %d block %d size %lld", r, b,
+                             (long long)n);
+      bv[r].push_back(v);
+      v += round_up(n, PADV);
+    }
+    mpmax = std::max(mpmax, std::max<int64_t>(v, PADV));
+  }
+  if (c->Mpad > mpmax) return fail(c, SGV_ERR_ARG, "em_rep_setup: inconsistent layouts");
+  std::vector<ChunkDesc> ch;
+  std::vector<int> chb;
+  int gb = 0;
+  for (int r = 0; r < c->nranks; ++r)
+    for (int b = 0; b < nblk_per_rank[r]; ++b, ++gb) {
+      chb.push_back((int)ch.size());
+      const int64_t n = (int64_t)hr[(size_t)r * nb + b];
+      const int64_t base = (int64_t)r * c->K * mpmax + bv[r][b];
+      for (int64_t o = 0; o < n; o += CHUNK)
+        ch.push_back(ChunkDesc{base + o, (int32_t)std::min<int64_t>(CHUNK, n - o), gb});
+    }
+  chb.push_back((int)ch.size());
+  c->mpad_max = mpmax;
+  c->nchg = (int)ch.size();
+  c->nblkg = gb;
+  HIPCHK(hipMalloc(&c->d_chg, sizeof(ChunkDesc) * ch.size()));
+  HIPCHK(hipMemcpy(c->d_chg, ch.data(), sizeof(ChunkDesc) * ch.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&c->d_chg_begin, sizeof(int) * chb.size()));
+  HIPCHK(hipMemcpy(c->d_chg_begin, chb.data(), sizeof(int) * chb.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&c->d_partg, sizeof(double) * ch.size() * EM_NV));
+  const size_t per = (size_t)c->K * mpmax;
+  HIPCHK(hipMalloc(&c->d_r1send, sizeof(double) * per));
+  HIPCHK(hipMemset(c->d_r1send, 0, sizeof(double) * per));
+  HIPCHK(hipMalloc(&c->d_r1g, sizeof(double) * per * c->nranks));
+  if (!c->comm) {
+    HIPCHK(hipHostMalloc(&c->h_r1send, sizeof(double) * per));
+    HIPCHK(hipHostMalloc(&c->h_r1g, sizeof(double) * per * c->nranks));
+  }
+  c->em_rep = true;
+  return SGV_OK;
+}
+
+// every cohort's r1 from every rank -> d_r1g (once per EM loop)
+static int gather_r1(sgv_ctx* c) {
+  for (int k = 0; k < c->K; ++k)
+    HIPCHK(hipMemcpyAsync(c->d_r1send + (size_t)k * c->mpad_max, c->r1[k],
+                          sizeof(double) * c->Mpad, hipMemcpyDeviceToDevice, c->st));
+  return gather_f64(c, c->d_r1send, c->d_r1g, (size_t)c->K * c->mpad_max, c->h_r1send, c->h_r1g);
+}
+
 extern "C" int sgv_comm_init(sgv_ctx* c, int nranks, int rank, const char* id,
                              const int* nblk_per_rank) {
   ENTER(c);
@@ -1292,7 +1424,8 @@ extern "C" int sgv_comm_init(sgv_ctx* c, int nranks, int rank, const char* id,
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof uid);
   NCCLCHK(ncclCommInitRank(&c->comm, nranks, uid, rank));
-  return comm_buffers(c, nranks, rank, nblk_per_rank);
+  CHK(comm_buffers(c, nranks, rank, nblk_per_rank));
+  return em_rep_setup(c, nblk_per_rank);
 }
 
 extern "C" int sgv_comm_init_host(sgv_ctx* c, int nranks, int rank, const int* nblk_per_rank,
@@ -1306,7 +1439,7 @@ extern "C" int sgv_comm_init_host(sgv_ctx* c, int nranks, int rank, const int* n
   HIPCHK(hipHostMalloc(&c->h_bsum_all, sizeof(double) * per * nranks));
   c->host_ag = fn;
   c->host_ag_user = user;
-  return SGV_OK;
+  return em_rep_setup(c, nblk_per_rank);
 }
 
 // ---------------------------------------------------------------------------
@@ -1610,14 +1743,24 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
     HIPCHK(hipMemcpyAsync(c->d_ems, hi, sizeof(EmState), hipMemcpyHostToDevice, c->st));
     ea.st = c->d_ems;
     // one rank: reduction + control in one launch (k_em_reduce_ctl, same bits);
-    // SGV_EM_FUSE=0 A/B
-    const bool fuse = !c->comm && !c->host_ag && c->nblk <= EM_CTL_MAXBLK && em_fuse_default();
+    // SGV_EM_FUSE=0 A/B.  With a communicator: the replicated EM (em_rep_setup)
+    // runs the same one-rank loop over every rank's gathered r1.
+    const bool rep = c->em_rep;
+    const bool fuse = rep || (!c->comm && !c->host_ag && c->nblk <= EM_CTL_MAXBLK &&
+                              em_fuse_default());
+    const ChunkDesc* ech = rep ? c->d_chg : c->d_ch;
+    const int* ebeg = rep ? c->d_chg_begin : c->d_ch_begin;
+    const int enb = rep ? c->nblkg : c->nblk, ench = rep ? c->nchg : c->nch;
+    double* epart = rep ? c->d_partg : c->d_part;
+    if (rep) {
+      CHK(gather_r1(c));
+      for (int k = 0; k < c->K; ++k) ea.r1[k] = c->d_r1g + (size_t)k * c->mpad_max;
+    }
     auto enqueue = [&](int j) -> int {
       if (fuse) {
-        HIPCHK(launch_em(c->d_ch, c->nch, ea, c->d_part, c->st));
-        const EmCtl f{c->d_ch_begin, c->nblk, nslab, c->h_emm + j % CG_RING, (double)c->Mtot, j,
-                      maxit};
-        HIPCHK(launch_em_reduce_ctl(c->d_part, c->d_ems, f, c->st));
+        HIPCHK(launch_em(ech, ench, ea, epart, c->st));
+        const EmCtl f{ebeg, enb, nslab, c->h_emm + j % CG_RING, (double)c->Mtot, j, maxit};
+        HIPCHK(launch_em_reduce_ctl(epart, c->d_ems, f, c->st));
         HIPCHK(hipEventRecord(c->ev_em[j % CG_RING], c->st));
         return SGV_OK;
       }
