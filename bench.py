@@ -94,14 +94,17 @@ def make_problem(eng, comm, args):
     return beta, ys
 
 
-def read_traffic(kernel_prefix="k_ld_pass"):
-    """HBM bytes per LD-pass launch from the committed PMC summary, if any
-    (profiles/*pmc*.json written by tools/pmc_summary.py)."""
-    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+def read_traffic(kernel_prefix, bytes_launch):
+    """HBM bytes per LD-pass launch from the committed PMC summary of the same
+    workload (profiles/*pmc*.json written by tools/pmc_summary.py): the newest
+    summary for this kernel whose algorithmic bytes per launch agree with this
+    run's within 1 %.  None when no summary was collected on this workload."""
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))   # by round label
     for path in reversed(cands):
         try:
             d = json.load(open(path))
-            if kernel_prefix in d.get("kernel", ""):
+            alg = float(d.get("algorithmic_bytes_per_launch") or 0)
+            if kernel_prefix in d.get("kernel", "") and abs(alg - bytes_launch) <= 0.01 * bytes_launch:
                 return float(d["hbm_bytes_per_launch"]), os.path.basename(path)
         except Exception:
             continue
@@ -218,7 +221,8 @@ def main():
     dense_equiv = (tm["dense_bytes"] / launches + tm["rhs_bytes"] / launches) / avg_s / 1e9
     mfma = args.ld_format == "packed" and 2 * K >= 3     # NC >= 3: the f64 MFMA pass
     traffic, traffic_src = read_traffic(("k_sym_mfma" if mfma else "k_sym_pass")
-                                        if args.ld_format == "packed" else "k_ld_pass")
+                                        if args.ld_format == "packed" else "k_ld_pass",
+                                        bytes_launch)
     if eng.M == 200000 and args.ridge == 0 and not args.lmmse_damp:
         cname = {1: "C2 (BASELINE.json configs[1])", 4: "C3 (BASELINE.json configs[2])"}.get(K, "custom")
     elif eng.M == 1000000 and K == 1 and args.ridge == 0 and not args.lmmse_damp:
