@@ -423,16 +423,19 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize_strip(
   double y[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) y[c] = 0.0;
+#pragma unroll 4
   for (int itm = pn.item_begin + q; itm < pn.item_end; itm += FIN_Q) {
     const double* rp = rowpart + ((int64_t)itm * SYM_H + t) * NC;
 #pragma unroll
     for (int c = 0; c < NC; ++c) y[c] += ldg(rp + c);
   }
+#pragma unroll 4
   for (int sl = pn.own_sb + q; sl < pn.own_se; sl += FIN_Q) {
     const double* cp = colpart + (int64_t)sl * NC * MF_CW + tr;
 #pragma unroll
     for (int c = 0; c < NC; ++c) y[c] += ldg(cp + c * MF_CW);
   }
+#pragma unroll 4
   for (int sl = pn.oth_sb + q; sl < pn.oth_se; sl += FIN_Q) {
     const double* cp = colpart + (int64_t)sl * NC * MF_CW + SYM_H + tr;
 #pragma unroll

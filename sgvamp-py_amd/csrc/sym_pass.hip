@@ -306,6 +306,7 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize(const SymPanel* __
   for (int c = 0; c < NC; ++c) y[c] = 0.0;
   const int i = pn.r0 + (t < pn.H ? t : 0);   // block-relative row
   // this panel's row parts, chunk order within the part
+#pragma unroll 4
   for (int itm = pn.item_begin + q; itm < pn.item_end; itm += FIN_Q) {
     const double* rp = rowpart + ((int64_t)itm * SYM_H + t) * NC;
 #pragma unroll
