@@ -1,0 +1,47 @@
+"""bench.py's roofline bookkeeping (CPU): the PMC traffic attached to a bench
+line must come from a summary of the same workload."""
+import json
+import os
+import sys
+
+from tests.conftest import ROOT
+
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def _summaries():
+    out = {}
+    for f in sorted(os.listdir(os.path.join(ROOT, "profiles"))):
+        if "pmc" in f and f.endswith(".json"):
+            out[f] = json.load(open(os.path.join(ROOT, "profiles", f)))
+    return out
+
+
+def test_traffic_matches_workload_bytes():
+    sums = _summaries()
+    assert sums, "no PMC summaries committed under profiles/"
+    for name, d in sums.items():
+        alg = d.get("algorithmic_bytes_per_launch")
+        if not alg:
+            continue
+        kern = "k_sym_mfma" if "k_sym_mfma" in d["kernel"] else d["kernel"].split("<")[0]
+        traffic, src = bench.read_traffic(kern, alg)
+        assert src is not None
+        got = sums[src]
+        assert abs(got["algorithmic_bytes_per_launch"] - alg) <= 0.01 * alg
+        assert traffic == got["hbm_bytes_per_launch"]
+
+
+def test_traffic_none_for_unprofiled_workload():
+    # the C2 pass bytes at ten times the size: no summary, so no traffic claimed
+    assert bench.read_traffic("k_sym_pass", 2.0e11) == (None, None)
+    assert bench.read_traffic("k_no_such_kernel", 20210140245.0) == (None, None)
+
+
+def test_northstar_and_c2_summaries_present():
+    sums = _summaries()
+    kinds = {(d["kernel"].split("<")[0], round(d.get("algorithmic_bytes_per_launch") or 0, -9))
+             for d in sums.values()}
+    assert ("k_sym_pass", 2.0e10) in kinds          # C2, K = 1
+    assert ("k_sym_mfma", 6.4e10) in kinds          # north star, M = 1e6, K = 4
