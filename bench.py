@@ -94,17 +94,19 @@ def make_problem(eng, comm, args):
     return beta, ys
 
 
-def read_traffic(kernel_prefix, bytes_launch):
+def read_traffic(kernel_prefix, bytes_launch, K, M):
     """HBM bytes per LD-pass launch from the committed PMC summary of the same
     workload (profiles/*pmc*.json written by tools/pmc_summary.py): the newest
-    summary for this kernel whose algorithmic bytes per launch agree with this
-    run's within 1 %.  None when no summary was collected on this workload."""
+    summary for this kernel, K and M whose algorithmic bytes per launch agree
+    with this run's within 1 %.  None when no summary was collected on this
+    workload."""
     cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))   # by round label
     for path in reversed(cands):
         try:
             d = json.load(open(path))
             alg = float(d.get("algorithmic_bytes_per_launch") or 0)
-            if kernel_prefix in d.get("kernel", "") and abs(alg - bytes_launch) <= 0.01 * bytes_launch:
+            if (kernel_prefix in d.get("kernel", "") and d.get("K") == K and d.get("M") == M
+                    and abs(alg - bytes_launch) <= 0.01 * bytes_launch):
                 return float(d["hbm_bytes_per_launch"]), os.path.basename(path)
         except Exception:
             continue
@@ -222,7 +224,7 @@ def main():
     mfma = args.ld_format == "packed" and 2 * K >= 3     # NC >= 3: the f64 MFMA pass
     traffic, traffic_src = read_traffic(("k_sym_mfma" if mfma else "k_sym_pass")
                                         if args.ld_format == "packed" else "k_ld_pass",
-                                        bytes_launch)
+                                        bytes_launch, K, eng.M)
     if eng.M == 200000 and args.ridge == 0 and not args.lmmse_damp:
         cname = {1: "C2 (BASELINE.json configs[1])", 4: "C3 (BASELINE.json configs[2])"}.get(K, "custom")
     elif eng.M == 1000000 and K == 1 and args.ridge == 0 and not args.lmmse_damp:

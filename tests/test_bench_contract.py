@@ -26,17 +26,22 @@ def test_traffic_matches_workload_bytes():
         if not alg:
             continue
         kern = "k_sym_mfma" if "k_sym_mfma" in d["kernel"] else d["kernel"].split("<")[0]
-        traffic, src = bench.read_traffic(kern, alg)
+        traffic, src = bench.read_traffic(kern, alg, d["K"], d["M"])
         assert src is not None
         got = sums[src]
         assert abs(got["algorithmic_bytes_per_launch"] - alg) <= 0.01 * alg
+        assert (got["K"], got["M"]) == (d["K"], d["M"])
         assert traffic == got["hbm_bytes_per_launch"]
 
 
 def test_traffic_none_for_unprofiled_workload():
     # the C2 pass bytes at ten times the size: no summary, so no traffic claimed
-    assert bench.read_traffic("k_sym_pass", 2.0e11) == (None, None)
-    assert bench.read_traffic("k_no_such_kernel", 20210140245.0) == (None, None)
+    assert bench.read_traffic("k_sym_pass", 2.0e11, 1, 200000) == (None, None)
+    assert bench.read_traffic("k_no_such_kernel", 20210140245.0, 1, 200000) == (None, None)
+    # C5 and the north star store the same LD (bytes within 0.2 %): K tells them apart
+    assert bench.read_traffic("k_sym_mfma", 63779430912.0, 8, 1000000)[1] == "pmc_sym_mfma_r01s6_c5.json"
+    assert bench.read_traffic("k_sym_mfma", 63651430912.0, 4, 1000000)[1] == \
+        "pmc_sym_mfma_r01s6_northstar.json"
 
 
 def test_northstar_and_c2_summaries_present():

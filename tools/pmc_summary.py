@@ -3,7 +3,9 @@
 
 Usage:
   tools/pmc_summary.py --fetch DIR_OR_CSV --write DIR_OR_CSV --kernel k_ld_pass \
-      --label r01 [--algorithmic-bytes B] > profiles/pmc_ld_pass_r01.json
+      --label r01 [--algorithmic-bytes B] [--K K --M M] > profiles/pmc_ld_pass_r01.json
+(bench.py attaches a summary's traffic only to a run of the same kernel, K, M and
+algorithmic bytes per launch.)
 
 Corrections (MI355X_MICROARCH.md, HBM section; cdna_hip_programming.md section 7):
 * FETCH_SIZE and WRITE_SIZE are in KiB (x1024);
@@ -52,6 +54,8 @@ def main():
     ap.add_argument("--kernel", default="k_ld_pass")
     ap.add_argument("--label", default="")
     ap.add_argument("--algorithmic-bytes", type=float, default=None)
+    ap.add_argument("--K", type=int, default=None, help="cohorts of the profiled bench run")
+    ap.add_argument("--M", type=int, default=None, help="markers of the profiled bench run")
     a = ap.parse_args()
     fetch = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
     write = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
@@ -64,6 +68,8 @@ def main():
     out = {
         "kernel": a.kernel,
         "label": a.label,
+        "K": a.K,
+        "M": a.M,
         "dispatches_fetch": len(fetch),
         "dispatches_write": len(write),
         "FETCH_SIZE_kib_median": f_kib,
