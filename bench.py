@@ -1,8 +1,14 @@
 #!/usr/bin/env python3
-"""Benchmark: VAMP iterations/s on BASELINE.json configs[1] (C2).
+"""Benchmark: VAMP iterations/s on the north-star configuration.
 
-Workload (C2): K = 1 cohort, M = 200,000 markers in 8 LD blocks of 25,000,
-N = 10,000 samples, the reference CLI's default flags (gamw 5, gam1 1e-6,
+Default workload = the configuration BASELINE.json's north_star states its
+target on ("70 % of the HBM roofline on the LD mat-vec at M=1e6, K=4"):
+M = 1,000,000 markers in 64 LD blocks of 15,625 (C4's block structure), K = 4
+cohorts sharing one LD (8 CG right-hand sides per LD pass: the f64-MFMA pass),
+N = 10,000 samples per cohort, one GPU (63.5 GB of packed LD fits one MI355X).
+Other configurations are flags: C2 (configs[1]) ``--blocks 8 --block-size 25000
+--K 1``; C3 adds ``--K 4``; C4 ``--K 1``; C5 ``--K 8 --ridge 0.1 --lmmse-damp 1``.
+The reference CLI's default flags (gamw 5, gam1 1e-6,
 rho 0.5, cg-maxit 500, EM prior from it 1 with <= 100 steps, learn-gamw 1,
 lmmse-damp 0, s 0) except the prior: --prior matched (default) sets
 --prior-vars 0,0.8/cm --prior-probs 0.5,0.5, the simulated mixture.  With the
@@ -17,8 +23,10 @@ causal markers, h2 = 0.8).  A "step" is one VAMP outer iteration
 learning, output files.  Inputs are resident in HBM before timing starts.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-the 8 LD blocks are sharded over the N ranks (strong scaling, one problem);
+the LD blocks are sharded over the N ranks (strong scaling, one problem);
 CG dot products are ordered per-block sums exchanged with RCCL all-gathers.
+The launcher only sets RANK/WORLD_SIZE/MASTER_*: the host communicator is the
+build's own TCP rendezvous (sgvamp-py_amd/comm.py), torch is never imported.
 
 Prints ONE JSON line on rank 0 (other output goes to stderr).
 """
@@ -48,13 +56,15 @@ def parse():
     p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--blocks", type=int, default=8)
-    p.add_argument("--block-size", type=int, default=25000)
+    p.add_argument("--blocks", type=int, default=64)
+    p.add_argument("--block-size", type=int, default=15625)
     p.add_argument("--nsamp", type=int, default=10000)
-    p.add_argument("--K", type=int, default=1)
+    p.add_argument("--K", type=int, default=4)
     p.add_argument("--seed", type=int, default=2025)
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    p.add_argument("--cpu-iters", type=int, default=30)   # ~10 s of CPU work on the box
+    p.add_argument("--cpu-blocks", type=int, default=2,
+                   help="LD blocks of the CPU-baseline sample (see cpu_baseline)")
+    p.add_argument("--cpu-iters", type=int, default=3)
     p.add_argument("--no-files", action="store_true", help="skip the per-iteration output files")
     p.add_argument("--out-dir", default=None, help="keep the output files here (default: a temp dir)")
     p.add_argument("--share-device", action="store_true",
@@ -113,30 +123,75 @@ def read_traffic(kernel_prefix, bytes_launch, K, M):
     return None, None
 
 
-def cpu_baseline(eng, args, ref_flags):
-    """The oracle (the build's NumPy restatement, OpenBLAS threads) on a bounded
-    sample: LD block 0 (n = block-size markers) of the same workload."""
+def matvecs_per_step(recs, learn_gamw=True):
+    """Single-column LD mat-vecs the reference performs for one outer iteration
+    with the CG counts the GPU run recorded: per cohort CG #1 + CG #2 iterations
+    (src/sgvamp.py:316,332), the two warm-start residuals (iterative.py:392:
+    x0.any() holds from iteration 1 on) and the two gamw products (:352,359)."""
+    tot = 0
+    for rec in recs:
+        for n1, n2 in rec["cg_iters"]:
+            tot += n1 + n2 + 2 + (2 if learn_gamw else 0)
+    return tot / max(len(recs), 1)
+
+
+def cpu_baseline(eng, args, ref_flags, recs, x0):
+    """The oracle (the build's NumPy restatement of the reference, OpenBLAS
+    threads) timed on a bounded sample of the SAME workload and extrapolated to
+    the full one with the GPU run's own CG counts.
+
+    Sample: LD blocks 0 .. cpu_blocks-1 (dense f64, as the reference stores
+    them) with all K cohorts' r and x0 restricted to those markers, run for
+    cpu_iters outer iterations.  The oracle's LD mat-vecs are timed separately
+    (one call = one column over the sample's blocks).  Full-workload step time
+    = (non-LD time per step) x (M / sample markers) + (mat-vec time per block)
+    x (LD blocks) x (single-column mat-vecs per step of the reference with the
+    CG counts recorded in the timed GPU steps).  The reference itself never
+    travels to the GPU box; its CPU cost model is that of this restatement."""
     import threadpoolctl
 
     from oracle import vamp_oracle as vo
     import hip_backend as hb
 
-    n = eng.block_sizes[0]
-    B = eng.get_ld_block(0, 0)
-    r = eng.get_vector(hb.VEC_R, 0)[:n].copy()
-    L = vo.BlockLD([B], s=args.ridge)
+    S = max(1, min(args.cpu_blocks, len(eng.block_sizes)))
+    n = int(sum(eng.block_sizes[:S]))
+    blocks = [eng.get_ld_block(0, b) for b in range(S)]
+    r_list = [eng.get_vector(hb.VEC_R, k)[:n].copy() for k in range(eng.K)]
+    L = vo.BlockLD(blocks, s=args.ridge)
+    t_mv = [0.0, 0]
+    raw = L.matvec_R
+
+    def timed(v):
+        t = time.perf_counter()
+        out = raw(v)
+        t_mv[0] += time.perf_counter() - t
+        t_mv[1] += 1
+        return out
+
+    L.matvec_R = timed
     its = args.cpu_iters
     t0 = time.perf_counter()
-    vo.infer([L], [0], [r], [args.nsamp], its, reducer=vo.Reducer(), seed=args.seed, **ref_flags)
+    vo.infer([L], [0] * eng.K, r_list, [args.nsamp] * eng.K, its, x0=x0[:n],
+             reducer=vo.Reducer(), seed=args.seed, **ref_flags)
     dt = time.perf_counter() - t0
     info = threadpoolctl.threadpool_info()
-    cores = max([i.get("num_threads", 1) for i in info if i.get("internal_api") in
-                 ("openblas", "mkl", "blis")] or [1])
-    frac = (n * n) / float(sum(b * b for b in eng.block_sizes))
-    return dict(value=its / dt * frac, unit="VAMP it/s", cores=int(cores), kind="port",
-                sample="oracle/vamp_oracle.py (NumPy+OpenBLAS) on LD block 0 only (%d markers, "
-                       "%.1f GB), iterations 0-%d, %.2f s; it/s scaled by the LD-byte fraction "
-                       "%.4f of the full workload" % (n, n * n * 8 / 1e9, its - 1, dt, frac))
+    threads = max([i.get("num_threads", 1) for i in info if i.get("internal_api") in
+                   ("openblas", "mkl", "blis")] or [1])
+    mv_block = t_mv[0] / max(t_mv[1], 1) / S
+    other = (dt - t_mv[0]) / its * (eng.M / float(n))
+    nmv = matvecs_per_step(recs, ref_flags.get("learn_gamw", True))
+    step = other + mv_block * len(eng.block_sizes) * nmv
+    return dict(value=1.0 / step, unit="VAMP it/s", cores=int(threads), kind="port",
+                host_cpus=os.cpu_count(), extrapolated=True,
+                sample="extrapolated: oracle/vamp_oracle.py (NumPy + OpenBLAS, %d threads) on LD "
+                       "blocks 0-%d (%d markers, %.1f GB dense), all %d cohorts, %d iterations "
+                       "in %.2f s: %.1f ms per single-column mat-vec per LD block, %.1f ms of "
+                       "non-LD work per step scaled to M=%d; full step = %.1f ms non-LD + %d "
+                       "blocks x %.1f mat-vecs per step (the reference's count with the GPU "
+                       "run's CG iterations) = %.2f s" % (
+                           threads, S - 1, n, sum(b * b for b in eng.block_sizes[:S]) * 8 / 1e9, eng.K, its, dt,
+                           mv_block * 1e3, other * 1e3, eng.M, other * 1e3,
+                           len(eng.block_sizes), nmv, step))
 
 
 def main():
@@ -227,6 +282,9 @@ def main():
                                         bytes_launch, K, eng.M)
     if eng.M == 200000 and args.ridge == 0 and not args.lmmse_damp:
         cname = {1: "C2 (BASELINE.json configs[1])", 4: "C3 (BASELINE.json configs[2])"}.get(K, "custom")
+    elif eng.M == 1000000 and K == 4 and args.ridge == 0 and not args.lmmse_damp:
+        cname = ("north-star configuration (BASELINE.json north_star: LD mat-vec at M=1e6, K=4) "
+                 "on %d GPU(s)" % world)
     elif eng.M == 1000000 and K == 1 and args.ridge == 0 and not args.lmmse_damp:
         cname = "C4 (BASELINE.json configs[3]) on %d GPU(s)" % world
     elif eng.M == 1000000 and K == 8 and args.ridge == 0.1 and args.lmmse_damp:
@@ -283,7 +341,7 @@ def main():
     }
     if rank == 0 and world == 1 and args.cpu_baseline == "auto":
         log("[bench] cpu baseline ...")
-        result["cpu_baseline"] = cpu_baseline(eng, args, dict(flags, **run))
+        result["cpu_baseline"] = cpu_baseline(eng, args, dict(flags, **run), recs, x0)
     else:
         result["cpu_baseline"] = None
     if rank == 0:

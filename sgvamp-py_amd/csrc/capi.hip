@@ -62,11 +62,33 @@ struct LdPlan {
   double stored_bytes = 0.0, dense_bytes = 0.0;
 };
 
+// A/B tuning switches: an environment override is honoured only with
+// SGV_AB=1 (and then announced once on stderr); without it a set override is
+// ignored with a warning, so no stray variable changes a production run.
+static const char* ab_env(const char* name) {
+  const char* v = std::getenv(name);
+  if (!v) return nullptr;
+  const char* ab = std::getenv("SGV_AB");
+  const bool on = ab && ab[0] == '1';
+  static std::mutex mu;
+  static std::vector<std::string> told;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (std::find(told.begin(), told.end(), name) == told.end()) {
+      told.emplace_back(name);
+      std::fprintf(stderr, on ? "[sgvamp] A/B override %s=%s active (SGV_AB=1)\n"
+                              : "[sgvamp] %s=%s ignored: A/B overrides need SGV_AB=1\n",
+                   name, v);
+    }
+  }
+  return on ? v : nullptr;
+}
+
 // chunk-width class of the packed pass for nc columns (CW = 1024 >> cls);
 // SGV_SYM_WIDE=0 selects the narrower supported class (A/B tuning)
 static int sym_class(int nc) {
   static const int narrow = [] {
-    const char* e = std::getenv("SGV_SYM_WIDE");
+    const char* e = ab_env("SGV_SYM_WIDE");
     return (e && e[0] == '0') ? 1 : 0;
   }();
   const int base = nc <= 2 ? 0 : nc <= 4 ? 1 : nc <= 8 ? 2 : 3;
@@ -77,7 +99,7 @@ static int sym_class(int nc) {
 // 0 disables; per context: sgv_set_mfma_min
 static int mfma_min_default() {
   static const int v = [] {
-    const char* e = std::getenv("SGV_MFMA_MIN");
+    const char* e = ab_env("SGV_MFMA_MIN");
     return e ? std::atoi(e) : 3;
   }();
   return v;
@@ -85,7 +107,7 @@ static int mfma_min_default() {
 // CG loop driver: 1 (default) = pipelined, device-side control (cg_loop_dev);
 // 0 = host-side stop test per iteration (cg_loop).  Env SGV_CG_PIPE.
 static int cg_pipe_default() {
-  const char* e = std::getenv("SGV_CG_PIPE");
+  const char* e = ab_env("SGV_CG_PIPE");
   return (e && e[0] == '0') ? 0 : 1;
 }
 constexpr int CG_RING = 4;   // mirror slots of the pipelined CG
@@ -94,7 +116,7 @@ constexpr int NOUT_SLOTS = 3;   // pinned output slots (a writer reads one while
 // SGV_EM_FUSE=0: the device EM loop keeps three launches per step at one rank (A/B)
 static bool em_fuse_default() {
   static const bool v = [] {
-    const char* e = std::getenv("SGV_EM_FUSE");
+    const char* e = ab_env("SGV_EM_FUSE");
     return !(e && e[0] == '0');
   }();
   return v;
@@ -532,14 +554,14 @@ static int grow(sgv_ctx* c, double** buf, size_t* cap, size_t need) {
 
 // VALU-pass items dispatched largest first (env SGV_SYM_LPT=0: panel/chunk order)
 static bool sym_lpt() {
-  const char* e = std::getenv("SGV_SYM_LPT");
+  const char* e = ab_env("SGV_SYM_LPT");
   return !(e && e[0] == '0');
 }
 
 // panels per MFMA strip (env SGV_MFMA_STRIP, read when a plan is built; 1 =
 // one (panel, chunk) item per workgroup)
 static int mfma_strip_len() {
-  const char* e = std::getenv("SGV_MFMA_STRIP");
+  const char* e = ab_env("SGV_MFMA_STRIP");
   const int v = e ? std::atoi(e) : 8;
   return std::max(1, std::min(64, v));
 }
@@ -1325,7 +1347,7 @@ static int gather_f64(sgv_ctx* c, const double* d_send, double* d_recv, size_t c
 // SGV_EM_REP=0: with a communicator, one exchange per EM step instead (A/B)
 static bool em_rep_default() {
   static const bool v = [] {
-    const char* e = std::getenv("SGV_EM_REP");
+    const char* e = ab_env("SGV_EM_REP");
     return !(e && e[0] == '0');
   }();
   return v;

@@ -133,154 +133,6 @@ __global__ __launch_bounds__(256, OCC) void k_sym_pass(const SymItem* __restrict
   }
 }
 
-// k_sym_pass with a two-segment software pipeline (NC <= 2, RWI * NC <= 16):
-// a wave issues the loads of segment s + 1 -- across the sub-sweep boundary, of
-// the next sub-sweep's first segment -- before it consumes segment s, so 16 KiB
-// stay in flight per wave instead of 8 KiB draining to zero every segment pair
-// (k_sym_pass's compiled loop: issue s, consume s, issue s + 1, consume s + 1,
-// vmcnt(0)).  Past the wave's last sub-sweep the prefetch reads the chunk's P
-// values again (cache-resident, never used): the load count is the same on
-// every path, so the compiler drains nothing at a branch join.  Every sum is
-// formed in k_sym_pass's order: same bits.
-template <int NC, int RWI, int NSEG>
-__global__ __launch_bounds__(256, 2) void k_sym_pass_pl(const SymItem* __restrict__ items,
-                                                        PassArgs pa,
-                                                        double* __restrict__ rowpart,
-                                                        double* __restrict__ colpart) {
-  constexpr int CW = NSEG * 128;
-  static_assert(RWI * NC <= 16, "row results per sub-sweep");
-  static_assert(NSEG % 2 == 0, "ring of two segments");
-  __shared__ d2 cbw[4][NC][CW / 2];
-
-  const SymItem it = items[blockIdx.x];
-  if (pa.run && !ldg(pa.run)) return;   // no-op pass (pipelined CG past its stop test)
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-  const double* pp[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) pp[c] = pa.in[c] + it.voff;
-  const bool has_cols = it.c0 + it.nc > it.diag_end;   // uniform
-  if (has_cols) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-      for (int s = 0; s < NSEG; ++s) cbw[wid][c][s * 64 + lane] = d2{0.0, 0.0};
-  }
-  // this wave's sub-sweeps: rbase = sub * 4 RWI + wid RWI < H
-  const int nsw = it.H > wid * RWI ? (it.H - wid * RWI + 4 * RWI - 1) / (4 * RWI) : 0;
-  const int64_t coff = it.c0 - it.r0;
-
-  // loads of segment s of the sub-sweep whose first row is rb; rb < 0: dummy
-  // (the chunk's first P values, stride 0)
-  auto load_seg = [&](int rb, int s, d2* rv, d2* pv) {
-    const bool live = rb >= 0;                      // wave-uniform
-    const int rb0 = live ? rb : 0;
-    int64_t ws = live ? it.w : 0;
-    uint64_t base = live ? (uint64_t)(it.P + coff) : (uint64_t)(pp[0] + it.c0);
-    asm volatile("" : "+s"(base), "+s"(ws));        // opaque: no select turned into branches
-    const int jl = s * 128 + 2 * lane;
-    const bool valid = live && jl < it.nc;
-    const int jj = valid ? jl : (live ? 0 : 2 * lane);
-#pragma unroll
-    for (int r = 0; r < RWI; ++r) {
-      const int rr = min(rb0 + r, it.H - 1);
-      rv[r] = ldg_nt((const d2*)((const double*)base + rr * ws + jj));
-    }
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const d2 v = ldg((const d2*)(pp[c] + it.c0 + jj));
-      pv[c] = valid ? v : d2{0.0, 0.0};
-    }
-  };
-
-  d2 rvA[RWI], rvB[RWI], pvA[NC], pvB[NC];
-  load_seg(nsw > 0 ? wid * RWI : -1, 0, rvA, pvA);
-#pragma unroll 1
-  for (int sub = 0; sub < nsw; ++sub) {
-    const int rbase = sub * 4 * RWI + wid * RWI;   // panel-relative first row of this wave
-    const int rnext = sub + 1 < nsw ? rbase + 4 * RWI : -1;
-    double prow[RWI][NC];
-#pragma unroll
-    for (int r = 0; r < RWI; ++r) {
-      const int rr = rbase + r;
-      const int rrc = min(rr, it.H - 1);
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const double v = ldg(pp[c] + it.r0 + rrc);
-        prow[r][c] = rr < it.H ? v : 0.0;
-      }
-    }
-    double racc[RWI][NC];
-#pragma unroll
-    for (int r = 0; r < RWI; ++r)
-#pragma unroll
-      for (int c = 0; c < NC; ++c) racc[r][c] = 0.0;
-
-    auto consume = [&](int s, const d2* rv, const d2* pv) {
-#pragma unroll
-      for (int r = 0; r < RWI; ++r)
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          racc[r][c] = __builtin_fma(rv[r].x, pv[c].x, racc[r][c]);
-          racc[r][c] = __builtin_fma(rv[r].y, pv[c].y, racc[r][c]);
-        }
-      if (it.c0 + s * 128 >= it.diag_end) {         // wave-uniform: right of the diagonal block
-#pragma unroll
-        for (int c = 0; c < NC; ++c) {
-          d2 cv = cbw[wid][c][s * 64 + lane];
-#pragma unroll
-          for (int r = 0; r < RWI; ++r) {
-            cv.x = __builtin_fma(rv[r].x, prow[r][c], cv.x);
-            cv.y = __builtin_fma(rv[r].y, prow[r][c], cv.y);
-          }
-          cbw[wid][c][s * 64 + lane] = cv;
-        }
-      }
-    };
-#pragma unroll 1
-    for (int s = 0; s < NSEG; s += 2) {
-      load_seg(rbase, s + 1, rvB, pvB);
-      consume(s, rvA, pvA);
-      const bool last = s + 2 >= NSEG;              // then: next sub-sweep, or the dummy
-      load_seg(last ? rnext : rbase, last ? 0 : s + 2, rvA, pvA);
-      consume(s + 1, rvB, pvB);
-    }
-    // all RWI x NC row sums at once (halving reduction)
-    constexpr int P = Pow2Ceil<RWI * NC>::value;
-    constexpr int SH = (P >= 64) ? 0 : (P >= 32) ? 1 : (P >= 16) ? 2 : (P >= 8) ? 3
-                     : (P >= 4) ? 4 : (P >= 2) ? 5 : 6;
-    double v[P];
-#pragma unroll
-    for (int k = 0; k < P; ++k) v[k] = (k < RWI * NC) ? racc[k / NC][k % NC] : 0.0;
-    const double y = wave_reduce_many<P>(v);
-    const int idx = (lane >> SH) & (P - 1);
-    const int rr = idx / NC, cc = idx % NC;
-    if ((lane & ((1 << SH) - 1)) == 0 && idx < RWI * NC && rbase + rr < it.H)
-      rowpart[((int64_t)it.item * SYM_H + rbase + rr) * NC + cc] = y;
-  }
-
-  if (has_cols) {
-    __syncthreads();
-    d2* out = (d2*)(colpart + (int64_t)it.item * NC * CW);
-    for (int t = threadIdx.x; t < NC * CW / 2; t += 256) {
-      const int c = t / (CW / 2), q = t % (CW / 2);
-      const d2 a = cbw[0][c][q], b = cbw[1][c][q], e = cbw[2][c][q], f = cbw[3][c][q];
-      out[t] = d2{((a.x + b.x) + e.x) + f.x, ((a.y + b.y) + e.y) + f.y};
-    }
-  }
-}
-
-// SGV_SYM_PL=1: k_sym_pass_pl instead of k_sym_pass for NC <= 2 (A/B only).
-// Same bits; measured on one box (C2 blocks, 20 reps): NC=1 3.45-3.53 vs
-// 3.18-3.19 ms, NC=2 3.19-3.24 vs 3.26 ms, C2 bench 3.365 vs 3.338 ms per pass
-// -- no gain, so k_sym_pass stays the default.
-static bool sym_pl_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("SGV_SYM_PL");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
 // one workgroup per panel, FIN_Q threads per panel row (row t = r0 + (thread
 // & 255), part q = thread >> 8): part q sums the row's chunk row-parts
 // item_begin + q, + 2q, ... and the column parts of the block's earlier panels
@@ -335,13 +187,6 @@ template <int NC, int NSEG>
 static hipError_t launch_sym_nc(const SymItem* d_items, int nitems, const PassArgs& pa,
                                 double* rowpart, double* colpart, hipStream_t st) {
   constexpr int RWI = (NC <= 2) ? 8 : (NC <= 4) ? 4 : (NC <= 8) ? 2 : 1;   // RWI*NC <= 16
-  if constexpr (NC <= 2 && NSEG % 2 == 0) {
-    if (sym_pl_enabled()) {
-      hipLaunchKernelGGL((k_sym_pass_pl<NC, RWI, NSEG>), dim3(nitems), dim3(256), 0, st, d_items,
-                         pa, rowpart, colpart);
-      return hipGetLastError();
-    }
-  }
   hipLaunchKernelGGL((k_sym_pass<NC, RWI, NSEG>), dim3(nitems), dim3(256), 0, st, d_items, pa,
                      rowpart, colpart);
   return hipGetLastError();

@@ -10,8 +10,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# SGV_LIB: another build of the same library (same-box A/B runs in tools/)
-LIB_PATH = os.environ.get("SGV_LIB") or os.path.join(HERE, "libsgvamp_hip.so")
+LIB_PATH = os.path.join(HERE, "libsgvamp_hip.so")   # the in-tree build, nothing else
 
 SGV_OK = 0
 VEC_R, VEC_R1, VEC_XHAT1, VEC_XHAT2, VEC_SIG2U, VEC_X0 = range(6)
@@ -94,6 +93,20 @@ class HipError(RuntimeError):
     pass
 
 
+def ab_env(name):
+    """A/B tuning switch from the environment, honoured only with SGV_AB=1 (as
+    the library's own overrides); a set switch without it is ignored loudly."""
+    v = os.environ.get(name)
+    if v is None:
+        return None
+    if os.environ.get("SGV_AB") != "1":
+        import warnings
+
+        warnings.warn("%s=%s ignored: A/B overrides need SGV_AB=1" % (name, v))
+        return None
+    return v
+
+
 def load(path=LIB_PATH):
     """Load and type the library (cached).  Raises if it is absent."""
     global _lib
@@ -104,8 +117,9 @@ def load(path=LIB_PATH):
                        "`make -C sgvamp-py_amd/csrc` (there is no CPU fallback)" % path)
     lib = ctypes.CDLL(path)
     for name, args in _SIGS.items():
-        if os.environ.get("SGV_LIB") and not hasattr(lib, name):
-            continue   # A/B run against an older build (tools/gpu_ab_bitwise.sh)
+        if not hasattr(lib, name):
+            raise HipError("%s does not export %s: stale build -- rebuild with "
+                           "`make -C sgvamp-py_amd/csrc`" % (path, name))
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, ctypes.c_int)
@@ -184,14 +198,9 @@ class ProbeStream:
         self.key = np.ascontiguousarray(key, dtype=np.uint32).copy()
         self.pos = np.array([pos], dtype=np.int32)
         self.lib = load()
-        # A/B runs against an older build without sgv_probe_draw draw with numpy
-        self.rs = rs if os.environ.get("SGV_LIB") and not hasattr(self.lib, "sgv_probe_draw") \
-            else None
 
     def draw(self, n, lo, hi):
         """Advance by n samples; return u[lo:hi] as int8 +-1."""
-        if self.rs is not None:
-            return (self.rs.binomial(p=1 / 2, n=1, size=n) * 2 - 1)[lo:hi].astype(np.int8)
         out = np.empty(max(hi - lo, 1), dtype=np.int8)
         rc = self.lib.sgv_probe_draw(self.key.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
                                      self.pos.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),

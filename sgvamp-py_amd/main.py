@@ -5,9 +5,10 @@ Same flags, defaults, validation messages, log lines and output files
 {name}_cohort_{k}.csv, {name}_metrics.csv).  Differences:
 
 * one process per GPU instead of one MPI rank per cohort: a single process
-  handles all K cohorts (python main.py ...); for several GPUs launch with
-  ``python -m torch.distributed.run --nproc-per-node G main.py ...`` and the LD
-  blocks are sharded over the G ranks;
+  handles all K cohorts (python main.py ...); for several GPUs start G
+  processes with RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR and MASTER_PORT set
+  (any one-process-per-GPU launcher does) and the LD blocks are sharded over
+  the G ranks (host rendezvous: comm.SocketComm);
 * --seed (extension): seeds the Hutchinson probes per cohort, RandomState(seed+k)
   (the reference draws from the unseeded global RNG, src/sgvamp.py:326);
 * --bim-files may be omitted when every cohort has the same marker order;

@@ -336,7 +336,7 @@ class VAMP:
         sgv_outputs_begin, then write xhat1 and every r1, one file per task."""
         Nt = self.Nt
         out = self.engine.outputs_wait(slot)
-        if self._st["return_xhat"] and not os.environ.get("SGV_STEP") == "phases":
+        if self._st["return_xhat"] and not hb.ab_env("SGV_STEP") == "phases":
             self._xhat_loc[it] = out[0].copy()   # gathered in order by drain()
         futs = [self._write_pool.submit(lambda: self.write_xhat_to_file(
             it, out[0] / np.sqrt(Nt)))]                                              # :281
@@ -465,7 +465,7 @@ class VAMP:
         return (self._n_iter is not None and nxt < self._n_iter
                 and not (st["return_xhat"] and not self.write_files)
                 and not (st["prior_update"] == "mle" and nxt >= st["update_prior_from"])
-                and os.environ.get("SGV_STEP") != "nochain")
+                and hb.ab_env("SGV_STEP") != "nochain")
 
     def _begin_step(self, it, flags, u, chain):
         st = self._st
@@ -483,7 +483,7 @@ class VAMP:
         count is known), starts the file writers of finished iterations and hands
         the CSV rows to their writer -- so the GPU does not wait for Python
         between iterations.  Logs follow the step in the reference's order."""
-        if os.environ.get("SGV_STEP") == "phases":
+        if hb.ab_env("SGV_STEP") == "phases":
             return self._step_phases(it)
         st = self._st
         eng = self.engine

@@ -1,7 +1,9 @@
-"""N > 1 path on CPU: world_size-2 gloo.
+"""N > 1 path on CPU: world_size 2, over the product's host communicator
+(comm.SocketComm, the torch-free TCP rendezvous) and over torch.distributed
+gloo (test-side reference transport only; the product never imports torch).
 
-* the product's host communicator (comm.TorchGlooComm: RCCL-id bootstrap,
-  barrier, allgather) and block partition agree across ranks;
+* the host communicator (RCCL-id bootstrap, barrier, allgather) and the block
+  partition agree across ranks;
 * the sharded decomposition the GPU path uses -- each rank owns a contiguous
   range of LD blocks for all cohorts, every M-length sum is a per-block partial
   exchanged by all-gather and added in global block order -- reproduces the
@@ -27,6 +29,30 @@ def _free_port():
     return port
 
 
+class _TestGlooComm:
+    """torch.distributed gloo with the comm.SocketComm interface (test only)."""
+
+    def __init__(self):
+        import torch.distributed as dist
+
+        self.dist = dist
+        dist.init_process_group(backend="gloo", init_method="env://")
+        self.rank, self.size = dist.get_rank(), dist.get_world_size()
+
+    def bcast(self, obj, root=0):
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=root)
+        return box[0]
+
+    def allgather(self, obj):
+        out = [None] * self.size
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def barrier(self):
+        self.dist.barrier()
+
+
 class _GlooBlocks:
     def __init__(self, comm):
         self.comm = comm
@@ -35,14 +61,14 @@ class _GlooBlocks:
         return np.concatenate(self.comm.allgather(np.asarray(part)))
 
 
-def _rank(rank, world, port, case_name, q):
+def _rank(rank, world, port, case_name, q, kind):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                          WORLD_SIZE=str(world))
-        from comm import TorchGlooComm
+                          WORLD_SIZE=str(world), SGV_COMM_PORT=str(port))
+        from comm import world_from_env
         from partition import marker_offsets, partition_blocks
 
-        comm = TorchGlooComm()
+        comm = world_from_env() if kind == "socket" else _TestGlooComm()
         uid = comm.bcast(b"\x01" * 128 if rank == 0 else None, root=0)
         assert uid == b"\x01" * 128
         c = Case(case_name)
@@ -76,14 +102,15 @@ def _single(case_name):
                         reducer=red, **c.kwargs())
 
 
+@pytest.mark.parametrize("kind", ["socket", "gloo"])
 @pytest.mark.parametrize("case_name", ["k2_shared", "k1_blocks_csr_s_damp", "k4_shared_s_damp",
                                        "k1_mle", "k2_mle_L3"])
-def test_two_rank_sharded_run_is_bit_identical(case_name):
+def test_two_rank_sharded_run_is_bit_identical(case_name, kind):
     world = 2
     ctx = mp.get_context("fork")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, world, port, case_name, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, port, case_name, q, kind)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -102,3 +129,54 @@ def test_two_rank_sharded_run_is_bit_identical(case_name):
         np.testing.assert_array_equal(res[r][3], np.array(ref["cg_iters"]))
         assert res[r][4] == list(ref["em_steps"])
         np.testing.assert_array_equal(res[r][5], np.array(ref["metrics"]))
+
+
+def _comm_rank(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), SGV_COMM_PORT=str(port))
+        import sys
+
+        from comm import SocketComm, world_from_env
+
+        comm = world_from_env()
+        assert isinstance(comm, SocketComm) and "torch" not in sys.modules
+        out = {}
+        out["bcast"] = comm.bcast(("id", 7) if rank == 1 else None, root=1)
+        out["ag"] = comm.allgather({"r": rank})
+        out["f64"] = comm.allgather_f64(np.arange(3, dtype=np.float64) + 10 * rank)
+        out["empty"] = comm.allgather_f64(np.zeros(0))
+        big = np.random.RandomState(rank).normal(size=200_000)
+        out["big"] = float(comm.allgather_f64(big).sum())
+        comm.barrier()
+        comm.close()
+        q.put((rank, out))
+    except Exception:
+        import traceback
+
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_socket_comm_collectives(world):
+    """comm.SocketComm alone: rank order, bcast from a non-zero root, empty and
+    multi-MB payloads; torch is never imported."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    want_big = sum(float(np.random.RandomState(r).normal(size=200_000).sum()) for r in range(world))
+    for r in range(world):
+        out = res[r]
+        assert isinstance(out, dict), out
+        assert out["bcast"] == ("id", 7)
+        assert out["ag"] == [{"r": i} for i in range(world)]
+        np.testing.assert_array_equal(out["f64"], np.concatenate(
+            [np.arange(3.0) + 10 * i for i in range(world)]))
+        assert out["empty"].shape == (0,)
+        assert abs(out["big"] - want_big) < 1e-6

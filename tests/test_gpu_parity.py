@@ -238,6 +238,7 @@ def test_vamp_matches_reference_golden(name, packing, tmp_path, monkeypatch):
     device-side control (SGV_CG_PIPE=0)."""
     c = Case(name)
     if packing == "hostcg":
+        monkeypatch.setenv("SGV_AB", "1")
         monkeypatch.setenv("SGV_CG_PIPE", "0")
     if packing == "valu" and c.K == 1:
         pytest.skip("K = 1 never reaches 3 columns: same as packing=True")
@@ -285,6 +286,7 @@ def test_cg_pipeline_matches_host_loop(name, tmp_path, monkeypatch):
     the column count) bitwise identical trajectories and CSV files."""
     c = Case(name)
     out = {}
+    monkeypatch.setenv("SGV_AB", "1")
     for mode in ("0", "1"):
         monkeypatch.setenv("SGV_CG_PIPE", mode)
         d = tmp_path / mode
@@ -314,6 +316,7 @@ def test_step_driver_matches_phases(name, tmp_path, monkeypatch):
     (SGV_STEP=phases): every output file byte-identical, same CG/EM counts."""
     c = Case(name)
     res = {}
+    monkeypatch.setenv("SGV_AB", "1")
     for mode in ("phases", "nochain", ""):
         monkeypatch.setenv("SGV_STEP", mode)
         d = tmp_path / (mode or "chain")
@@ -527,6 +530,7 @@ def test_mfma_strips_vs_numpy(strip, ncol, monkeypatch):
     """MFMA pass work items are strips of up to SGV_MFMA_STRIP panels of one
     parity sharing a 512-column chunk (sym_mfma.hip); blocks with up to 20
     panels, so chunks split into several strips at every setting."""
+    monkeypatch.setenv("SGV_AB", "1")
     monkeypatch.setenv("SGV_MFMA_STRIP", str(strip))
     sizes = [5000, 513, 2600, 1]
     blocks = rand_blocks(sizes, seed=strip + ncol, symmetric=True)
