@@ -30,6 +30,17 @@ __device__ __forceinline__ T ldg_nt(const T* p) {   // streaming (read-once) dat
   return __builtin_nontemporal_load((const SGV_GLOBAL T*)p);
 }
 
+// The value lane (l + 16 - N) mod 16 of the caller's 16-lane row holds (DPP
+// row_ror:N): a VALU move, no LDS round trip as __shfl_xor's ds_bpermute.
+template <int N>
+__device__ __forceinline__ double row_ror(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x120 + N, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x120 + N, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (long long)(((unsigned long long)(unsigned)hi << 32) |
+                                                (unsigned)lo));
+}
+
 // One LD block of one LD matrix: n x n dense f64, row-major, row stride lda
 // (multiple of PADV, zero padded); voff = offset of the block's first marker
 // in the padded device vector layout.

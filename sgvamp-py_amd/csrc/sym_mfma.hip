@@ -30,8 +30,9 @@
 //   row fragment  lane l: R[row 4q + (l&3)][col pair (l>>4) + 4b, + e] (q = 0..3)
 //       A_b[m][k] = R[row m][pair k+4b]: Drow[row][c] += R[j][i] P[i][c]
 // is read back without bank conflicts.  Each 4x4x4 block contracts its own 4
-// column pairs, so the 4 blocks' row partials are summed by two xor-shuffles
-// per row group (fixed order), then over the waves through LDS (wave order).
+// column pairs, so the 4 blocks' row partials are summed by two DPP row
+// rotations per row group (fixed order), then over the waves through LDS (wave
+// order).
 // Dcol accumulates over all rows of the strip in registers; every order is fixed.
 #include "common.h"
 
@@ -222,8 +223,10 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
 #pragma unroll
         for (int q = 0; q < NG; ++q) {
           double v = drow[r][q];
-          v = v + __shfl_xor(v, 4);
-          v = v + __shfl_xor(v, 8);
+          // lanes bq = 0: (v0 + v1) + (v2 + v3), block b's value at lane + 4b
+          // (DPP row rotations: VALU moves, no LDS round trip)
+          v = v + row_ror<12>(v);
+          v = v + row_ror<8>(v);
           if (bq == 0) rb[((4 * r + hi) << 4) + 4 * q + n4] = v;   // D row 4r + m (m = hi)
         }
       __syncthreads();
