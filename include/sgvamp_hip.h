@@ -104,6 +104,17 @@ int sgv_comm_init_host(sgv_ctx* ctx, int nranks, int rank, const int* nblk_per_r
  * Replaces the R loaders src/main.py:199-202 (dense .npy / CSR .npz blocks). */
 int sgv_set_ld_block(sgv_ctx* ctx, int ld, int blk_local, const double* rowmajor,
                      int64_t ld_host);
+/* Upload one symmetric LD block from the CSR arrays of its upper triangle
+ * (diagonal included; block-relative column indices >= the row; duplicates are
+ * summed).  Replaces the sparse loaders src/main.py:199-200 (.npz CSR of any
+ * sparsity) and :251-257 (PLINK .ld pairs assembled into CSR): a block whose
+ * entries lie within j - i <= bw is stored as a packed BAND -- panel g (rows
+ * 256g ..) keeps columns 256g .. 256g + round_up(256 + bw, 512) - 1 -- so
+ * windowed LD over a whole chromosome needs n * (bw + 256..767) doubles instead
+ * of n^2 / 2.  Blocks whose band is as wide as the triangle are stored as the
+ * packed triangle.  Never allocates n x n on the host. */
+int sgv_set_ld_block_csr(sgv_ctx* ctx, int ld, int blk_local, const int64_t* indptr /* n+1 */,
+                         const int64_t* indices, const double* data);
 /* R_s xhat2 and R_s Sigma2_u for gamw learning (src/sgvamp.py:352,359) and the
  * next warm start's R_s x0 (scipy iterative.py:392): on (default), carried
  * through both CG solves -- x_k = x_0 + sum a_i p_i, so R_s x_k = R_s x_0 +
@@ -128,10 +139,15 @@ int sgv_set_cg_pipeline(sgv_ctx* ctx, int on);
  * the bytes per pass: the LD matrix of src/main.py:199-265 is symmetric by
  * construction, R = X^T X); mode 0 always stores the full square. */
 int sgv_set_ld_packing(sgv_ctx* ctx, int mode);
-/* fmt_out: 0 dense, 1 packed symmetric, -1 not set. */
+/* fmt_out: 0 dense, 1 packed symmetric (triangle), 2 packed band, -1 not set. */
 int sgv_ld_block_format(sgv_ctx* ctx, int ld, int blk_local, int* fmt_out);
 /* Download one LD block (row-major n x n into a host array of row stride ld_host). */
 int sgv_get_ld_block(sgv_ctx* ctx, int ld, int blk_local, double* rowmajor, int64_t ld_host);
+/* Start a new VAMP.infer on this context (src/sgvamp.py:198-217 restarts from
+ * r1 = r, xhat2 = 0, Sigma2_u_prev = 0 on every call): zeroes every solver
+ * vector except r, r1 and x0 and clears the warm-start and chained-step state.
+ * LD blocks, ridge and cohort sizes are kept.  Fails while a step is queued. */
+int sgv_reset_solver(sgv_ctx* ctx);
 /* R_s = (1 - s) R + s I, applied inside every LD pass (src/main.py:265). */
 int sgv_set_ridge(sgv_ctx* ctx, double s);
 /* Cohort sample size N_k (src/main.py:83-85; used by gamw learning :352,363). */

@@ -256,6 +256,56 @@ class BlockLD:
         return (1 - self.s) * self.matvec_R(v) + self.s * v
 
 
+class CsrLD:
+    """A general sparse LD matrix R (scipy CSR, any sparsity pattern): the
+    reference's own operator for .npz and PLINK .ld inputs (src/main.py:199-200,
+    251-257), whose products are CSR mat-vecs inside scipy's cg
+    (src/sgvamp.py:312-316,332).  ``s`` as in BlockLD."""
+
+    def __init__(self, A, s=0.0):
+        self.A = A.tocsr()
+        self.s = s
+
+    def matvec_R(self, v):
+        return self.A @ v
+
+    def matvec_Rs(self, v):
+        if self.s == 0.0:
+            return self.matvec_R(v)
+        return (1 - self.s) * self.matvec_R(v) + self.s * v
+
+
+def banded_ld(n, bw, seed=0, decay=None, taps=40):
+    """Test input: an exactly symmetric, positive semi-definite LD-like matrix
+    with unit diagonal whose entries vanish for |i - j| > bw (CSR), bandwidth
+    exactly bw.  R = B B^T with B lower-banded -- row i mixes the "haplotype
+    factors" i - k for k in a fixed set of `taps` offsets that includes 0 and bw
+    -- scaled to unit diagonal: the shape of windowed LD (PLINK --ld-window)
+    without its truncation artefacts, cheap to build at any n."""
+    import scipy.sparse
+
+    rs = np.random.RandomState(seed)
+    decay = decay or max(bw / 3.0, 1.0)
+    offs = {0, bw}
+    if bw > 1:
+        offs |= set(rs.choice(np.arange(1, bw), min(bw - 1, taps), replace=False).tolist())
+    rows, cols, vals = [], [], []
+    for k in sorted(offs):
+        i = np.arange(k, n)
+        rows.append(i)
+        cols.append(i - k)
+        vals.append(rs.normal(size=n - k) * np.exp(-k / decay) + (1.0 if k == 0 else 0.0))
+    B = scipy.sparse.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
+                                shape=(n, n))
+    R = (B @ B.T).tocsr()
+    d = 1.0 / np.sqrt(R.diagonal())
+    R = scipy.sparse.diags(d) @ R @ scipy.sparse.diags(d)
+    R = ((R + R.T) * 0.5).tocsr()
+    R.sum_duplicates()
+    R.sort_indices()
+    return R
+
+
 def cg_scipy(matvec, b, x0, maxiter, red, rtol=1e-5):
     """scipy 1.15.3 cg (iterative.py:375-422), with counters.
     Returns (x, info, n_iter, n_matvec)."""

@@ -36,6 +36,9 @@ static thread_local std::string g_last_err;
 struct LdBlock {
   double* ptr = nullptr;
   int fmt = 0;                 // 0: dense n x lda row-major; 1: packed symmetric panels
+  // packed band: panel g stores columns r0 .. r0 + min(n - r0, ext) - 1 only
+  // (ext a multiple of BAND_Q; 0 = the whole upper triangle)
+  int64_t ext = 0;
   std::vector<int64_t> poff, pw;   // packed: panel offsets and row strides (doubles)
   int64_t* d_poff = nullptr;
   int64_t* d_pw = nullptr;
@@ -491,15 +494,23 @@ static void free_block(LdBlock& lb) {
   lb = LdBlock();
 }
 
-// allocate block b of LD matrix ld in format fmt (zero filled)
-static int ld_alloc(sgv_ctx* c, int ld, int b, int fmt) {
+// stored columns of panel g (first row r0) of an n-row packed block
+static int64_t panel_ext(int64_t n, int64_t r0, int64_t ext) {
+  return ext > 0 ? std::min(n - r0, ext) : n - r0;
+}
+
+// allocate block b of LD matrix ld in format fmt (zero filled); ext: packed
+// band extent (0 = full upper triangle)
+static int ld_alloc(sgv_ctx* c, int ld, int b, int fmt, int64_t ext = 0) {
   LdBlock& lb = c->ldb[ld][b];
-  if (lb.ptr && lb.fmt == fmt) return SGV_OK;
+  if (fmt == 0) ext = 0;
+  if (lb.ptr && lb.fmt == fmt && lb.ext == ext) return SGV_OK;
   free_block(lb);
   c->plan[ld].valid = false;
   const int64_t n = c->bn[b];
   size_t elems = 0;
   lb.fmt = fmt;
+  lb.ext = ext;
   if (fmt == 0) {
     elems = (size_t)c->lda[b] * (size_t)n;
     lb.stored_bytes = (double)n * (double)n * 8.0;
@@ -507,11 +518,12 @@ static int ld_alloc(sgv_ctx* c, int ld, int b, int fmt) {
     double valid = 0.0;
     for (int64_t r0 = 0; r0 < n; r0 += SYM_H) {
       const int64_t H = std::min<int64_t>(SYM_H, n - r0);
-      const int64_t w = round_up(n - r0, PADV);
+      const int64_t e = panel_ext(n, r0, ext);
+      const int64_t w = round_up(e, PADV);
       lb.poff.push_back((int64_t)elems);
       lb.pw.push_back(w);
       elems += (size_t)(H * w);
-      valid += (double)H * (double)(n - r0);
+      valid += (double)H * (double)e;
     }
     lb.stored_bytes = valid * 8.0;
     HIPCHK(hipMalloc(&lb.d_poff, sizeof(int64_t) * lb.poff.size()));
@@ -520,7 +532,20 @@ static int ld_alloc(sgv_ctx* c, int ld, int b, int fmt) {
                      hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(lb.d_pw, lb.pw.data(), sizeof(int64_t) * lb.pw.size(), hipMemcpyHostToDevice));
   }
-  HIPCHK(hipMalloc(&lb.ptr, sizeof(double) * elems));
+  {
+    const hipError_t e = hipMalloc(&lb.ptr, sizeof(double) * elems);
+    if (e != hipSuccess) {
+      lb.ptr = nullptr;
+      size_t fr = 0, tot = 0;
+      (void)hipGetLastError();
+      (void)hipMemGetInfo(&fr, &tot);
+      return fail(c, SGV_ERR_HIP,
+                  "LD matrix %d block %d (n=%lld, %s): %.2f GB of device memory needed, %.2f GB "
+                  "free: %s", ld, b, (long long)n,
+                  fmt == 0 ? "dense" : ext > 0 ? "packed band" : "packed triangle",
+                  sizeof(double) * (double)elems / 1e9, (double)fr / 1e9, hipGetErrorString(e));
+    }
+  }
   HIPCHK(hipMemsetAsync(lb.ptr, 0, sizeof(double) * elems, c->st));
   BlkDesc d{fmt == 0 ? lb.ptr : nullptr, c->lda[b], c->bn[b], c->bvoff[b]};
   HIPCHK(hipMemcpyAsync(c->d_blks[ld] + b, &d, sizeof d, hipMemcpyHostToDevice, c->st));
@@ -588,7 +613,11 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
       for (int64_t c0 = (int64_t)SYM_H * p; c0 < n; c0 += 2 * SYM_H) {
         const int G = (int)(c0 / SYM_H);
         const int sb = (int)strips.size();
-        for (int g0 = p; g0 <= G; g0 += 2 * S) {
+        // a band block's panel g reaches c0 iff c0 - 256 g < ext (ext a multiple
+        // of 512: the panels G - ext/256 + 2, ..., G of this parity)
+        const int64_t ext = c->ldb[ld][b].ext;
+        const int glo = ext > 0 ? std::max(p, G - (int)(ext / SYM_H) + 2) : p;
+        for (int g0 = glo; g0 <= G; g0 += 2 * S) {
           SymStrip st;
           st.it0 = (int)sitems.size();
           st.npan = 0;
@@ -664,7 +693,8 @@ static int ensure_plan(sgv_ctx* c, int ld) {
         const int r0 = (int)(g * SYM_H);
         const int H = (int)std::min<int64_t>(SYM_H, n - r0);
         const int ib = (int)items.size();
-        for (int64_t c0 = r0; c0 < n; c0 += cw) {
+        const int64_t cend = r0 + panel_ext(n, r0, lb.ext);
+        for (int64_t c0 = r0; c0 < cend; c0 += cw) {
           SymItem it;
           it.P = lb.ptr + lb.poff[g];
           it.w = lb.pw[g];
@@ -672,7 +702,7 @@ static int ensure_plan(sgv_ctx* c, int ld) {
           it.r0 = r0;
           it.H = H;
           it.c0 = (int32_t)c0;
-          it.nc = (int32_t)std::min<int64_t>(cw, n - c0);
+          it.nc = (int32_t)std::min<int64_t>(cw, cend - c0);
           it.item = (int32_t)items.size();
           it.diag_end = r0 + H;
           items.push_back(it);
@@ -686,7 +716,8 @@ static int ensure_plan(sgv_ctx* c, int ld) {
         pn.g = (int)g;
         pn.blk_panel0 = blk_panel0;
         pn.part = pbeg[b] + (int)g;
-        pn.pad_ = 0;
+        // first earlier panel whose stored columns cover this panel's rows
+        pn.gmin = lb.ext > 0 ? std::max<int>(0, (int)g - (int)(lb.ext / SYM_H) + 1) : 0;
         pn.own_sb = pn.own_se = pn.oth_sb = pn.oth_se = 0;
         panels.push_back(pn);
       }
@@ -1478,6 +1509,26 @@ static bool host_symmetric(const double* A, int64_t n, int64_t ld) {
   return true;
 }
 
+// Start a new infer() on the same context (src/sgvamp.py:198-217 resets r1,
+// xhat1, xhat2, Sigma2_u_prev and the scalars every call): every solver vector
+// except r, r1 and x0 is zeroed, the warm-start flags and the chained-step
+// inputs are cleared.  LD blocks, ridge and cohort sizes stay.
+extern "C" int sgv_reset_solver(sgv_ctx* c) {
+  ENTER(c);
+  if (c->job_ended != c->job_begun)
+    return fail(c, SGV_ERR_STATE, "sgv_reset_solver: a step is still queued");
+  const size_t n = sizeof(double) * (size_t)c->Mpad;
+  for (auto* v : {&c->r2, &c->U, &c->X, &c->X0, &c->Rr, &c->P, &c->Q, &c->RX0, &c->Y, &c->RXp})
+    for (double* d : *v) HIPCHK(hipMemsetAsync(d, 0, n, c->st));
+  HIPCHK(hipMemsetAsync(c->xhat1, 0, n, c->st));
+  CHK(stream_wait(c));
+  std::fill(c->xnz.begin(), c->xnz.end(), 0);
+  std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), 0);
+  c->chain.valid = 0;
+  c->met_pending = 0;
+  return SGV_OK;
+}
+
 extern "C" int sgv_set_rs_recurrence(sgv_ctx* c, int on) {
   ENTER(c);
   c->rs_rec = on ? 1 : 0;
@@ -1528,6 +1579,58 @@ extern "C" int sgv_set_ld_block(sgv_ctx* c, int ld, int b, const double* host, i
   return SGV_OK;
 }
 
+// Upper triangle (diagonal included) of a symmetric LD block as CSR, block-
+// relative: row i holds columns indices[indptr[i] .. indptr[i+1]) (each >= i,
+// duplicates summed).  Stored packed; when the entries stay within a band
+// j - i <= bw and the band's panels are narrower than the triangle, only the
+// band is stored (panel extent round_up(256 + bw, BAND_Q) columns).  Panels
+// are assembled in pinned host memory one at a time, no n x n buffer.
+extern "C" int sgv_set_ld_block_csr(sgv_ctx* c, int ld, int b, const int64_t* indptr,
+                                    const int64_t* indices, const double* data) {
+  ENTER(c);
+  if (ld < 0 || ld >= c->nld || b < 0 || b >= c->nblk || !indptr || (!indices && indptr[c->bn[b]]) ||
+      (!data && indptr[c->bn[b]]))
+    return fail(c, SGV_ERR_ARG, "sgv_set_ld_block_csr: bad arguments (ld=%d b=%d)", ld, b);
+  const int64_t n = c->bn[b];
+  if (indptr[0] != 0) return fail(c, SGV_ERR_ARG, "sgv_set_ld_block_csr: indptr[0] != 0");
+  int64_t bw = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (indptr[i + 1] < indptr[i])
+      return fail(c, SGV_ERR_ARG, "sgv_set_ld_block_csr: indptr decreases at row %lld",
+                  (long long)i);
+    for (int64_t e = indptr[i]; e < indptr[i + 1]; ++e) {
+      const int64_t j = indices[e];
+      if (j < i || j >= n)
+        return fail(c, SGV_ERR_ARG,
+                    "sgv_set_ld_block_csr: entry (%lld, %lld) outside the upper triangle of a "
+                    "%lld-marker block", (long long)i, (long long)j, (long long)n);
+      bw = std::max(bw, j - i);
+    }
+  }
+  int64_t ext = round_up(SYM_H + bw, BAND_Q);
+  if (ext >= n) ext = 0;   // the band is as wide as the triangle
+  CHK(ld_alloc(c, ld, b, 1, ext));
+  const LdBlock& lb = c->ldb[ld][b];
+  size_t pmax = 0;
+  for (size_t g = 0; g < lb.poff.size(); ++g) pmax = std::max<size_t>(pmax, SYM_H * lb.pw[g]);
+  CHK(ensure_hstage(c, sizeof(double) * pmax));
+  double* hp = (double*)c->h_stage;
+  for (size_t g = 0; g < lb.poff.size(); ++g) {
+    const int64_t r0 = (int64_t)g * SYM_H, H = std::min<int64_t>(SYM_H, n - r0);
+    const int64_t w = lb.pw[g];
+    std::memset(hp, 0, sizeof(double) * (size_t)(H * w));
+    for (int64_t i = r0; i < r0 + H; ++i)
+      for (int64_t e = indptr[i]; e < indptr[i + 1]; ++e) hp[(i - r0) * w + (indices[e] - r0)] += data[e];
+    for (int64_t a = 0; a < H; ++a)   // the panel's diagonal block is stored in full
+      for (int64_t d = a + 1; d < H; ++d) hp[d * w + a] = hp[a * w + d];
+    HIPCHK(hipMemcpyAsync(lb.ptr + lb.poff[g], hp, sizeof(double) * (size_t)(H * w),
+                          hipMemcpyHostToDevice, c->st));
+    CHK(stream_wait(c));   // the pinned panel buffer is reused
+  }
+  std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), 0);
+  return SGV_OK;
+}
+
 extern "C" int sgv_get_ld_block(sgv_ctx* c, int ld, int b, double* host, int64_t ld_host) {
   ENTER(c);
   if (ld < 0 || ld >= c->nld || b < 0 || b >= c->nblk || !host || ld_host < c->bn[b])
@@ -1541,10 +1644,12 @@ extern "C" int sgv_get_ld_block(sgv_ctx* c, int ld, int b, double* host, int64_t
                        sizeof(double) * n, n, hipMemcpyDeviceToHost));
     return SGV_OK;
   }
+  if (lb.ext > 0)   // outside the band nothing is stored
+    for (int64_t i = 0; i < n; ++i) std::memset(host + i * ld_host, 0, sizeof(double) * n);
   for (size_t g = 0; g < lb.poff.size(); ++g) {
     const int64_t r0 = (int64_t)g * SYM_H, H = std::min<int64_t>(SYM_H, n - r0);
     HIPCHK(hipMemcpy2D(host + r0 * ld_host + r0, sizeof(double) * ld_host, lb.ptr + lb.poff[g],
-                       sizeof(double) * lb.pw[g], sizeof(double) * (n - r0), H,
+                       sizeof(double) * lb.pw[g], sizeof(double) * panel_ext(n, r0, lb.ext), H,
                        hipMemcpyDeviceToHost));
   }
   for (int64_t i = 0; i < n; ++i) {          // mirror the part left of each panel
@@ -1558,7 +1663,8 @@ extern "C" int sgv_ld_block_format(sgv_ctx* c, int ld, int b, int* fmt_out) {
   ENTER(c);
   if (ld < 0 || ld >= c->nld || b < 0 || b >= c->nblk || !fmt_out)
     return fail(c, SGV_ERR_ARG, "sgv_ld_block_format: bad arguments");
-  *fmt_out = c->ldb[ld][b].ptr ? c->ldb[ld][b].fmt : -1;
+  const LdBlock& lb = c->ldb[ld][b];
+  *fmt_out = lb.ptr ? (lb.fmt == 1 && lb.ext > 0 ? 2 : lb.fmt) : -1;
   return SGV_OK;
 }
 
@@ -2354,6 +2460,7 @@ extern "C" int sgv_step(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
       !alpha2_prev || !probes || !res || !ires || !out || !cg_out || out_slot >= NOUT_SLOTS)
     return fail(c, SGV_ERR_ARG, "sgv_step: bad arguments");
   const int K = c->K;
+  c->chain.valid = 0;   // a step chained behind this one fails unless this one completes
   res[0] = 0.0;
   ires[0] = 0;
   // this step's probes go up now, behind nothing: the copy overlaps EM/denoiser

@@ -71,6 +71,10 @@ struct RowGroup {
 
 // ---- packed symmetric LD blocks (sym_pass.hip) ----------------------------
 constexpr int SYM_H = 256;   // rows per panel
+// packed band blocks: a panel's stored column extent is a multiple of BAND_Q, so
+// every item of an MFMA strip (512-column chunk) covers the same columns and the
+// earlier panels covering a panel's rows are a contiguous range
+constexpr int BAND_Q = 512;
 // one (panel, column chunk) work item of k_sym_pass
 struct SymItem {
   const double* P;   // panel base: element (r0, r0)
@@ -89,7 +93,8 @@ struct SymPanel {
   int32_t g;                     // panel index inside its block
   int32_t blk_panel0;            // index (in the panel table) of the block's first panel
   int32_t part;                  // partial slot
-  int32_t pad_;
+  int32_t gmin;                  // first earlier panel of the block storing columns of this
+                                 // panel's rows (0 unless the block is a packed band)
   // MFMA strips (k_sym_finalize_strip): the column sums of this panel's rows
   // sit in the strips of two 512-column chunks -- the chunk starting at r0 (the
   // panels of this panel's parity, row offset 0) and the one starting at

@@ -165,7 +165,8 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize(const SymPanel* __
     for (int c = 0; c < NC; ++c) y[c] += ldg(rp + c);
   }
   // column parts of the earlier panels of this block, panel order within the part
-  for (int g0 = 0; g0 < pn.g; g0 += PCH) {
+  // (band blocks: only the panels gmin .. g-1 store columns of these rows)
+  for (int g0 = pn.gmin; g0 < pn.g; g0 += PCH) {
     const int gn = min(PCH, pn.g - g0);
     __syncthreads();
     for (int k = threadIdx.x; k < gn; k += 256 * FIN_Q)

@@ -77,6 +77,21 @@ class Engine:
             raise ValueError("LD block %d has shape %s, expected (%d, %d)" % (b_global, B.shape, n, n))
         self.ctx.sgv_set_ld_block(ld, b_global - self.b0, hb.dptr(B), n)
 
+    def set_ld_block_csr(self, ld, b_global, upper):
+        """Upload LD block b_global from the scipy CSR of its upper triangle
+        (block-relative, diagonal included) if this rank owns it; stored as a
+        packed band when the entries stay near the diagonal (sgv_set_ld_block_csr)."""
+        if not (self.b0 <= b_global < self.b1):
+            return
+        n = self.block_sizes[b_global]
+        if upper.shape != (n, n):
+            raise ValueError("LD block %d has shape %s, expected (%d, %d)" % (b_global, upper.shape, n, n))
+        indptr = np.ascontiguousarray(upper.indptr, dtype=np.int64)
+        indices = np.ascontiguousarray(upper.indices, dtype=np.int64)
+        data = np.ascontiguousarray(upper.data, dtype=np.float64)
+        self.ctx.sgv_set_ld_block_csr(ld, b_global - self.b0, indptr.ctypes.data_as(hb._c_i64_p),
+                                      indices.ctypes.data_as(hb._c_i64_p), hb.dptr(data))
+
     def get_ld_block(self, ld, b_global):
         n = self.block_sizes[b_global]
         out = np.empty((n, n), dtype=np.float64)
@@ -95,6 +110,10 @@ class Engine:
     def set_rs_recurrence(self, on):
         """Carry R_s x through the CG (default) instead of a gamw LD pass."""
         self.ctx.sgv_set_rs_recurrence(1 if on else 0)
+
+    def reset_solver(self):
+        """Zero the solver state for a new infer() (src/sgvamp.py:198-217)."""
+        self.ctx.sgv_reset_solver()
 
     def set_ridge(self, s):
         self.ctx.sgv_set_ridge(float(s))

@@ -40,6 +40,7 @@ _SIGS = {
     "sgv_set_mfma_min": [_vp, ctypes.c_int],
     "sgv_set_cg_pipeline": [_vp, ctypes.c_int],
     "sgv_set_rs_recurrence": [_vp, ctypes.c_int],
+    "sgv_reset_solver": [_vp],
     "sgv_outputs_begin": [_vp, ctypes.c_int],
     "sgv_outputs_wait": [_vp, ctypes.c_int, ctypes.POINTER(_c_dbl_p)],
     "sgv_mle_exp_max": [_vp, _c_dbl_p, ctypes.c_int, _c_dbl_p, _c_dbl_p],
@@ -47,6 +48,7 @@ _SIGS = {
                       _c_dbl_p],
     "sgv_set_ld_block": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, ctypes.c_int64],
     "sgv_get_ld_block": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, ctypes.c_int64],
+    "sgv_set_ld_block_csr": [_vp, ctypes.c_int, ctypes.c_int, _c_i64_p, _c_i64_p, _c_dbl_p],
     "sgv_set_ld_packing": [_vp, ctypes.c_int],
     "sgv_ld_block_format": [_vp, ctypes.c_int, ctypes.c_int, _c_int_p],
     "sgv_set_ridge": [_vp, ctypes.c_double],

@@ -10,8 +10,10 @@ Same constructor and ``infer`` arguments, same log lines, same output files
   own a contiguous range of LD blocks.  Hence ``N`` is the list of per-cohort
   sample sizes (a scalar is accepted for K = 1), and ``R``/``r`` hold every
   cohort (``R``: one ``BlockLD`` shared by all cohorts, or a list of K);
-* the LD matrix is block-diagonal and handed over as dense diagonal blocks
-  (``BlockLD``); ``R_s = (1 - s) R + s I`` is applied inside the LD pass;
+* the LD matrix is handed over as its block-diagonal structure (``BlockLD``:
+  dense blocks, or sparse blocks stored as packed bands on the device, so
+  windowed/banded LD of any size is accepted); ``R_s = (1 - s) R + s I`` is
+  applied inside the LD pass;
 * the Hutchinson probes come from ``RandomState(seed + k)`` per cohort, the
   stream the reference draws after ``np.random.seed(seed + rank)``
   (src/sgvamp.py:326; the reference itself never seeds);
@@ -31,23 +33,45 @@ from engine import Engine
 from partition import detect_blocks_csr, detect_blocks_dense
 
 
+# Largest LD block densified on the host (n x n f64).  Symmetric CSR blocks never
+# are (they go up as CSR and are stored as a packed band or triangle); this
+# bounds non-symmetric sparse blocks and the dense-storage mode.
+DENSE_BLOCK_LIMIT = int(os.environ.get("SGV_DENSE_BLOCK_LIMIT", str(16 << 30)))
+
+
+def _dense_guard(n, why):
+    need = 8.0 * n * n
+    if need > DENSE_BLOCK_LIMIT:
+        raise ValueError(
+            "LD block of %d markers would be densified (%s): %.1f GB exceeds the dense-block "
+            "limit of %.1f GB (SGV_DENSE_BLOCK_LIMIT).  Symmetric sparse/banded LD is stored as "
+            "a packed band instead; check that the LD matrix is symmetric and dense storage is "
+            "not forced." % (n, why, need / 1e9, DENSE_BLOCK_LIMIT / 1e9))
+
+
 class BlockLD:
-    """Block-diagonal LD matrix: dense f64 diagonal blocks in marker order.
+    """Block-diagonal LD matrix: diagonal blocks in marker order, each from a
+    dense loader or (sparse sources) a CSR loader.
 
-    ``s`` is the ridge of src/main.py:265 (R_s = (1-s) R + s I); it is applied
-    on the device, the blocks stay unregularised."""
+    Dense blocks go to the device as they are; a symmetric CSR block goes up as
+    the CSR of its upper triangle and is stored as a packed band when its entries
+    stay near the diagonal (windowed LD: the reference's .npz / PLINK .ld paths,
+    src/main.py:199-200,251-257), without ever being densified.  ``s`` is the
+    ridge of src/main.py:265 (R_s = (1-s) R + s I); it is applied on the device,
+    the blocks stay unregularised."""
 
-    def __init__(self, blocks=None, block_sizes=None, loader=None, s=0.0):
+    def __init__(self, blocks=None, block_sizes=None, loader=None, s=0.0, csr_loader=None):
         if blocks is not None:
             self._blocks = [np.asarray(b, dtype=np.float64) for b in blocks]
             self.block_sizes = [b.shape[0] for b in self._blocks]
             self._loader = None
         else:
-            if block_sizes is None or loader is None:
+            if block_sizes is None or (loader is None and csr_loader is None):
                 raise ValueError("BlockLD needs blocks, or block_sizes and a loader")
             self._blocks = None
             self.block_sizes = [int(b) for b in block_sizes]
             self._loader = loader
+        self._csr_loader = csr_loader
         self.s = float(s)
 
     @property
@@ -55,9 +79,34 @@ class BlockLD:
         return int(sum(self.block_sizes))
 
     def block(self, b):
+        """Block b as a dense array."""
         if self._blocks is not None:
             return self._blocks[b]
+        if self._loader is None:
+            _dense_guard(self.block_sizes[b], "dense block requested")
+            return self._csr_loader(b).toarray()
         return np.asarray(self._loader(b), dtype=np.float64)
+
+    def block_csr(self, b):
+        """Block b as scipy CSR, or None for a dense source."""
+        return None if self._csr_loader is None else self._csr_loader(b).tocsr()
+
+    def upload(self, eng, ld, b, packed=True):
+        """Put block b of this matrix into LD slot `ld` of the engine."""
+        A = self.block_csr(b) if packed else None
+        if A is not None:
+            if (A != A.T).nnz == 0:
+                import scipy.sparse
+
+                U = scipy.sparse.triu(A, format="csr")
+                U.sum_duplicates()
+                U.sort_indices()
+                eng.set_ld_block_csr(ld, b, U)
+                return
+            _dense_guard(self.block_sizes[b], "the block is not symmetric")
+        elif self._csr_loader is not None:
+            _dense_guard(self.block_sizes[b], "dense LD storage requested")
+        eng.set_ld_block(ld, b, self.block(b))
 
     @classmethod
     def from_dense(cls, R, block_sizes=None, s=0.0):
@@ -71,13 +120,15 @@ class BlockLD:
 
     @classmethod
     def from_csr(cls, A, block_sizes=None, s=0.0):
-        """A scipy CSR LD matrix (the reference's .npz path, src/main.py:199-200)."""
+        """A scipy sparse LD matrix (the reference's .npz path, src/main.py:199-200,
+        and the PLINK .ld assembly, :251-257), any sparsity pattern: blocks are the
+        finest block-diagonal partition of its pattern, each kept sparse."""
         A = A.tocsr()
         M = A.shape[0]
         sizes = block_sizes or detect_blocks_csr(A.indptr, A.indices, M)
         offs = np.concatenate([[0], np.cumsum(sizes)])
         return cls(block_sizes=sizes,
-                   loader=lambda b: A[offs[b]:offs[b + 1], offs[b]:offs[b + 1]].toarray(), s=s)
+                   csr_loader=lambda b: A[offs[b]:offs[b + 1], offs[b]:offs[b + 1]], s=s)
 
     def regroup(self, sizes):
         """The same matrix on a coarser partition (every boundary of ``sizes`` must
@@ -89,14 +140,23 @@ class BlockLD:
         if not set(theirs.tolist()) <= set(mine.tolist()):
             raise ValueError("partition is not a coarsening of the LD block structure")
 
+        def parts(b):
+            s0, s1 = theirs[b], theirs[b + 1]
+            return [j for j in range(len(self.block_sizes)) if mine[j] >= s0 and mine[j + 1] <= s1]
+
+        if self._csr_loader is not None:
+            import scipy.sparse
+
+            return BlockLD(block_sizes=sizes, s=self.s, csr_loader=lambda b: scipy.sparse.block_diag(
+                [self.block_csr(j) for j in parts(b)], format="csr"))
+
         def load(b):
             s0, s1 = theirs[b], theirs[b + 1]
             out = np.zeros((s1 - s0, s1 - s0))
-            for j in range(len(self.block_sizes)):
-                if mine[j] >= s0 and mine[j + 1] <= s1:
-                    o = mine[j] - s0
-                    n = self.block_sizes[j]
-                    out[o:o + n, o:o + n] = self.block(j)
+            for j in parts(b):
+                o = mine[j] - s0
+                n = self.block_sizes[j]
+                out[o:o + n, o:o + n] = self.block(j)
             return out
 
         return BlockLD(block_sizes=sizes, loader=load, s=self.s)
@@ -231,7 +291,7 @@ class VAMP:
         eng.set_ridge(s_vals.pop())
         for l, L in enumerate(uniq):
             for b in range(eng.b0, eng.b1):
-                eng.set_ld_block(l, b, L.block(b))
+                L.upload(eng, l, b, packed=self.ld_packing)
         rr = np.asarray(r, dtype=np.float64)
         rr = rr.reshape(K, -1) if rr.size == K * self.M else rr
         for k in range(K):
@@ -254,6 +314,7 @@ class VAMP:
         """Use an Engine whose LD blocks and r vectors are already on the device
         (e.g. generated there); sets r1 = r (src/sgvamp.py:204) and N_k."""
         self.engine = engine
+        self._begun = False
         for k in range(self.K):
             engine.set_vector(hb.VEC_R1, k, engine.get_vector(hb.VEC_R, k))
             engine.set_cohort_n(k, self.N_list[k])
@@ -287,7 +348,11 @@ class VAMP:
         self._unwritten = []       # finished iterations whose files are not started
         if self.engine is None:
             self._setup(R, r, x0)
+            self._ld_src = R
             self._has_x0 = x0 is not None
+        elif getattr(self, "_begun", False):
+            self._restart(R, r, x0)
+        self._begun = True
         K = self.K
         self._st = dict(gam1=[self.gam1] * K, gamw=[self.gamw] * K, alpha1=[0] * K,
                         alpha2=[0] * K, gamws=[[] for _ in range(K)], xhat1s=[],
@@ -319,6 +384,34 @@ class VAMP:
         gc.freeze()
         if self.rank == 0:
             logging.debug(f"a = {self.a}")
+
+    def _restart(self, R, r, x0):
+        """A further infer()/begin() on this object starts over as the reference's
+        infer does (src/sgvamp.py:198-217: r1 = r, xhat1 = xhat2 = Sigma2_u_prev
+        = 0); lam/omegas/gam carry over, as they are attributes there too.  A
+        different R rebuilds the engine; the same R keeps its LD on the device."""
+        if R is not None and R is not getattr(self, "_ld_src", None):
+            self.engine.close()
+            self.engine = None
+            self._setup(R, r, x0)
+            self._ld_src = R
+            self._has_x0 = x0 is not None
+            return
+        eng = self.engine
+        eng.reset_solver()
+        if r is not None:
+            rr = np.asarray(r, dtype=np.float64)
+            rr = rr.reshape(self.K, -1) if rr.size == self.K * self.M else rr
+            for k in range(self.K):
+                eng.set_vector(hb.VEC_R, k, rr[k].ravel())
+        for k in range(self.K):
+            eng.set_vector(hb.VEC_R1, k, eng.get_vector(hb.VEC_R, k))
+        if x0 is not None:
+            eng.set_vector(hb.VEC_X0, 0, np.asarray(x0, dtype=np.float64).ravel())
+            self._has_x0 = True
+        elif R is not None or r is not None:   # a new problem without a true signal
+            eng.set_vector(hb.VEC_X0, 0, np.zeros(self.M))
+            self._has_x0 = False
 
     def _draw_probe(self, k):
         """u_k = binomial(p=1/2, n=1, size=M)*2-1 (src/sgvamp.py:326), local slice:
@@ -523,7 +616,18 @@ class VAMP:
                 self._flush_until(it + 1 - hb.OUT_SLOTS, rec1)
             self._queued = dict(it=it + 1, h=self._begin_step(it + 1, flags1, u1, chain=True),
                                 flags=flags1, rec=rec1)
-        r = eng.step_end(h)
+        try:
+            r = eng.step_end(h)
+        except Exception:
+            # the step queued behind a failed one fails too (its chained inputs are
+            # gone): collect it so no later drain() completes it, then re-raise
+            if self._queued is not None:
+                try:
+                    eng.step_end(self._queued["h"])
+                except Exception:  # noqa: BLE001 -- the first error is the one raised
+                    pass
+                self._queued = None
+            raise
         if self.write_files:
             self._unwritten.append(it)
 

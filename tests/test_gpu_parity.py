@@ -544,3 +544,159 @@ def test_mfma_strips_vs_numpy(strip, ncol, monkeypatch):
     for j in range(ncol):
         assert maxrel(Y[j], L.matvec_Rs(V[j])) < 1e-12, j
     eng.close()
+
+
+def _infer_again(v, c, out_dir):  # noqa: ARG001
+    f = c.flags
+    lds = [BlockLD(blocks, s=f["s"]) for blocks in c.ld_blocks]
+    R = lds[0] if len(lds) == 1 else [lds[c.ld_of[k]] for k in range(c.K)]
+    return v.infer(R, c.r, f["iterations"], x0=c.x0, cg_maxit=f["cg_maxit"],
+                   em_prior_maxit=f["em_prior_maxit"], learn_gamw=f["learn_gamw"],
+                   lmmse_damp=f["lmmse_damp"], prior_update=f["prior_update"],
+                   update_prior_from=f["update_prior_from"])
+
+
+@pytest.mark.parametrize("name", ["k1_noem_fixgamw", "k4_shared_s_damp"])
+def test_second_infer_restarts(name, tmp_path):
+    """A second infer() on the same VAMP object restarts from r1 = r, xhat2 = 0,
+    Sigma2_u_prev = 0 (src/sgvamp.py:198-217); lam/omegas carry over as object
+    attributes, as in the reference.  Without a prior update the second run
+    matches the golden fixture again; with EM it equals a fresh object started
+    from the first run's lam/omegas (the device state left by run 1 is gone)."""
+    c = Case(name)
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    v, _ = run_vamp_case(c, tmp_path / "a")
+    lam1, om1 = v.lam, np.array(v.omegas, dtype=np.float64).copy()
+    v.setup_io(str(tmp_path / "b"), c.name)      # run 2's files in their own directory
+    xh2 = _infer_again(v, c, tmp_path / "b")
+    its = c.flags["iterations"]
+    Nt = sum(c.N)
+    if c.flags["prior_update"] in (None, "none"):
+        for it in range(its):
+            xb = np.fromfile(tmp_path / "b" / ("%s_xhat_it_%d.bin" % (name, it)))
+            assert maxrel(xb, c.xhat[it]) < 1e-8, (it, maxrel(xb, c.xhat[it]))
+            assert maxrel(xh2[it].ravel() / np.sqrt(Nt), c.xhat[it]) < 1e-8
+    else:
+        f = c.flags
+        (tmp_path / "c").mkdir()
+        lds = [BlockLD(blocks, s=f["s"]) for blocks in c.ld_blocks]
+        R = lds[0] if len(lds) == 1 else [lds[c.ld_of[k]] for k in range(c.K)]
+        a = np.array(c.N) / Nt
+        w = VAMP(N=c.N, Nt=Nt, M=c.M, K=c.K, rho=f["rho"], gamw=f["gamw"], gam1=f["gam1"], a=a,
+                 prior_vars=f["prior_vars"], prior_probs=f["prior_probs"],
+                 out_dir=str(tmp_path / "c"), out_name=c.name, seed=f["seed"])
+        w.lam, w.omegas = lam1, om1
+        xh3 = w.infer(R, c.r, its, x0=c.x0, cg_maxit=f["cg_maxit"],
+                      em_prior_maxit=f["em_prior_maxit"], learn_gamw=f["learn_gamw"],
+                      lmmse_damp=f["lmmse_damp"], prior_update=f["prior_update"],
+                      update_prior_from=f["update_prior_from"])
+        for it in range(its):
+            np.testing.assert_array_equal(xh2[it], xh3[it])
+        w.engine.close()
+    v.engine.close()
+
+
+# ---------------------------------------------------------------------------
+# non-block-diagonal (banded / windowed) LD: packed band storage
+# ---------------------------------------------------------------------------
+_BAND_CACHE = {}
+
+
+def _band_matrix(parts, seed=0):
+    """Block-diagonal matrix of banded blocks: parts = [(n, bw)] (bw None: a
+    dense random block).  Cached: the parametrized tests share them."""
+    import scipy.sparse
+
+    key = (tuple(parts), seed)
+    if key in _BAND_CACHE:
+        return _BAND_CACHE[key]
+    mats = []
+    for i, (n, bw) in enumerate(parts):
+        if bw is None:
+            mats.append(scipy.sparse.csr_matrix(rand_blocks([n], seed=seed + i)[0]))
+        else:
+            mats.append(vo.banded_ld(n, bw, seed=seed + i))
+    _BAND_CACHE[key] = scipy.sparse.block_diag(mats, format="csr")
+    return _BAND_CACHE[key]
+
+
+@pytest.mark.parametrize("parts", [[(5000, 300)], [(2100, 100), (700, None), (3000, 1000)],
+                                   [(1030, 5), (4000, 40)], [(4000, 1200)]])
+@pytest.mark.parametrize("ncol", [1, 2, 3, 8, 13, 16])
+@pytest.mark.parametrize("s", [0.0, 0.1])
+@pytest.mark.parametrize("kern", ["packed", "packed_valu"])
+def test_ld_matvec_band_vs_scipy(parts, ncol, s, kern):
+    """Sparse symmetric LD uploaded as CSR (sgv_set_ld_block_csr): a block whose
+    band is narrower than its triangle is stored as a packed band (format 2),
+    otherwise as the packed triangle (1); the pass equals scipy's CSR mat-vec
+    (the reference's operator, src/sgvamp.py:316) to 1e-12."""
+    A = _band_matrix(parts, seed=3)
+    L = BlockLD.from_csr(A, s=s)
+    assert L.block_sizes == [n for n, _ in parts]
+    eng = Engine(L.block_sizes, K=1)
+    eng.set_ridge(s)
+    if kern == "packed_valu":
+        eng.set_mfma_min(0)
+    for b in range(len(parts)):
+        L.upload(eng, 0, b)
+    for b, (n, bw) in enumerate(parts):
+        band = bw is not None and -(-(256 + bw) // 512) * 512 < n
+        assert eng.ld_block_format(0, b) == (2 if band else 1), (b, n, bw)
+    rs = np.random.RandomState(ncol)
+    V = rs.normal(size=(ncol, A.shape[0]))
+    Y = eng.ld_matvec(0, V)
+    ref = vo.CsrLD(A, s=s)
+    for j in range(ncol):
+        want = ref.matvec_Rs(V[j])
+        assert maxrel(Y[j], want) < 1e-12, (j, maxrel(Y[j], want))
+    eng.close()
+
+
+def test_band_block_roundtrip():
+    """get_ld_block of a band block: the stored band, zeros outside it."""
+    A = _band_matrix([(1500, 200)], seed=11)
+    L = BlockLD.from_csr(A)
+    eng = Engine(L.block_sizes, K=1)
+    L.upload(eng, 0, 0)
+    assert eng.ld_block_format(0, 0) == 2
+    np.testing.assert_array_equal(eng.get_ld_block(0, 0), A.toarray())
+    eng.close()
+
+
+@pytest.mark.parametrize("K,s,damp", [(1, 0.0, False), (1, 0.05, True), (4, 0.05, True)])
+def test_vamp_band_ld_vs_oracle(K, s, damp, tmp_path):
+    """Whole VAMP iterations on one banded (not block-diagonal) LD matrix of
+    8,000 markers, bw = 600 -- the shape the reference's .npz / PLINK .ld paths
+    produce (src/main.py:199-200,251-257) -- against the oracle running scipy's
+    CSR mat-vec on the same matrix: xhat <= 1e-8 relative, CG counts and EM
+    steps exact."""
+    M, bw, N = 8000, 600, 5000
+    A = vo.banded_ld(M, bw, seed=21)
+    rs = np.random.RandomState(4)
+    cm = M // 20
+    beta = np.zeros(M)
+    beta[rs.choice(M, cm, replace=False)] = rs.normal(0, np.sqrt(0.5 / cm), cm) * np.sqrt(N)
+    r = [A @ beta + rs.normal(size=M) * np.sqrt(0.5) for _ in range(K)]
+    Ns = [float(N)] * K
+    Nt = sum(Ns)
+    a = np.array(Ns) / Nt
+    prior_vars, prior_probs = [0.0, 0.5 / cm], [0.95, 0.05]
+    L = BlockLD.from_csr(A, s=s)
+    v = VAMP(N=Ns, Nt=Nt, M=M, K=K, rho=0.5, gamw=2.0, gam1=1e-6, a=a, prior_vars=prior_vars,
+             prior_probs=prior_probs, out_dir=str(tmp_path), out_name="band", seed=9,
+             write_files=False)
+    its = 6
+    xh = v.infer(L, np.stack(r), its, x0=beta, lmmse_damp=damp, prior_update="em")
+    assert v.engine.ld_block_format(0, 0) == 2
+    t = vo.infer([vo.CsrLD(A, s=s)], [0] * K, r, Ns, its, rho=0.5, gamw=2.0, gam1=1e-6,
+                 prior_vars=prior_vars, prior_probs=prior_probs, x0=beta, seed=9,
+                 lmmse_damp=damp, reducer=vo.Reducer("blocked", bounds=np.array([0, M])),
+                 rs_recurrence=True)
+    for it in range(its):
+        ref = np.asarray(t["xhat"][it]).ravel()
+        got = xh[it].ravel() / np.sqrt(Nt)
+        assert maxrel(got, ref) < 1e-8, (it, maxrel(got, ref))
+    assert [h["cg_iters"] for h in v.history] == [[list(c) for c in x] for x in t["cg_iters"]]
+    assert [h.get("em_steps") for h in v.history][1:] == list(t["em_steps"])
+    v.engine.close()

@@ -1,0 +1,85 @@
+"""Host side of sparse / banded LD (CPU): a symmetric CSR LD matrix of any
+sparsity goes to the library as the CSR of each block's upper triangle and is
+never densified; non-symmetric blocks are densified only within a size limit,
+with a clear error instead of an n x n allocation (src/main.py:199-200,251-257
+hand the reference's cg such matrices)."""
+import numpy as np
+import pytest
+import scipy.sparse
+
+from oracle import vamp_oracle as vo
+from sgvamp import BlockLD
+
+
+class FakeEngine:
+    def __init__(self):
+        self.csr, self.dense = {}, {}
+
+    def set_ld_block_csr(self, ld, b, U):
+        self.csr[(ld, b)] = U
+
+    def set_ld_block(self, ld, b, B):
+        self.dense[(ld, b)] = B
+
+
+def test_banded_ld_goes_up_as_upper_csr_without_densifying():
+    M, bw = 200_000, 40            # dense: 320 GB; band: ~70 MB of CSR
+    A = vo.banded_ld(M, bw, seed=2)
+    L = BlockLD.from_csr(A)
+    assert L.block_sizes == [M]    # one block: the band links every marker
+    eng = FakeEngine()
+    L.upload(eng, 0, 0)
+    assert not eng.dense
+    U = eng.csr[(0, 0)]
+    rows = np.repeat(np.arange(M), np.diff(U.indptr))
+    assert np.all(U.indices >= rows) and np.max(U.indices - rows) == bw
+    assert abs(U.nnz - (A.nnz + M) // 2) == 0          # the upper triangle, diagonal included
+    np.testing.assert_array_equal((U + scipy.sparse.triu(U, 1).T).tocsr()[:50, :50].toarray(),
+                                  A[:50, :50].toarray())
+
+
+def test_block_diagonal_csr_splits_into_blocks():
+    A = scipy.sparse.block_diag([vo.banded_ld(300, 10, seed=1), vo.banded_ld(500, 60, seed=2)],
+                                format="csr")
+    L = BlockLD.from_csr(A)
+    assert L.block_sizes == [300, 500]
+    eng = FakeEngine()
+    for b in range(2):
+        L.upload(eng, 0, b)
+    assert set(eng.csr) == {(0, 0), (0, 1)} and not eng.dense
+    np.testing.assert_array_equal(L.block(1), A[300:, 300:].toarray())
+
+
+def test_nonsymmetric_large_block_fails_fast(monkeypatch):
+    import sgvamp
+
+    M = 50_000
+    A = vo.banded_ld(M, 8, seed=3).tolil()
+    A[0, 7] = A[0, 7] + 1e-3                 # no longer symmetric
+    L = BlockLD.from_csr(A.tocsr())
+    monkeypatch.setattr(sgvamp, "DENSE_BLOCK_LIMIT", 1 << 30)
+    with pytest.raises(ValueError, match="not symmetric"):
+        L.upload(FakeEngine(), 0, 0)
+    # dense storage forced (packing off) on a huge sparse block: same clear error
+    B = BlockLD.from_csr(vo.banded_ld(M, 8, seed=4))
+    with pytest.raises(ValueError, match="dense LD storage requested"):
+        B.upload(FakeEngine(), 0, 0, packed=False)
+
+
+def test_regroup_keeps_csr():
+    A1 = scipy.sparse.block_diag([vo.banded_ld(200, 4, seed=5), vo.banded_ld(100, 4, seed=6)],
+                                 format="csr")
+    L = BlockLD.from_csr(A1)
+    G = L.regroup([300])
+    eng = FakeEngine()
+    G.upload(eng, 0, 0)
+    np.testing.assert_array_equal(eng.csr[(0, 0)].toarray(), scipy.sparse.triu(A1).toarray())
+
+
+def test_banded_ld_generator_properties():
+    R = vo.banded_ld(1200, 100, seed=7)
+    assert (R != R.T).nnz == 0
+    np.testing.assert_allclose(R.diagonal(), 1.0, rtol=0, atol=1e-15)
+    rows = np.repeat(np.arange(1200), np.diff(R.indptr))
+    assert np.max(np.abs(R.indices - rows)) == 100
+    assert np.linalg.eigvalsh(R.toarray()).min() > -1e-12
