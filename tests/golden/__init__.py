@@ -8,6 +8,66 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
+def exact_ld(X, blocks):
+    """Block-diagonal LD of genotypes X (N x M, values 0/1/2) exactly as
+    G^T G with G = (X - mean) / (std * sqrt(N)) (the simulation recipe,
+    simulation/sim_gen_phen_mult.py:40,53-55), formed so every machine gets the
+    same bits: the integer Gram S = X^T X is exact in f64 BLAS (integer partial
+    sums < 2^53, any order), column sums and N*sum(x^2) - (sum x)^2 are exact
+    integers, and R_ij = (N S_ij - s_i s_j) / (sqrt(v_i) sqrt(v_j)) uses only
+    correctly rounded operations.  Returns the dense M x M matrix."""
+    X = np.asarray(X, dtype=np.float64)
+    N, M = X.shape
+    s1 = X.sum(axis=0).astype(np.int64)                      # exact (integers)
+    s2 = (X * X).sum(axis=0).astype(np.int64)
+    v = N * s2 - s1 * s1                                     # N^2 var, exact
+    sq = np.sqrt(v.astype(np.float64))
+    R = np.zeros((M, M))
+    o = 0
+    for n in blocks:
+        Xb = X[:, o:o + n]
+        S = np.rint(Xb.T @ Xb).astype(np.int64)              # exact integer Gram
+        num = N * S - np.outer(s1[o:o + n], s1[o:o + n])     # exact
+        R[o:o + n, o:o + n] = num.astype(np.float64) / np.outer(sq[o:o + n], sq[o:o + n])
+        o += n
+    return R
+
+
+def ld_checksum(R, blocks):
+    import hashlib
+
+    h = hashlib.sha256()
+    o = 0
+    for n in blocks:
+        h.update(np.ascontiguousarray(R[o:o + n, o:o + n]).tobytes())
+        o += n
+    return h.hexdigest()
+
+
+def regen_inputs(flags):
+    """The LD of an exact-recipe fixture, regenerated from its seed (the draws of
+    make_golden.make_inputs in the same order)."""
+    rs = np.random.RandomState(flags["seed"])
+    M, Ns, blocks = flags["M"], flags["N"], flags["blocks"]
+    lam_sim = flags.get("lam_sim", None)
+    cm = flags["_cm"]
+    rs.choice(M, cm, replace=False)
+    rs.normal(0, 1.0, cm)
+    Rs = []
+    for k, N in enumerate(Ns):
+        X = rs.binomial(2, 0.4, size=(N, M)).astype(np.float64)
+        if flags["distinct_ld"] or k == 0:
+            Rs.append(exact_ld(X, blocks))
+        if not flags["distinct_ld"]:
+            break
+        rs.normal(0.0, 1.0, size=N)                           # the noise draw of cohort k
+    del lam_sim
+    return Rs
+
+
+_REGEN = {}   # regenerated LD of the exact-recipe fixtures, per process
+
+
 def case_names():
     return sorted(os.path.splitext(os.path.basename(p))[0]
                   for p in glob.glob(os.path.join(HERE, "*.npz")))
@@ -31,9 +91,25 @@ class Case:
         sizes2 = [n * n for n in self.block_sizes]
         offs = np.cumsum([0] + sizes2)
         self.ld_blocks = []
-        for row in d["R_blocks"]:
-            self.ld_blocks.append([row[offs[b]:offs[b + 1]].reshape(n, n)
-                                   for b, n in enumerate(self.block_sizes)])
+        if "R_blocks" in d.files:
+            for row in d["R_blocks"]:
+                self.ld_blocks.append([row[offs[b]:offs[b + 1]].reshape(n, n)
+                                       for b, n in enumerate(self.block_sizes)])
+        elif name in _REGEN:
+            self.ld_blocks = _REGEN[name]
+        else:                         # exact recipe: regenerate, check the checksum
+            f["_cm"] = int(np.count_nonzero(self.beta))
+            want = [str(x) for x in d["R_sha256"]]
+            bounds = np.cumsum([0] + self.block_sizes)
+            for l, R in enumerate(regen_inputs(f)):
+                got = ld_checksum(R, self.block_sizes)
+                if got != want[l]:
+                    raise RuntimeError("%s: regenerated LD %d checksum %s != fixture %s"
+                                       % (name, l, got, want[l]))
+                self.ld_blocks.append([R[bounds[b]:bounds[b + 1], bounds[b]:bounds[b + 1]].copy()
+                                       for b in range(len(self.block_sizes))])
+            del f["_cm"]
+            _REGEN[name] = self.ld_blocks
         self.ld_of = list(range(self.K)) if f["distinct_ld"] else [0] * self.K
         self.xhat = d["xhat"]
         self.r1 = d["r1"]

@@ -44,10 +44,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # --------------------------------------------------------------------------
 # synthetic inputs (simulation/sim_gen_phen_mult.py:28-55, seeded)
 # --------------------------------------------------------------------------
-def make_inputs(seed, M, Ns, blocks, lam_sim=0.5, h2=0.8, distinct_ld=False):
+def make_inputs(seed, M, Ns, blocks, lam_sim=0.5, h2=0.8, distinct_ld=False, exact=False):
     """Each cohort k has its own genotypes X_k (sim_gen_phen_mult.py:36-39) and
     r_k = X_k^T y_k.  R_k = blockdiag(X_k,b^T X_k,b).  With shared LD every
-    cohort is given R_0 (cohort 0's LD used as the reference panel)."""
+    cohort is given R_0 (cohort 0's LD used as the reference panel).
+
+    exact=True: R is formed by tests.golden.exact_ld (bit-reproducible on any
+    IEEE machine, so the fixture stores a checksum instead of the matrix and
+    the tests regenerate it); everything else is the same recipe."""
     rs = np.random.RandomState(seed)
     cm = max(1, int(M * lam_sim))
     idx = rs.choice(M, cm, replace=False)
@@ -57,13 +61,21 @@ def make_inputs(seed, M, Ns, blocks, lam_sim=0.5, h2=0.8, distinct_ld=False):
     rvecs, Rs = [], []
     for k, N in enumerate(Ns):
         X = rs.binomial(2, 0.4, size=(N, M)).astype(np.float64)
+        if exact and (distinct_ld or k == 0):
+            sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+            from tests.golden import exact_ld
+
+            Rs.append(exact_ld(X, blocks))
         X = (X - X.mean(axis=0)) / X.std(axis=0)          # :40
         g = X @ beta                                      # :44 (before /sqrt(N))
         w = rs.normal(0.0, np.sqrt(1 - h2), size=N)       # :46
         y = g + w
         X /= np.sqrt(N)                                   # :53
         rvecs.append(X.T @ y)                             # :54
-        if distinct_ld or k == 0:
+        if exact:
+            if not (distinct_ld or k == 0):
+                Rs.append(Rs[0])
+        elif distinct_ld or k == 0:
             R = np.zeros((M, M))
             for b in range(len(blocks)):
                 s0, s1 = bounds[b], bounds[b + 1]
@@ -241,12 +253,27 @@ CASES = {
     "k4_shared_s_damp": dict(seed=17, M=320, N=[1000, 1200, 1400, 1600],
                              blocks=[160, 160], iterations=8, s=0.05, lmmse_damp=1,
                              update_prior_from=2, prior="auto", lam_sim=0.1),
+    # --- the north star's accuracy gate (xhat within 1e-5 after 50 iterations),
+    # pinned to the reference itself; R regenerated by the tests (exact=True) ---
+    # (rho = 0.3: with the default 0.5 these runs blow up to NaN within 15-45
+    # iterations -- in the reference as in the oracle -- which would gate nothing)
+    # K=1, three blocks, ridge, damping, EM: 50 iterations
+    "k1_long50": dict(seed=41, M=2400, N=[4000], blocks=[800, 900, 700], iterations=50,
+                      s=0.02, lmmse_damp=1, rho=0.3, prior="auto", lam_sim=0.1, exact=True),
+    # K=4 cohorts sharing one LD (MFMA pass), ridge, damping, EM: 50 iterations
+    "k4_long50": dict(seed=42, M=2000, N=[3000, 3500, 4000, 4500], blocks=[1000, 1000],
+                      iterations=50, s=0.02, lmmse_damp=1, rho=0.3, prior="auto", lam_sim=0.1,
+                      exact=True),
+    # C1 (BASELINE.json configs[0]): K=1, M=5000, N=10000, one dense block, 20
+    # iterations; the simulation recipe's 50 % causal markers, matched prior
+    "c1": dict(seed=43, M=5000, N=[10000], blocks=[5000], iterations=20, prior="auto",
+               lam_sim=0.5, exact=True),
 }
 
 DEFAULTS = dict(rho=0.5, gamw=5.0, gam1=1e-6, prior_vars=[0.0, 1.0],
                 prior_probs=[0.99, 0.01], cg_maxit=500, em_prior_maxit=100,
                 learn_gamw=1, lmmse_damp=0, s=0.0, prior_update="em",
-                update_prior_from=1, sparse=False, distinct_ld=False)
+                update_prior_from=1, sparse=False, distinct_ld=False, exact=False)
 
 
 def make_case(name, spec, workdir):
@@ -257,7 +284,8 @@ def make_case(name, spec, workdir):
     cfg["K"] = K
     lam_sim = cfg.get("lam_sim", 0.5)
     beta, rvecs, Rs = make_inputs(cfg["seed"], cfg["M"], cfg["N"], cfg["blocks"],
-                                  lam_sim=lam_sim, distinct_ld=cfg["distinct_ld"])
+                                  lam_sim=lam_sim, distinct_ld=cfg["distinct_ld"],
+                                  exact=cfg["exact"])
     prior = cfg.get("prior")
     if prior in ("auto", "auto3"):
         cm = max(1, int(cfg["M"] * lam_sim))
@@ -303,7 +331,7 @@ def make_case(name, spec, workdir):
                                  "gam1", "prior_vars", "prior_probs", "cg_maxit",
                                  "em_prior_maxit", "learn_gamw", "lmmse_damp", "s",
                                  "prior_update", "update_prior_from", "sparse",
-                                 "distinct_ld"]}
+                                 "distinct_ld", "exact"]}
     out = dict(
         flags=np.array(json.dumps(flags)),
         beta=beta,
@@ -316,9 +344,21 @@ def make_case(name, spec, workdir):
         warnings=np.array(json.dumps(list(results[0][2]))),
     )
     # R is block-diagonal by construction: store only the diagonal blocks,
-    # concatenated row-major, one row per distinct LD matrix.
+    # concatenated row-major, one row per distinct LD matrix -- or, for the
+    # exact recipe, only their checksum (the tests regenerate them).
     bounds = np.cumsum([0] + list(cfg["blocks"]))
     lds = Rs if cfg["distinct_ld"] else Rs[:1]
+    if cfg["exact"]:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+        from tests.golden import ld_checksum
+
+        out["R_sha256"] = np.array([ld_checksum(Rl, cfg["blocks"]) for Rl in lds])
+        path = os.path.join(HERE, name + ".npz")
+        np.savez_compressed(path, **out)
+        print("%-24s K=%d M=%d its=%d cg=%s em=%s -> %s (%d KB)" % (
+            name, K, M, its, cg[0, :, :, 0].tolist()[:3], em.tolist()[:4],
+            os.path.basename(path), os.path.getsize(path) // 1024))
+        return
     for Rl in lds:
         mask = np.ones(Rl.shape, dtype=bool)
         for b in range(len(cfg["blocks"])):
