@@ -121,35 +121,47 @@ def load_plink_ld_all(ld_paths, r, bim_ref, bim_list, N_list):
     touches a requested marker -- once per requested endpoint, so a pair whose
     two markers were both requested arrives twice and, summed, doubles -- and
     with its r at those markers; k appends the answers of j = 0..K-1 to its own
-    entries and overwrites r[source == j].  R = I + pairs + transposed pairs."""
+    entries and overwrites r[source == j].  R = I + pairs + transposed pairs.
+
+    The reference scans j's whole table once per requested marker
+    (O(requests x pairs), main.py:221-225); here one vectorised pass per (k, j)
+    selects the same entries in the same order (requested marker ascending,
+    then table order; oracle/ldio_oracle.py keeps the loop, tests compare)."""
     import scipy.sparse
 
     K = len(ld_paths)
     M = len(bim_ref)
     idx = {rs: i for i, rs in enumerate(bim_ref)}
-    own = [read_plink_ld(p, idx) for p in ld_paths]
+    own = [tuple(np.asarray(a) for a in read_plink_ld(p, idx)) for p in ld_paths]
+    own = [(A.astype(np.int64), B.astype(np.int64), C.astype(np.float64)) for A, B, C in own]
     sources = plink_ld_sources(bim_ref, bim_list, N_list)
     r_in = np.asarray(r, dtype=np.float64)
     r_out = r_in.copy()
     mats = []
     for k in range(K):
-        indA, indB, R_col = list(own[k][0]), list(own[k][1]), list(own[k][2])
+        parts_a, parts_b, parts_c = [own[k][0]], [own[k][1]], [own[k][2]]
         source = sources[k]
         for j in range(K):
             if j == k or j not in source:
                 continue
-            req = [i for i in range(M) if source[i] == j]
+            req = np.flatnonzero(source == j)
             jA, jB, jC = own[j]
-            for ind in req:
-                for i, corr in enumerate(jC):
-                    if jA[i] == ind or jB[i] == ind:
-                        indA.append(jA[i])
-                        indB.append(jB[i])
-                        R_col.append(corr)
+            want = np.zeros(M, dtype=bool)
+            want[req] = True
+            inA, inB = want[jA], want[jB] & (jB != jA)    # a self pair answers once
+            e = np.concatenate([np.flatnonzero(inA), np.flatnonzero(inB)])
+            key = np.concatenate([jA[inA], jB[inB]])          # the requested endpoint
+            order = np.lexsort((e, key))                      # by marker, then table order
+            e = e[order]
+            parts_a.append(jA[e])
+            parts_b.append(jB[e])
+            parts_c.append(jC[e])
             r_out[k][source == j] = r_in[j][req]
-        ind_r = list(range(M)) + indA + indB
-        ind_c = list(range(M)) + indB + indA
-        v = np.array(list(np.ones(M)) + R_col + R_col)
+        indA, indB, R_col = (np.concatenate(x) for x in (parts_a, parts_b, parts_c))
+        ar = np.arange(M)
+        ind_r = np.concatenate([ar, indA, indB])
+        ind_c = np.concatenate([ar, indB, indA])
+        v = np.concatenate([np.ones(M), R_col, R_col])
         mats.append(scipy.sparse.csr_matrix((v, (ind_r, ind_c)), shape=(M, M)))
     return mats, r_out
 

@@ -182,3 +182,54 @@ def test_plink_ld_exchange_source_quirk(tmp_path):
     np.testing.assert_array_equal(r_out[2], [11, 22, 23, 24, 25])
     np.testing.assert_array_equal(r_out[0], r[0])                # E never filled: r = 0
     assert mats[0].toarray()[4].tolist() == [0, 0, 0, 0, 1]
+
+
+def test_plink_exchange_vectorised_equals_reference_loop(tmp_path):
+    """The vectorised .ld exchange selects the same entries in the same order
+    as the reference's per-marker table scan (oracle/ldio_oracle.py restates
+    src/main.py:203-257): identical COO triplets, identical CSR (bitwise), on
+    three cohorts with missing markers, pairs whose both ends are requested
+    (sent twice) and self pairs."""
+    import scipy.sparse
+
+    from ldio import load_plink_ld_all, plink_ld_sources
+    from oracle import ldio_oracle
+
+    rs = np.random.RandomState(12)
+    M, K = 300, 3
+    ref = ["rs%d" % i for i in range(M)]
+    missing = [set(), set(rs.choice(M, 40, replace=False)), set(rs.choice(M, 25, replace=False))]
+    lists = [[x for i, x in enumerate(ref) if i not in missing[k]] for k in range(K)]
+    N = [1000, 1500, 1200]
+    tables = []
+    for k in range(K):
+        have = [i for i in range(M) if i not in missing[k]]
+        pairs = set()
+        while len(pairs) < 900:
+            a, b = sorted(rs.choice(have, 2))
+            if abs(a - b) < 30:
+                pairs.add((a, b))
+        pairs = sorted(pairs) + [(have[3], have[3])]          # a self pair
+        tables.append(pairs)
+        with open(tmp_path / ("c%d.ld" % k), "w") as fh:
+            fh.write(" CHR_A BP_A SNP_A CHR_B BP_B SNP_B R\n")
+            for a, b in pairs:
+                fh.write(" 1 %d %s 1 %d %s %r\n" % (a, ref[a], b, ref[b], float(rs.uniform(-.9, .9))))
+    r = rs.normal(size=(K, M))
+    paths = [str(tmp_path / ("c%d.ld" % k)) for k in range(K)]
+    mats, r_out = load_plink_ld_all(paths, r, ref, lists, N)
+    import pandas as pd
+
+    idx = {x: i for i, x in enumerate(ref)}
+    own = []
+    for p in paths:
+        df = pd.read_table(p, sep=r"\s+")
+        own.append(([idx[x] for x in df["SNP_A"]], [idx[x] for x in df["SNP_B"]], list(df["R"])))
+    trip, r_ref = ldio_oracle.exchange(own, plink_ld_sources(ref, lists, N), r, M)
+    np.testing.assert_array_equal(r_out, r_ref)
+    for k in range(K):
+        ind_r, ind_c, v = trip[k]
+        want = scipy.sparse.csr_matrix((np.array(v), (ind_r, ind_c)), shape=(M, M))
+        got = mats[k]
+        assert (got != want).nnz == 0
+        np.testing.assert_array_equal(got.toarray(), want.toarray())
