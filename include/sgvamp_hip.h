@@ -36,7 +36,8 @@ extern "C" {
 #define SGV_ERR_RCCL (-3)
 #define SGV_ERR_STATE (-4)
 
-#define SGV_MAX_COHORTS 8   /* 2K <= 16 right-hand sides per LD pass   */
+#define SGV_MAX_COHORTS 32  /* cohorts per context; the LMMSE batches them 8 at a
+                               time (16 CG right-hand sides per LD pass)          */
 #define SGV_MAX_SLABS 8     /* L - 1 slab components of the prior      */
 
 /* vector ids for sgv_set_vector / sgv_get_vector */

@@ -1819,7 +1819,7 @@ static int denoise_enqueue(sgv_ctx* c, const double* gam1s, const double* a, dou
     da.sq[l] = std::sqrt(da.s2[l] / sigmas[l]);         // np.sqrt(sigma2_meta / sigmas)
   }
   HIPCHK(launch_denoise(c->d_ch, c->nch, da, c->d_part, c->st));
-  CHK(reduce_dev(c, MAXK, c->d_ch_begin, identity_map(), c->h_tot));
+  CHK(reduce_dev(c, c->K, c->d_ch_begin, identity_map(), c->h_tot));
   return SGV_OK;
 }
 
@@ -1958,12 +1958,9 @@ static int mle_args(sgv_ctx* c, const double* gam1s, int L, const double* sigma2
   m->L = L;
   for (int k = 0; k < c->K; ++k) {
     m->r1[k] = c->r1[k];
-    const double ginv = 1.0 / gam1s[k];                       // :146
-    for (int l = 0; l < L; ++l) {
-      m->v[k][l] = sigma2[l] + ginv;                          // prior_vars0 + gam1invs
-      m->sv[k][l] = std::sqrt(m->v[k][l]);
-    }
+    m->ginv[k] = 1.0 / gam1s[k];                             // :146
   }
+  for (int l = 0; l < L; ++l) m->sigma2[l] = sigma2[l];
   return SGV_OK;
 }
 
@@ -1979,7 +1976,7 @@ extern "C" int sgv_mle_exp_max(sgv_ctx* c, const double* gam1s, int L, const dou
   // :152: max over (k, m, l) of (-r1^2 / 2) / v_kl, attained at min_m r1_km^2
   double best = -std::numeric_limits<double>::infinity();
   for (int k = 0; k < c->K; ++k)
-    for (int l = 0; l < L; ++l) best = std::max(best, -mn[k] / 2.0 / m.v[k][l]);
+    for (int l = 0; l < L; ++l) best = std::max(best, -mn[k] / 2.0 / (m.sigma2[l] + m.ginv[k]));
   *exp_max = best;
   return SGV_OK;
 }
@@ -2044,28 +2041,15 @@ extern "C" int sgv_outputs_wait(sgv_ctx* c, int slot, double** data) {
   return SGV_OK;
 }
 
-extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* gam2,
-                         const double* alpha1, const double* alpha2_prev, const int8_t* probes,
-                         int cg_maxit, double rtol, int lmmse_damp, double rho, int learn_gamw,
-                         double* out, int* cg_out, int* passes_out) {
-  ENTER(c);
-  (void)it;
-  if (!gamw || !gam2 || !alpha1 || !alpha2_prev || !probes || !out || !cg_out || cg_maxit < 0)
-    return fail(c, SGV_ERR_ARG, "sgv_lmmse: bad arguments");
-  const int K = c->K, ncol = 2 * K;
+// LMMSE of the cohorts g0 .. g0 + Kg - 1 (Kg <= MAXKG: 2 Kg <= MAXC CG columns,
+// one batched CG loop); per-cohort inputs/outputs are the group's slices
+static int lmmse_group(sgv_ctx* c, int g0, int Kg, const double* gamw, const double* gam2,
+                       const double* alpha1, const double* alpha2_prev, int cg_maxit, double rtol,
+                       int lmmse_damp, double rho, int learn_gamw, double* out, int* cg_out,
+                       int* passes_out) {
+  const int K = Kg, ncol = 2 * K;
   const double s = c->s;
   int passes = 0;
-
-  // probes u_k (:326), int8 +-1 -> f64; uploaded at the start of sgv_step, or now
-  int ps = c->pref_slot;
-  if (ps < 0 || c->pref_src != probes) CHK(probe_upload(c, probes, &ps));
-  c->pref_slot = -1;
-  c->pref_src = nullptr;
-  HIPCHK(hipStreamWaitEvent(c->st, c->ev_probe[ps], 0));
-  for (int k = 0; k < K; ++k)
-    HIPCHK(launch_unpack_i8(c->d_ch, c->nch, c->d_ch_doff,
-                            c->d_probe + ps * c->probe_cap + (size_t)k * c->Mloc, c->U[k], c->st));
-  HIPCHK(hipEventRecord(c->ev_unpk[ps], c->st));
 
   // warm start needs R_s x0: carried from the previous iteration (rs_rec), or the
   // previous gamw pass; a pass only when X was set from outside
@@ -2073,14 +2057,14 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
     PassArgs pa{};
     int nc = 0;
     for (int j = 0; j < ncol; ++j) {
-      if (!c->xnz[j] || c->rx0_valid[j] || c->ld_of[j / 2] != ld) continue;
-      pa.in[nc] = c->X[j];
-      pa.out[nc] = c->RX0[j];
+      if (!c->xnz[2 * g0 + j] || c->rx0_valid[2 * g0 + j] || c->ld_of[g0 + (j / 2)] != ld) continue;
+      pa.in[nc] = c->X[2 * g0 + j];
+      pa.out[nc] = c->RX0[2 * g0 + j];
       pa.dot[nc] = nullptr;
       pa.c1[nc] = 1.0 - s;
       pa.c2[nc] = s;
       ++nc;
-      c->rx0_valid[j] = 1;
+      c->rx0_valid[2 * g0 + j] = 1;
     }
     if (nc) {
       CHK(ld_pass(c, ld, nc, pa));
@@ -2094,36 +2078,36 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
   ia.K = K;
   ia.save_x0 = lmmse_damp;
   for (int k = 0; k < K; ++k) {
-    ia.cp.r[k] = c->r[k];
-    ia.cp.r1[k] = c->r1[k];
-    ia.cp.r2[k] = c->r2[k];
-    ia.cp.u[k] = c->U[k];
+    ia.cp.r[k] = c->r[g0 + k];
+    ia.cp.r1[k] = c->r1[g0 + k];
+    ia.cp.r2[k] = c->r2[g0 + k];
+    ia.cp.u[k] = c->U[g0 + k];
     ia.alpha1[k] = alpha1[k];
     ia.gamw[k] = gamw[k];
     ia.gam2[k] = gam2[k];
   }
   for (int j = 0; j < ncol; ++j) {
-    ia.col.X[j] = c->X[j];
-    ia.col.X0[j] = c->X0[j];
-    ia.col.Rr[j] = c->Rr[j];
-    ia.col.P[j] = c->P[j];
-    ia.col.Q[j] = c->Q[j];
-    ia.col.RX0[j] = c->RX0[j];
-    ia.col.RXp[j] = c->rs_rec ? c->RXp[j] : nullptr;
-    ia.warm[j] = c->xnz[j];
+    ia.col.X[j] = c->X[2 * g0 + j];
+    ia.col.X0[j] = c->X0[2 * g0 + j];
+    ia.col.Rr[j] = c->Rr[2 * g0 + j];
+    ia.col.P[j] = c->P[2 * g0 + j];
+    ia.col.Q[j] = c->Q[2 * g0 + j];
+    ia.col.RX0[j] = c->RX0[2 * g0 + j];
+    ia.col.RXp[j] = c->rs_rec ? c->RXp[2 * g0 + j] : nullptr;
+    ia.warm[j] = c->xnz[2 * g0 + j];
   }
   HIPCHK(launch_lmmse_init(c->d_ch, c->nch, ia, c->d_part, c->st));
   double tot[2 * MAXC];
   const bool dev_init = c->cg_pipe;   // CG prologue on the device: no host round trip
   if (dev_init) {
     CHK(reduce_dev(c, 2 * MAXC, c->d_ch_begin, identity_map(), c->d_tot));
-    HIPCHK(launch_cg_init(c->d_cgs, c->d_tot, rtol, ncol, c->d_ch, c->nch, c->X.data(),
-                          c->RX0.data(), c->st));
+    HIPCHK(launch_cg_init(c->d_cgs, c->d_tot, rtol, ncol, c->d_ch, c->nch, c->X.data() + 2 * g0,
+                          c->RX0.data() + 2 * g0, c->st));
   } else {
     CHK(reduce_host(c, 2 * MAXC, c->d_ch_begin, tot));
   }
   // carried: RX0 follows X through the CG; otherwise the gamw pass refreshes it
-  std::fill(c->rx0_valid.begin(), c->rx0_valid.end(), c->rs_rec ? 1 : 0);
+  for (int j = 0; j < ncol; ++j) c->rx0_valid[2 * g0 + j] = c->rs_rec ? 1 : 0;
 
   CgCols cc;
   cc.ncol = ncol;
@@ -2131,16 +2115,16 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
   int active[MAXC], iters[MAXC], info[MAXC];
   for (int j = 0; j < ncol; ++j) {
     const int k = j / 2;
-    cc.col_ld[j] = c->ld_of[k];
+    cc.col_ld[j] = c->ld_of[g0 + k];
     cc.c1[j] = gamw[k] * (1.0 - s);           // A = gamw R_s + gam2 I (:312)
     cc.c2[j] = gamw[k] * s + gam2[k];
-    cc.X[j] = c->X[j];
-    cc.Rr[j] = c->Rr[j];
-    cc.P[j] = c->P[j];
-    cc.Q[j] = c->Q[j];
+    cc.X[j] = c->X[2 * g0 + j];
+    cc.Rr[j] = c->Rr[2 * g0 + j];
+    cc.P[j] = c->P[2 * g0 + j];
+    cc.Q[j] = c->Q[2 * g0 + j];
     if (c->rs_rec) {
-      cc.RX[j] = c->RX0[j];
-      cc.Y[j] = c->Y[j];
+      cc.RX[j] = c->RX0[2 * g0 + j];
+      cc.Y[j] = c->Y[2 * g0 + j];
     }
     active[j] = 1;
     if (dev_init) continue;                   // k_cg_init
@@ -2148,8 +2132,8 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
     atol[j] = std::max(0.0, rtol * bn);
     rhov[j] = tot[MAXC + j];
     if (bn == 0.0) {                          // iterative.py:380-381: return b
-      HIPCHK(hipMemsetAsync(c->X[j], 0, sizeof(double) * c->Mpad, c->st));
-      HIPCHK(hipMemsetAsync(c->RX0[j], 0, sizeof(double) * c->Mpad, c->st));   // R_s 0
+      HIPCHK(hipMemsetAsync(c->X[2 * g0 + j], 0, sizeof(double) * c->Mpad, c->st));
+      HIPCHK(hipMemsetAsync(c->RX0[2 * g0 + j], 0, sizeof(double) * c->Mpad, c->st));   // R_s 0
       active[j] = 0;
     }
   }
@@ -2164,43 +2148,43 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
   po.rs = c->rs_rec;
   po.rho = rho;
   for (int j = 0; j < ncol; ++j) {
-    po.X[j] = c->X[j];
-    po.X0[j] = c->X0[j];
-    po.RX[j] = c->RX0[j];
-    po.RXp[j] = c->RXp[j];
+    po.X[j] = c->X[2 * g0 + j];
+    po.X0[j] = c->X0[2 * g0 + j];
+    po.RX[j] = c->RX0[2 * g0 + j];
+    po.RXp[j] = c->RXp[2 * g0 + j];
   }
   for (int k = 0; k < K; ++k) {
-    po.u[k] = c->U[k];
-    po.r[k] = c->r[k];
+    po.u[k] = c->U[g0 + k];
+    po.r[k] = c->r[g0 + k];
   }
   HIPCHK(launch_lmmse_post(c->d_ch, c->nch, po, c->d_part, c->st));
-  double pt[4 * MAXK + MAXC];
+  double pt[4 * MAXKG + MAXC];
   R1Args ra{};
   ra.K = K;
   if (dev_init) {
     // r1 takes alpha2 from the device-reduced Tr(Sigma2): the update is queued
     // before the host reads the sums (which it computes alpha2 from as well)
-    CHK(reduce_dev(c, 4 * MAXK + MAXC, c->d_ch_begin, identity_map(), c->d_tot));
+    CHK(reduce_dev(c, 4 * MAXKG + MAXC, c->d_ch_begin, identity_map(), c->d_tot));
     ra.trs = c->d_tot;
     ra.Mtot = (double)c->Mtot;
     ra.rho = rho;
     ra.damp = lmmse_damp;
     for (int k = 0; k < K; ++k) {
-      ra.X[k] = c->X[2 * k];
-      ra.r2[k] = c->r2[k];
-      ra.r1[k] = c->r1[k];
+      ra.X[k] = c->X[2 * g0 + (2 * k)];
+      ra.r2[k] = c->r2[g0 + k];
+      ra.r1[k] = c->r1[g0 + k];
       ra.gam2[k] = gam2[k];
       ra.alpha2_prev[k] = alpha2_prev[k];
     }
     HIPCHK(launch_r1_update(c->d_ch, c->nch, ra, c->st));   // :348
-    HIPCHK(launch_copy_f64(c->h_tot, c->d_tot, 4 * MAXK + MAXC, c->st));
+    HIPCHK(launch_copy_f64(c->h_tot, c->d_tot, 4 * MAXKG + MAXC, c->st));
     CHK(stream_wait(c));
     resolve_timers(c);
     std::memcpy(pt, c->h_tot, sizeof(pt));
   } else {
-    CHK(reduce_host(c, 4 * MAXK + MAXC, c->d_ch_begin, pt));
+    CHK(reduce_host(c, 4 * MAXKG + MAXC, c->d_ch_begin, pt));
   }
-  for (int j = 0; j < ncol; ++j) c->xnz[j] = pt[2 * MAXK + j] > 0.0;
+  for (int j = 0; j < ncol; ++j) c->xnz[2 * g0 + j] = pt[2 * MAXKG + j] > 0.0;
 
   for (int k = 0; k < K; ++k) {
     const double TrSigma2 = pt[k];
@@ -2211,14 +2195,14 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
     o[SGV_O_TRSIGMA2] = TrSigma2;
     o[SGV_O_ALPHA2] = a2;
     o[SGV_O_GAM1] = g1;
-    o[SGV_O_XR] = pt[MAXK + k];
+    o[SGV_O_XR] = pt[MAXKG + k];
     o[SGV_O_Z] = 0.0;
     o[SGV_O_TRRSIGMA2] = 0.0;
     o[SGV_O_XRX] = 0.0;
     o[SGV_O_GAMW] = gamw[k];
-    ra.X[k] = c->X[2 * k];
-    ra.r2[k] = c->r2[k];
-    ra.r1[k] = c->r1[k];
+    ra.X[k] = c->X[2 * g0 + (2 * k)];
+    ra.r2[k] = c->r2[g0 + k];
+    ra.r1[k] = c->r1[g0 + k];
     ra.alpha2[k] = a2;
     cg_out[4 * k + 0] = iters[2 * k];
     cg_out[4 * k + 1] = info[2 * k];
@@ -2229,10 +2213,10 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
 
   if (learn_gamw && c->rs_rec) {  // :350-363 from the carried products: no pass
     for (int k = 0; k < K; ++k) {
-      const double N = c->Ncoh[k];
+      const double N = c->Ncoh[g0 + k];
       double* o = out + (size_t)k * SGV_LMMSE_NOUT;
-      const double xRx = pt[2 * MAXK + MAXC + k];
-      const double TrRSigma2 = pt[3 * MAXK + MAXC + k];
+      const double xRx = pt[2 * MAXKG + MAXC + k];
+      const double TrRSigma2 = pt[3 * MAXKG + MAXC + k];
       double z = N - 2 * o[SGV_O_XR] + xRx;                        // :352
       if (z < 0) z = 0;                                            // :353-354
       o[SGV_O_Z] = z;
@@ -2247,15 +2231,15 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
       int nc = 0;
       for (int j = 0; j < ncol; ++j) {
         const int k = j / 2;
-        if (c->ld_of[k] != ld) continue;
-        pa.in[nc] = c->X[j];
-        pa.out[nc] = c->RX0[j];
-        pa.dot[nc] = (j % 2 == 0) ? c->X[j] : c->U[k];
+        if (c->ld_of[g0 + k] != ld) continue;
+        pa.in[nc] = c->X[2 * g0 + j];
+        pa.out[nc] = c->RX0[2 * g0 + j];
+        pa.dot[nc] = (j % 2 == 0) ? c->X[2 * g0 + j] : c->U[g0 + k];
         pa.c1[nc] = 1.0 - s;
         pa.c2[nc] = s;
         map.d[nc] = j;
         ++nc;
-        c->rx0_valid[j] = 1;
+        c->rx0_valid[2 * g0 + j] = 1;
       }
       if (!nc) continue;
       CHK(ld_pass(c, ld, nc, pa));
@@ -2266,8 +2250,8 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
       resolve_timers(c);
       std::memcpy(gt, c->h_tot, sizeof(double) * ncol);
       for (int k = 0; k < K; ++k) {
-        if (c->ld_of[k] != ld) continue;
-        const double N = c->Ncoh[k];
+        if (c->ld_of[g0 + k] != ld) continue;
+        const double N = c->Ncoh[g0 + k];
         double* o = out + (size_t)k * SGV_LMMSE_NOUT;
         const double xRx = gt[2 * k];
         const double TrRSigma2 = gt[2 * k + 1];
@@ -2281,6 +2265,43 @@ extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* g
     }
   } else {
     CHK(stream_wait(c));
+  }
+  if (passes_out) *passes_out = passes;
+  return SGV_OK;
+}
+
+extern "C" int sgv_lmmse(sgv_ctx* c, int it, const double* gamw, const double* gam2,
+                         const double* alpha1, const double* alpha2_prev, const int8_t* probes,
+                         int cg_maxit, double rtol, int lmmse_damp, double rho, int learn_gamw,
+                         double* out, int* cg_out, int* passes_out) {
+  ENTER(c);
+  (void)it;
+  if (!gamw || !gam2 || !alpha1 || !alpha2_prev || !probes || !out || !cg_out || cg_maxit < 0)
+    return fail(c, SGV_ERR_ARG, "sgv_lmmse: bad arguments");
+  const int K = c->K;
+
+  // probes u_k (:326), int8 +-1 -> f64; uploaded at the start of sgv_step, or now
+  int ps = c->pref_slot;
+  if (ps < 0 || c->pref_src != probes) CHK(probe_upload(c, probes, &ps));
+  c->pref_slot = -1;
+  c->pref_src = nullptr;
+  HIPCHK(hipStreamWaitEvent(c->st, c->ev_probe[ps], 0));
+  for (int k = 0; k < K; ++k)
+    HIPCHK(launch_unpack_i8(c->d_ch, c->nch, c->d_ch_doff,
+                            c->d_probe + ps * c->probe_cap + (size_t)k * c->Mloc, c->U[k], c->st));
+  HIPCHK(hipEventRecord(c->ev_unpk[ps], c->st));
+
+  // cohorts in groups of MAXKG (2 MAXKG = MAXC CG columns per LD pass): the
+  // LMMSE of a cohort touches only its own vectors and the shared xhat1, so the
+  // groups run one after another with the same per-cohort arithmetic
+  int passes = 0;
+  for (int g0 = 0; g0 < K; g0 += MAXKG) {
+    const int Kg = std::min(MAXKG, K - g0);
+    int gp = 0;
+    CHK(lmmse_group(c, g0, Kg, gamw + g0, gam2 + g0, alpha1 + g0, alpha2_prev + g0, cg_maxit, rtol,
+                    lmmse_damp, rho, learn_gamw, out + (size_t)g0 * SGV_LMMSE_NOUT, cg_out + 4 * g0,
+                    &gp));
+    passes += gp;
   }
   if (passes_out) *passes_out = passes;
   return SGV_OK;

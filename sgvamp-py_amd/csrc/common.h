@@ -10,8 +10,9 @@ constexpr int WAVE = 64;
 constexpr int VTHREADS = 256;   // threads per workgroup of the vector kernels
 constexpr int CHUNK = 1024;     // markers per chunk (vector-kernel workgroup)
 constexpr int PADV = 128;       // per-block padding of device vectors and LD rows (doubles = 1 KiB)
-constexpr int MAXC = 16;        // right-hand-side columns per LD pass (2 x 8 cohorts)
-constexpr int MAXK = 8;         // cohorts
+constexpr int MAXC = 16;        // right-hand-side columns per LD pass (2 x MAXKG cohorts)
+constexpr int MAXK = 32;        // cohorts
+constexpr int MAXKG = 8;        // cohorts per LMMSE group (one batched CG loop, <= MAXC columns)
 constexpr int MAXL = 8;         // slab components (L - 1)
 
 typedef double d2 __attribute__((ext_vector_type(2)));
@@ -137,7 +138,8 @@ struct PassArgs {
 };
 
 // most values one ordered reduction carries
-constexpr int MAXNV = 4 * MAXK + MAXC;
+constexpr int MAXNV = 4 * MAXKG + MAXC;
+static_assert(MAXK <= MAXNV, "per-cohort sums (denoiser, MLE) fit one ordered reduction");
 
 struct Map16 {
   int d[MAXNV];
@@ -304,8 +306,8 @@ hipError_t launch_denoise(const ChunkDesc* d_ch, int nch, const DenoiseArgs& a, 
 struct MleArgs {
   const double* r1[MAXK];
   double a[MAXK];
-  double v[MAXK][MAXL + 1];    // prior_vars0 + 1/gam1_k (:148-155), spike first
-  double sv[MAXK][MAXL + 1];   // sqrt(v)
+  double ginv[MAXK];           // 1/gam1_k (:146); v_kl = sigma2_l + ginv_k, sv = sqrt(v)
+  double sigma2[MAXL + 1];     // prior_vars0 (spike first)
   double omega[MAXL + 1];
   double exp_max;
   int K, L;                    // L = components incl. the spike (reference self.L)
@@ -355,11 +357,11 @@ struct EmCtl {
 hipError_t launch_em_reduce_ctl(const double* d_part, EmState* d_st, const EmCtl& f,
                                 hipStream_t st);
 
-struct CohortPtrs {
-  const double* r[MAXK];
-  const double* r1[MAXK];
-  double* r2[MAXK];
-  const double* u[MAXK];
+struct CohortPtrs {   // one LMMSE cohort group
+  const double* r[MAXKG];
+  const double* r1[MAXKG];
+  double* r2[MAXKG];
+  const double* u[MAXKG];
 };
 struct ColPtrs {
   double* X[MAXC];
@@ -374,8 +376,8 @@ struct InitArgs {
   CohortPtrs cp;
   ColPtrs col;
   const double* xhat1;
-  int K;
-  double alpha1[MAXK], gamw[MAXK], gam2[MAXK];
+  int K;                    // cohorts in the group
+  double alpha1[MAXKG], gamw[MAXKG], gam2[MAXKG];
   int warm[MAXC];           // residual r = b - A x0 (x0.any()); else r = b
   int save_x0;              // copy X[2k] to X0[2k] (and RX0 to RXp) for LMMSE damping
 };
@@ -447,9 +449,9 @@ struct PostArgs {
   const double* X0[MAXC];
   double* RX[MAXC];         // carried R_s X (rs != 0): damped with X, dotted for gamw
   const double* RXp[MAXC];
-  const double* u[MAXK];
-  const double* r[MAXK];
-  int K;
+  const double* u[MAXKG];
+  const double* r[MAXKG];
+  int K;                    // cohorts in the group
   int damp;
   int rs;
   double rho;
@@ -457,16 +459,16 @@ struct PostArgs {
 hipError_t launch_lmmse_post(const ChunkDesc* d_ch, int nch, const PostArgs& a, double* d_part,
                              hipStream_t st);
 
-struct R1Args {
-  const double* X[MAXK];    // xhat2_k
-  const double* r2[MAXK];
-  double* r1[MAXK];
-  double alpha2[MAXK];
+struct R1Args {               // one LMMSE cohort group
+  const double* X[MAXKG];    // xhat2_k
+  const double* r2[MAXKG];
+  double* r1[MAXKG];
+  double alpha2[MAXKG];
   int K;
   // non-null: alpha2 from the device-reduced Tr(Sigma2) trs[k] (:340, 345-346):
   // alpha2 = gam2 trs / Mtot, damped with alpha2_prev
   const double* trs;
-  double gam2[MAXK], alpha2_prev[MAXK];
+  double gam2[MAXKG], alpha2_prev[MAXKG];
   double Mtot, rho;
   int damp;
 };

@@ -53,22 +53,25 @@ __device__ __forceinline__ void zero_unowned(double* __restrict__ base, int nv, 
 // ---------------------------------------------------------------------------
 // denoiser_meta + der_denoiser_meta, src/sgvamp.py:93-114, per marker (:273,285)
 // ---------------------------------------------------------------------------
+// KM: cohort bound of the instantiation (registers: vr holds MPT x KM values);
+// partials [k] at stride K
+template <int KM>
 __global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restrict__ chs,
                                                       DenoiseArgs a,
                                                       double* __restrict__ part) {
   const ChunkDesc ch = chs[blockIdx.x];
-  double acc[MAXK];
+  double acc[KM];
 #pragma unroll
-  for (int k = 0; k < MAXK; ++k) acc[k] = 0.0;
+  for (int k = 0; k < KM; ++k) acc[k] = 0.0;
   // loads of the thread's MPT markers first (see MPT), then the markers in order
-  double vr[MPT][MAXK], vxo[MPT];
+  double vr[MPT][KM], vxo[MPT];
 #pragma unroll
   for (int j = 0; j < MPT; ++j) {
     const int t = threadIdx.x + j * VTHREADS;
     if (t < ch.len) {
       const int64_t i = ch.voff + t;
 #pragma unroll
-      for (int k = 0; k < MAXK; ++k)
+      for (int k = 0; k < KM; ++k)
         if (k < a.K) vr[j][k] = a.r1[k][i];
       if (a.damp) vxo[j] = a.xhat1[i];
     }
@@ -81,7 +84,7 @@ __global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restric
     // np.inner(rs, a*gam1s) (:96)
     double inner = 0.0;
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k)
+    for (int k = 0; k < KM; ++k)
       if (k < a.K) inner = (k == 0) ? vr[j][0] * a.ag[0] : inner + vr[j][k] * a.ag[k];
     double mu[MAXL];
     int m = 0;
@@ -122,7 +125,7 @@ __global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restric
     a.xhat1[i] = x;
     // der_denoiser_meta for every cohort k (:112-114 with a[k]*gam1s[k])
 #pragma unroll
-    for (int k = 0; k < MAXK; ++k)
+    for (int k = 0; k < KM; ++k)
       if (k < a.K) {
         double dn = 0.0, dd = 0.0;
 #pragma unroll
@@ -139,12 +142,20 @@ __global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restric
         acc[k] += (DerNum * Den - DerDen * Num) / (Den * Den);
       }
   }
-  block_reduce_store<MAXK>(acc, part + (int64_t)blockIdx.x * MAXK, MAXK);
+  block_reduce_store<KM>(acc, part + (int64_t)blockIdx.x * a.K, a.K);
 }
 
 hipError_t launch_denoise(const ChunkDesc* d_ch, int nch, const DenoiseArgs& a, double* d_part,
                           hipStream_t st) {
-  hipLaunchKernelGGL(k_denoise, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part);
+#define L_DEN(KM) hipLaunchKernelGGL(k_denoise<KM>, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, d_part)
+  if (a.K < 1 || a.K > MAXK) return hipErrorInvalidValue;   // cohorts
+  if (a.K <= 1) L_DEN(1);
+  else if (a.K <= 2) L_DEN(2);
+  else if (a.K <= 4) L_DEN(4);
+  else if (a.K <= 8) L_DEN(8);
+  else if (a.K <= 16) L_DEN(16);
+  else L_DEN(MAXK);
+#undef L_DEN
   return hipGetLastError();
 }
 
@@ -251,6 +262,10 @@ __global__ __launch_bounds__(EM_THREADS) void k_em(const ChunkDesc* __restrict__
     else if ((K) <= 4 && (L) <= 2) { LAUNCH(4, 2); }                          \
     else if ((K) <= 8 && (L) <= 2) { LAUNCH(8, 2); }                          \
     else if ((K) <= 4) { LAUNCH(4, MAXL); }                                   \
+    else if ((K) <= 8) { LAUNCH(8, MAXL); }                                   \
+    else if ((K) <= 16 && (L) <= 2) { LAUNCH(16, 2); }                        \
+    else if ((K) <= 16) { LAUNCH(16, MAXL); }                                 \
+    else if ((L) <= 2) { LAUNCH(MAXK, 2); }                                   \
     else { LAUNCH(MAXK, MAXL); }                                              \
   } while (0)
 
@@ -449,7 +464,7 @@ __global__ __launch_bounds__(VTHREADS) void k_lmmse_init(const ChunkDesc* __rest
 
 hipError_t launch_lmmse_init(const ChunkDesc* d_ch, int nch, const InitArgs& a, double* d_part,
                              hipStream_t st) {
-  if (a.K < 1 || a.K > MAXK) return hipErrorInvalidValue;
+  if (a.K < 1 || a.K > MAXKG) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_lmmse_init, dim3(nch, a.K), dim3(VTHREADS), 0, st, d_ch, a, d_part);
   return hipGetLastError();
 }
@@ -716,12 +731,12 @@ hipError_t launch_cg_ctl(CgState* d_st, CgState* mirror, const double* d_rho_new
 
 // ---------------------------------------------------------------------------
 // after both CG solves (src/sgvamp.py:322-338,352,359):
-//   xhat2 damping; partials [k] = u.Sigma2_u, [MAXK + k] = xhat2.r,
-//   [2 MAXK + c] = count(x_c != 0)  (next iteration's x0.any()),
-//   with the carried products (rs): [2 MAXK + MAXC + k] = xhat2.R_s xhat2,
-//   [3 MAXK + MAXC + k] = u.R_s Sigma2_u
+//   xhat2 damping; partials [k] = u.Sigma2_u, [MAXKG + k] = xhat2.r,
+//   [2 MAXKG + c] = count(x_c != 0)  (next iteration's x0.any()),
+//   with the carried products (rs): [2 MAXKG + MAXC + k] = xhat2.R_s xhat2,
+//   [3 MAXKG + MAXC + k] = u.R_s Sigma2_u
 // ---------------------------------------------------------------------------
-constexpr int POST_NV = 4 * MAXK + MAXC;
+constexpr int POST_NV = 4 * MAXKG + MAXC;
 static_assert(POST_NV <= MAXNV, "post partials");
 // grid (nch, K): workgroup (chunk, k) does cohort k
 __global__ __launch_bounds__(VTHREADS) void k_lmmse_post(const ChunkDesc* __restrict__ chs,
@@ -731,7 +746,7 @@ __global__ __launch_bounds__(VTHREADS) void k_lmmse_post(const ChunkDesc* __rest
   const int k = blockIdx.y;
   double* pb = part + (int64_t)blockIdx.x * POST_NV;
   zero_unowned(pb, POST_NV, a.K, [](int t) {
-    return t < 2 * MAXK ? t % MAXK : t < 2 * MAXK + MAXC ? (t - 2 * MAXK) / 2 : (t - 2 * MAXK - MAXC) % MAXK;
+    return t < 2 * MAXKG ? t % MAXKG : t < 2 * MAXKG + MAXC ? (t - 2 * MAXKG) / 2 : (t - 2 * MAXKG - MAXC) % MAXKG;
   });
   double* __restrict__ X0 = a.X[2 * k];
   const double* __restrict__ X1 = a.X[2 * k + 1];
@@ -790,14 +805,14 @@ __global__ __launch_bounds__(VTHREADS) void k_lmmse_post(const ChunkDesc* __rest
       acc[3] += (s2u != 0.0) ? 1.0 : 0.0;
     }
   }
-  const int slot[6] = {k, MAXK + k, 2 * MAXK + 2 * k, 2 * MAXK + 2 * k + 1, 2 * MAXK + MAXC + k,
-                       3 * MAXK + MAXC + k};
+  const int slot[6] = {k, MAXKG + k, 2 * MAXKG + 2 * k, 2 * MAXKG + 2 * k + 1, 2 * MAXKG + MAXC + k,
+                       3 * MAXKG + MAXC + k};
   block_reduce_slots<6>(acc, pb, slot);
 }
 
 hipError_t launch_lmmse_post(const ChunkDesc* d_ch, int nch, const PostArgs& a, double* d_part,
                              hipStream_t st) {
-  if (a.K < 1 || a.K > MAXK) return hipErrorInvalidValue;
+  if (a.K < 1 || a.K > MAXKG) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_lmmse_post, dim3(nch, a.K), dim3(VTHREADS), 0, st, d_ch, a, d_part);
   return hipGetLastError();
 }
@@ -833,7 +848,7 @@ __global__ __launch_bounds__(VTHREADS) void k_r1_update(const ChunkDesc* __restr
 }
 
 hipError_t launch_r1_update(const ChunkDesc* d_ch, int nch, const R1Args& a, hipStream_t st) {
-  if (a.K < 1 || a.K > MAXK) return hipErrorInvalidValue;
+  if (a.K < 1 || a.K > MAXKG) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_r1_update, dim3(nch, a.K), dim3(VTHREADS), 0, st, d_ch, a);
   return hipGetLastError();
 }
@@ -1125,7 +1140,8 @@ __global__ __launch_bounds__(VTHREADS) void k_mle_terms(const ChunkDesc* __restr
 #pragma unroll
         for (int l = 0; l < MLE_NV; ++l)
           if (l < a.L) {
-            p[l] = exp(nr2 / 2.0 / a.v[k][l] - a.exp_max) / a.sv[k][l];
+            const double v = a.sigma2[l] + a.ginv[k];       // prior_vars0 + gam1invs
+            p[l] = exp(nr2 / 2.0 / v - a.exp_max) / sqrt(v);
             den = (l == 0) ? p[l] * a.omega[l] : den + p[l] * a.omega[l];
           }
 #pragma unroll

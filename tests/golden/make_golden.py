@@ -264,6 +264,12 @@ CASES = {
     "k4_long50": dict(seed=42, M=2000, N=[3000, 3500, 4000, 4500], blocks=[1000, 1000],
                       iterations=50, s=0.02, lmmse_damp=1, rho=0.3, prior="auto", lam_sim=0.1,
                       exact=True),
+    # more than 8 cohorts (the LMMSE runs them in groups of 8 CG column pairs):
+    # K=10 sharing one LD with ridge + damping + EM, K=11 with distinct LDs
+    "k10_shared": dict(seed=51, M=300, N=[800 + 100 * k for k in range(10)], blocks=[150, 150],
+                       iterations=6, s=0.05, lmmse_damp=1, prior="auto", lam_sim=0.1),
+    "k11_distinct": dict(seed=52, M=200, N=[700 + 50 * k for k in range(11)], blocks=[200],
+                         iterations=6, distinct_ld=True, prior="auto", lam_sim=0.15),
     # C1 (BASELINE.json configs[0]): K=1, M=5000, N=10000, one dense block, 20
     # iterations; the simulation recipe's 50 % causal markers, matched prior
     "c1": dict(seed=43, M=5000, N=[10000], blocks=[5000], iterations=20, prior="auto",

@@ -434,14 +434,16 @@ def test_vamp_medium_scale_vs_oracle(prior, rs, tmp_path):
 
 
 @pytest.mark.parametrize("K,ridge,damp", [(4, 0.05, True), (8, 0.05, True), (4, 0.0, False),
-                                          (8, 0.0, False)])
+                                          (8, 0.0, False), (12, 0.05, True), (17, 0.0, False)])
 def test_vamp_medium_scale_shared_ld_vs_oracle(K, ridge, damp, tmp_path):
     """C3/C5-like: K cohorts sharing one LD (2K CG columns -> the f64 MFMA passes
     over multi-panel, multi-chunk blocks: 4x4x4 groups, 16x16x4 at 13..16
     columns), ridge s and LMMSE damping on, R_s x carried through the CG; vs the
     oracle with the same algebra (cg_track).  With s = 0 the blocks are rank
     deficient (n_b > N): 5-9 CG iterations, columns stopping at different
-    iterations, so one solve walks through several column counts / kernels."""
+    iterations, so one solve walks through several column counts / kernels.
+    K = 12 / 17: more than 8 cohorts -- the LMMSE runs them in groups of 8
+    (16 CG columns per pass), then 4 / 8 + 1."""
     sizes = [1300, 700, 1100]
     nsamp = 900
     M = sum(sizes)
@@ -733,9 +735,10 @@ def test_c5_shape_divergence_matches_oracle(tmp_path):
     same device-generated inputs.  The oracle (pinned to the reference) grows
     l2 from 0.9 to ~5e3 by iteration 8 with 1-iteration CG solves, so the
     divergence is the algorithm's (src/sgvamp.py:322-323 damps xhat2 only);
-    HIP follows it step for step: CG and EM counts exact, l2 to 1e-8, xhat to
-    1e-8 relative before the blow-up and within the north star's 1e-5 through
-    it (observed 2.6e-7: rounding differences grow with the unstable mode)."""
+    HIP follows it step for step: CG and EM counts exact, l2 and xhat to 1e-8
+    relative before the blow-up and within the north star's 1e-5 through it
+    (observed 2.6e-7 at l2 = 5e3: rounding differences grow with the unstable
+    mode)."""
     n, nsamp, K, s = 6000, 3840, 8, 0.1
     M = n
     rs = np.random.RandomState(2025)
@@ -773,6 +776,7 @@ def test_c5_shape_divergence_matches_oracle(tmp_path):
         assert errs[it] < (1e-8 if l2[it] < 1.5 else 1e-5), (it, errs[it])
     assert [h["cg_iters"] for h in v.history] == [[list(c) for c in x] for x in t["cg_iters"]]
     assert [h.get("em_steps") for h in v.history][1:] == list(t["em_steps"])
-    np.testing.assert_allclose(l2, [m[2] for m in t["metrics"]], rtol=1e-8)
+    for it, m in enumerate(t["metrics"]):
+        assert abs(l2[it] - m[2]) <= (1e-8 if l2[it] < 1.5 else 1e-5) * abs(m[2]), it
     assert l2[-1] > 100 * l2[2]          # the blow-up is in both
     eng.close()
