@@ -258,6 +258,7 @@ struct sgv_ctx {
   EmState* h_emm = nullptr;       // [CG_RING]
   EmState* h_emi = nullptr;
   double* d_emtot = nullptr;
+  double* d_emtab = nullptr;      // [K][EM_TAB] per-cohort EM constants (k_em_prep)
   hipEvent_t ev_em[4] = {nullptr, nullptr, nullptr, nullptr};
   hipEvent_t ev_den = nullptr;    // sgv_step: the denoiser's sums are in h_tot
   // timers
@@ -1215,6 +1216,7 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   CREATE_HIP(hipEventCreateWithFlags(&c->ev_den, hipEventDisableTiming));
   CREATE_HIP(hipMalloc(&c->d_ems, sizeof(EmState)));
   CREATE_HIP(hipMalloc(&c->d_emtot, sizeof(double) * MAXNV));
+  CREATE_HIP(hipMalloc(&c->d_emtab, sizeof(double) * MAXK * EM_TAB));
   CREATE_HIP(hipHostMalloc(&c->h_emm, sizeof(EmState) * CG_RING, hipHostMallocCoherent));
   CREATE_HIP(hipHostMalloc(&c->h_emi, sizeof(EmState)));
   for (int i = 0; i < CG_RING; ++i)
@@ -1287,6 +1289,7 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   if (c->h_r1send) (void)hipHostFree(c->h_r1send);
   if (c->h_r1g) (void)hipHostFree(c->h_r1g);
   if (c->d_emtot) (void)hipFree(c->d_emtot);
+  if (c->d_emtab) (void)hipFree(c->d_emtab);
   if (c->h_emm) (void)hipHostFree(c->h_emm);
   if (c->h_emi) (void)hipHostFree(c->h_emi);
   for (hipEvent_t e : c->ev_em)
@@ -1855,6 +1858,8 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
     ea.scl = (k == 0) ? a[0] : ea.scl + a[k];
   }
   for (int l = 0; l < nslab; ++l) ea.sigmas[l] = sigmas[l];
+  ea.tab = c->d_emtab;
+  HIPCHK(launch_em_prep(ea, c->d_emtab, c->st));
   double lam = *lam_io;
   double om[MAXL];
   for (int l = 0; l < nslab; ++l) om[l] = omegas_io[l];

@@ -326,8 +326,14 @@ struct EmState {
   int steps;
   int done;                 // converged or em_prior_maxit reached: k_em is a no-op
 };
+// per-cohort constants of an EM loop (k_em_prep, from gam1 and sigmas): [0] ginv
+// = 1/gam1, [1] sqrt(ginv), [2 + l] sigmas[l] + ginv, [2 + MAXL + l]
+// sqrt(ginv + sigmas[l]) -- the reference's per-element expressions (:125-131),
+// formed once instead of once per marker (same operations, same bits)
+constexpr int EM_TAB = 2 + 2 * MAXL;
 struct EmArgs {
   const EmState* st;        // non-null: lam and omegas from the device state
+  const double* tab;        // [K][EM_TAB] (k_em_prep)
   const double* r1[MAXK];
   double a[MAXK];
   double gam1[MAXK];
@@ -339,6 +345,8 @@ struct EmArgs {
 constexpr int EM_NV = MAXL + 2;   // [0] sum_j avg_k(pi); [1..L-1] omega numerators; [nslab+1] denominator
 hipError_t launch_em(const ChunkDesc* d_ch, int nch, const EmArgs& a, double* d_part,
                      hipStream_t st);
+// fills tab[K][EM_TAB] from a.gam1 / a.sigmas (once per EM loop)
+hipError_t launch_em_prep(const EmArgs& a, double* tab, hipStream_t st);
 // one EM update from the reduced sums tot[EM_NV] (src/sgvamp.py:134-136) and the
 // loop's stop test (:252-257); it + 1 == maxit also stops.  The state is
 // copied to `mirror` (host memory).

@@ -186,6 +186,9 @@ __device__ __forceinline__ bool em_partials(const ChunkDesc* __restrict__ chs, c
 #pragma unroll
   for (int v = 0; v < EM_NV; ++v) acc[v] = 0.0;
   const int t = threadIdx.x;
+  __shared__ double tab[KM * EM_TAB];
+  for (int q = t; q < a.K * EM_TAB; q += EM_THREADS) tab[q] = a.tab[q];
+  __syncthreads();
   if (t < ch.len) {
     double vr[KM];
 #pragma unroll
@@ -197,13 +200,13 @@ __device__ __forceinline__ bool em_partials(const ChunkDesc* __restrict__ chs, c
       if (k < a.K) {
         const double r = vr[k];
         const double r2 = r * r;                  // np.power(r1s, 2)
-        const double ginv = 1.0 / a.gam1[k];      // gam1invs
+        const double* tb = tab + k * EM_TAB;      // gam1invs and its sums/roots (k_em_prep)
         double tl[LM];
         double emax = 0.0;
 #pragma unroll
         for (int l = 0; l < LM; ++l)
           if (l < a.nslab) {
-            tl[l] = -r2 / 2 / (a.sigmas[l] + ginv);          // :127
+            tl[l] = -r2 / 2 / tb[2 + l];                     // :127
             emax = (l == 0 || tl[l] > emax) ? tl[l] : emax;
           }
         double xi[LM];
@@ -211,11 +214,11 @@ __device__ __forceinline__ bool em_partials(const ChunkDesc* __restrict__ chs, c
 #pragma unroll
         for (int l = 0; l < LM; ++l)
           if (l < a.nslab) {
-            xi[l] = lam * om[l] * exp(tl[l] - emax) / sqrt(ginv + a.sigmas[l]);   // :128
+            xi[l] = lam * om[l] * exp(tl[l] - emax) / tb[2 + MAXL + l];                 // :128
             sum_xi = (l == 0) ? xi[l] : sum_xi + xi[l];                                   // :129
           }
         const double pi =
-            1.0 / (1.0 + (1 - lam) * exp(-r2 / 2 * a.gam1[k] - emax) / sqrt(ginv) / sum_xi);  // :131
+            1.0 / (1.0 + (1 - lam) * exp(-r2 / 2 * a.gam1[k] - emax) / tb[1] / sum_xi);   // :131
         const double pa = pi * a.a[k];
         avg = (k == 0) ? pa : avg + pa;
         // compile-time accumulator indices (a runtime acc[1 + nslab] puts the
@@ -269,8 +272,28 @@ __global__ __launch_bounds__(EM_THREADS) void k_em(const ChunkDesc* __restrict__
     else { LAUNCH(MAXK, MAXL); }                                              \
   } while (0)
 
+__global__ __launch_bounds__(WAVE) void k_em_prep(EmArgs a, double* __restrict__ tab) {
+  for (int k = threadIdx.x; k < a.K; k += WAVE) {
+    double* tb = tab + k * EM_TAB;
+    const double ginv = 1.0 / a.gam1[k];      // gam1invs (:125)
+    tb[0] = ginv;
+    tb[1] = sqrt(ginv);                       // np.sqrt(gam1invs) (:131)
+    for (int l = 0; l < MAXL; ++l) {
+      tb[2 + l] = l < a.nslab ? a.sigmas[l] + ginv : 1.0;               // (:127)
+      tb[2 + MAXL + l] = l < a.nslab ? sqrt(ginv + a.sigmas[l]) : 1.0;   // (:128)
+    }
+  }
+}
+
+hipError_t launch_em_prep(const EmArgs& a, double* tab, hipStream_t st) {
+  if (a.K < 1 || a.K > MAXK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_em_prep, dim3(1), dim3(WAVE), 0, st, a, tab);
+  return hipGetLastError();
+}
+
 hipError_t launch_em(const ChunkDesc* d_ch, int nch, const EmArgs& a, double* d_part,
                      hipStream_t st) {
+  if (!a.tab) return hipErrorInvalidValue;
 #define L_EM(KM, LM) \
   hipLaunchKernelGGL((k_em<KM, LM>), dim3(nch), dim3(EM_THREADS), 0, st, d_ch, a, d_part)
   EM_DISPATCH(a.K, a.nslab, L_EM);
@@ -336,10 +359,44 @@ hipError_t launch_em_ctl(EmState* d_st, EmState* mirror, const double* d_tot, in
 // Waves take the (block, value) pairs LB_U at a time, all their loads first.
 constexpr int LB_U = 8;
 
+// When no block has more than 64 parts (blocks of <= 64 chunks: the C2 and
+// north-star layouts), lane l's strided sum is just 0 + part[begin[b] + l], so a
+// wave issues the loads of LB_W pairs at once from the LDS-staged part table
+// (one round trip per LB_W pairs instead of two dependent ones per pair).
+constexpr int LB_W = 32;
+
 __device__ void lb_reduce(const double* __restrict__ part, int nv, const int* __restrict__ begin,
                           int nblk, double* bs /* LDS, nv * nblk */, double* tot /* LDS, nv */) {
   const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   const int nw = blockDim.x / WAVE, npairs = nv * nblk;
+  __shared__ int sbeg[EM_CTL_MAXBLK + 1];
+  __shared__ int wide;
+  if (threadIdx.x == 0) wide = 0;
+  for (int b = threadIdx.x; b <= nblk; b += blockDim.x) sbeg[b] = begin[b];
+  __syncthreads();
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x)
+    if (sbeg[b + 1] - sbeg[b] > WAVE) wide = 1;
+  __syncthreads();
+  if (!wide) {
+    for (int q0 = w * LB_W; q0 < npairs; q0 += nw * LB_W) {
+      double s[LB_W];
+#pragma unroll
+      for (int u = 0; u < LB_W; ++u) {
+        s[u] = 0.0;
+        const int q = q0 + u;
+        if (q < npairs) {
+          const int b = q / nv, v = q - b * nv;
+          const int p = sbeg[b] + lane;
+          if (p < sbeg[b + 1]) s[u] = 0.0 + part[(int64_t)p * nv + v];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < LB_W; ++u) {
+        const double t = wave_sum(s[u]);
+        if (lane == 0 && q0 + u < npairs) bs[q0 + u] = t;
+      }
+    }
+  } else
   for (int q0 = w * LB_U; q0 < npairs; q0 += nw * LB_U) {
     double s[LB_U];
 #pragma unroll
