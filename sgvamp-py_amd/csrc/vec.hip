@@ -359,44 +359,10 @@ hipError_t launch_em_ctl(EmState* d_st, EmState* mirror, const double* d_tot, in
 // Waves take the (block, value) pairs LB_U at a time, all their loads first.
 constexpr int LB_U = 8;
 
-// When no block has more than 64 parts (blocks of <= 64 chunks: the C2 and
-// north-star layouts), lane l's strided sum is just 0 + part[begin[b] + l], so a
-// wave issues the loads of LB_W pairs at once from the LDS-staged part table
-// (one round trip per LB_W pairs instead of two dependent ones per pair).
-constexpr int LB_W = 32;
-
 __device__ void lb_reduce(const double* __restrict__ part, int nv, const int* __restrict__ begin,
                           int nblk, double* bs /* LDS, nv * nblk */, double* tot /* LDS, nv */) {
   const int lane = threadIdx.x & (WAVE - 1), w = threadIdx.x / WAVE;
   const int nw = blockDim.x / WAVE, npairs = nv * nblk;
-  __shared__ int sbeg[EM_CTL_MAXBLK + 1];
-  __shared__ int wide;
-  if (threadIdx.x == 0) wide = 0;
-  for (int b = threadIdx.x; b <= nblk; b += blockDim.x) sbeg[b] = begin[b];
-  __syncthreads();
-  for (int b = threadIdx.x; b < nblk; b += blockDim.x)
-    if (sbeg[b + 1] - sbeg[b] > WAVE) wide = 1;
-  __syncthreads();
-  if (!wide) {
-    for (int q0 = w * LB_W; q0 < npairs; q0 += nw * LB_W) {
-      double s[LB_W];
-#pragma unroll
-      for (int u = 0; u < LB_W; ++u) {
-        s[u] = 0.0;
-        const int q = q0 + u;
-        if (q < npairs) {
-          const int b = q / nv, v = q - b * nv;
-          const int p = sbeg[b] + lane;
-          if (p < sbeg[b + 1]) s[u] = 0.0 + part[(int64_t)p * nv + v];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < LB_W; ++u) {
-        const double t = wave_sum(s[u]);
-        if (lane == 0 && q0 + u < npairs) bs[q0 + u] = t;
-      }
-    }
-  } else
   for (int q0 = w * LB_U; q0 < npairs; q0 += nw * LB_U) {
     double s[LB_U];
 #pragma unroll
