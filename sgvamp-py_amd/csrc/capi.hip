@@ -1378,19 +1378,29 @@ static int gather_f64(sgv_ctx* c, const double* d_send, double* d_recv, size_t c
   return SGV_OK;
 }
 
-// SGV_EM_REP=0: with a communicator, one exchange per EM step instead (A/B)
-static bool em_rep_default() {
-  static const bool v = [] {
-    const char* e = ab_env("SGV_EM_REP");
-    return !(e && e[0] == '0');
-  }();
-  return v;
+// With a communicator the EM prior loop either runs REPLICATED (every rank's r1
+// all-gathered once per loop, then the one-rank loop over all M markers on every
+// rank) or with ONE EXCHANGE PER EM STEP (each rank sums its own markers; the
+// per-block partials are all-gathered every step, stream-ordered, the loop
+// still device-driven).  Per outer iteration with E EM steps:
+//   replicated: gather 8 K M bytes + E x (k_em over K M + one-workgroup reduce)
+//   per step:   E x (k_em over K M / N + all-gather latency + ordered total)
+// k_em is f64-VALU bound (exp, divisions: ~44 us at K M = 4e6 on one MI355X,
+// plus ~35 us of reduction/control) while one small all-gather costs ~10-30 us
+// over xGMI, so the replicated loop pays only below about a million
+// cohort-markers (C2: K M = 2e5 -> replicated; north star: 4e6 -> per step).
+// SGV_EM_REP=0/1 (with SGV_AB=1) forces either.
+constexpr double EM_REP_MAX_KM = 1048576.0;
+static bool em_rep_choice(const sgv_ctx* c) {
+  const char* e = ab_env("SGV_EM_REP");
+  if (e) return e[0] != '0';
+  return (double)c->K * (double)c->Mtot <= EM_REP_MAX_KM;
 }
 
 // replicated EM tables: every rank's block sizes (gathered), the global chunk
 // table and the gathered-r1 buffers
 static int em_rep_setup(sgv_ctx* c, const int* nblk_per_rank) {
-  if (!em_rep_default()) return SGV_OK;
+  if (!em_rep_choice(c)) return SGV_OK;
   int nbg = 0;
   for (int r = 0; r < c->nranks; ++r) nbg += nblk_per_rank[r];
   if (nbg > EM_CTL_MAXBLK) return SGV_OK;   // one-workgroup reduction cap: per-step exchange

@@ -26,16 +26,22 @@ def _free_port():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,cases", [
-    (2, ["k2_shared", "k1_blocks_csr_s_damp", "k4_shared_s_damp", "k1_L3", "k1_mle"]),
-    (3, ["k2_shared", "k1_blocks_csr_s_damp"]),
+@pytest.mark.parametrize("world,cases,em", [
+    (2, ["k2_shared", "k1_blocks_csr_s_damp", "k4_shared_s_damp", "k1_L3", "k1_mle"], "auto"),
+    (3, ["k2_shared", "k1_blocks_csr_s_damp"], "auto"),
+    (2, ["k2_shared", "k4_shared_s_damp", "k10_shared"], "per-step"),
 ])
-def test_sharded_ranks_match_golden(world, cases):
+def test_sharded_ranks_match_golden(world, cases, em):
+    """em: "auto" = the size rule (these small cases: replicated EM, r1 gathered
+    once per loop); "per-step" forces one exchange per EM step (the rule's choice
+    above about a million cohort-markers, e.g. the north star)."""
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SGV_EXCHANGE="host")
+        if em == "per-step":
+            env.update(SGV_AB="1", SGV_EM_REP="0")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "two_rank_gpu.py")]
                                       + cases, env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))
