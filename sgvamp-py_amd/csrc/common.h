@@ -217,38 +217,42 @@ constexpr int FIN_Q = 4;   // threads per panel row in the finalize kernels
 template <int NC>
 __device__ __forceinline__ void fin_epilogue(const SymPanel& pn, const PassArgs& pa, double (&y)[NC],
                                              double* __restrict__ partials) {
-  __shared__ double s_y[FIN_Q - 1][256];
+  // columns in batches of FIN_Q: every part stages its sums of the batch, then
+  // part q combines column 4b + q (parts in order 0..3: the same additions as
+  // one part adding the others' values) and writes its outputs and partial dot
+  // -- two barriers per batch instead of two per column, all 16 waves busy
+  constexpr int NB = (NC + FIN_Q - 1) / FIN_Q;
+  __shared__ double s_y[FIN_Q][FIN_Q][256];
   __shared__ double s_w[4][NC];
-  const int t = threadIdx.x & 255, q = threadIdx.x >> 8;
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    if (q) s_y[q - 1][t] = y[c];
-    __syncthreads();
-    if (!q) {
-      double v = y[c];
-#pragma unroll
-      for (int p = 0; p < FIN_Q - 1; ++p) v += s_y[p][t];
-      y[c] = v;
-    }
-    __syncthreads();
-  }
+  const int t = threadIdx.x & 255;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
   const int lane = t & (WAVE - 1), wid = t / WAVE;
-  const bool row = q == 0 && t < pn.H;   // part 0 writes the outputs
-  const int64_t idx = pn.voff + pn.r0 + (t < pn.H ? t : 0);
+  const bool row = t < pn.H;
+  const int64_t idx = pn.voff + pn.r0 + (row ? t : 0);
 #pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    double acc = 0.0;
-    if (row) {
-      const double in = pa.in[c][idx];
-      const double o = pa.c1[c] * y[c] + pa.c2[c] * in;
-      pa.out[c][idx] = o;
-      if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * y[c] + pa.ys0 * in;
-      if (pa.dot[c]) acc = pa.dot[c][idx] * o;
+  for (int b = 0; b < NB; ++b) {
+#pragma unroll
+    for (int j = 0; j < FIN_Q; ++j)
+      if (b * FIN_Q + j < NC) s_y[q][j][t] = y[b * FIN_Q + j];
+    __syncthreads();
+    const int c = b * FIN_Q + q;
+    if (c < NC) {
+      double v = s_y[0][q][t];
+#pragma unroll
+      for (int p = 1; p < FIN_Q; ++p) v += s_y[p][q][t];
+      double acc = 0.0;
+      if (row) {
+        const double in = pa.in[c][idx];
+        const double o = pa.c1[c] * v + pa.c2[c] * in;
+        pa.out[c][idx] = o;
+        if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * v + pa.ys0 * in;
+        if (pa.dot[c]) acc = pa.dot[c][idx] * o;
+      }
+      const double sm = wave_sum(acc);
+      if (lane == 0) s_w[wid][c] = sm;
     }
-    const double s = wave_sum(acc);
-    if (q == 0 && lane == 0) s_w[wid][c] = s;
+    __syncthreads();
   }
-  __syncthreads();
   if (threadIdx.x < NC)
     partials[(int64_t)pn.part * NC + t] = ((s_w[0][t] + s_w[1][t]) + s_w[2][t]) + s_w[3][t];
 }
