@@ -75,6 +75,10 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   static_assert(PD >= 1 && PD <= NT && NT % PD == 0, "prefetch depth divides the steps");
   __shared__ double red[2][NW][256];
   __shared__ __attribute__((aligned(16))) double stg[NW][16 * MF_LDP];
+  // a panel's row sums collect here and leave as one contiguous 16-B-store burst
+  // per (panel, chunk) item instead of one 8-B store per row and column after
+  // every 16-row group (same values; ~1 % faster per north-star pass)
+  __shared__ __attribute__((aligned(16))) double rbuf[SYM_H * 4 * NG];
   const SymStrip sp = strips[blockIdx.x];
   if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
   const int lane = threadIdx.x & (WAVE - 1);
@@ -236,8 +240,19 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
           double v = red[gg & 1][0][t];
 #pragma unroll
           for (int w = 1; w < NW; ++w) v += red[gg & 1][w][t];
-          rowpart[((int64_t)cur.item * SYM_H + 16 * g + row) * ncol + cc] = v;
+          rbuf[(16 * g + row) * ncol + cc] = v;
         }
+      }
+    }
+    {   // the item's H x ncol row sums, contiguous in rowpart
+      __syncthreads();
+      const int n = cur.H * ncol;
+      double* dst = rowpart + (int64_t)cur.item * SYM_H * ncol;
+      for (int i = threadIdx.x; 2 * i < n; i += NW * 64) {
+        if (2 * i + 1 < n)
+          *(d2*)(dst + 2 * i) = *(const d2*)(rbuf + 2 * i);
+        else
+          dst[2 * i] = rbuf[2 * i];
       }
     }
     cur = nx;
