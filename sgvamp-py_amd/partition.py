@@ -63,6 +63,31 @@ def detect_blocks_csr(indptr, indices, M):
     return _blocks_from_reach(reach)
 
 
+def coarsen_blocks(sizes, min_size=128):
+    """Merge runs of consecutive blocks smaller than min_size (PADV markers, one
+    padded vector segment) into blocks of at least min_size: a diagonal or
+    near-diagonal LD (e.g. a PLINK .ld without pairs: R = I) would otherwise
+    become M blocks of one marker, each padded to 128 in every device vector.
+    Blocks already >= min_size are kept as they are; the merged blocks hold zeros
+    between their parts (same matrix, coarser partition)."""
+    out, acc = [], 0
+    for n in sizes:
+        n = int(n)
+        if acc and n >= min_size:     # a pending run of small blocks stays apart from a big one
+            out.append(acc)
+            acc = 0
+        acc += n
+        if acc >= min_size:
+            out.append(acc)
+            acc = 0
+    if acc:
+        if out and acc < min_size:
+            out[-1] += acc
+        else:
+            out.append(acc)
+    return out
+
+
 def _blocks_from_reach(reach):
     sizes = []
     start = 0

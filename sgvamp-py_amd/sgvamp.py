@@ -30,7 +30,7 @@ import numpy as np
 
 import hip_backend as hb
 from engine import Engine
-from partition import detect_blocks_csr, detect_blocks_dense
+from partition import coarsen_blocks, detect_blocks_csr, detect_blocks_dense
 
 
 # Largest LD block densified on the host (n x n f64).  Symmetric CSR blocks never
@@ -113,7 +113,7 @@ class BlockLD:
         """A dense M x M LD matrix (the reference's .npy path, src/main.py:201-202);
         block structure detected from its zero pattern unless given."""
         R = np.asarray(R, dtype=np.float64)
-        sizes = block_sizes or detect_blocks_dense(R)
+        sizes = block_sizes or coarsen_blocks(detect_blocks_dense(R))
         offs = np.concatenate([[0], np.cumsum(sizes)])
         return cls(block_sizes=sizes, loader=lambda b: R[offs[b]:offs[b + 1], offs[b]:offs[b + 1]],
                    s=s)
@@ -125,7 +125,7 @@ class BlockLD:
         finest block-diagonal partition of its pattern, each kept sparse."""
         A = A.tocsr()
         M = A.shape[0]
-        sizes = block_sizes or detect_blocks_csr(A.indptr, A.indices, M)
+        sizes = block_sizes or coarsen_blocks(detect_blocks_csr(A.indptr, A.indices, M))
         offs = np.concatenate([[0], np.cumsum(sizes)])
         return cls(block_sizes=sizes,
                    csr_loader=lambda b: A[offs[b]:offs[b + 1], offs[b]:offs[b + 1]], s=s)

@@ -61,7 +61,7 @@ def _bd(sizes, seed=1):
 
 
 def test_load_ld_formats(tmp_path):
-    sizes = [4, 6, 3]
+    sizes = [140, 160, 130]
     R = _bd(sizes)
     np.save(tmp_path / "R.npy", R)
     scipy.sparse.save_npz(tmp_path / "R.npz", scipy.sparse.csr_matrix(R))

@@ -624,7 +624,7 @@ def _band_matrix(parts, seed=0):
 
 
 @pytest.mark.parametrize("parts", [[(5000, 300)], [(2100, 100), (700, None), (3000, 1000)],
-                                   [(1030, 5), (4000, 40)], [(4000, 1200)]])
+                                   [(1030, 5), (4000, 40)], [(4000, 1200)], [(3000, 0), (2050, 1)]])
 @pytest.mark.parametrize("ncol", [1, 2, 3, 8, 13, 16])
 @pytest.mark.parametrize("s", [0.0, 0.1])
 @pytest.mark.parametrize("kern", ["packed", "packed_valu"])
@@ -635,16 +635,20 @@ def test_ld_matvec_band_vs_scipy(parts, ncol, s, kern):
     (the reference's operator, src/sgvamp.py:316) to 1e-12."""
     A = _band_matrix(parts, seed=3)
     L = BlockLD.from_csr(A, s=s)
-    assert L.block_sizes == [n for n, _ in parts]
     eng = Engine(L.block_sizes, K=1)
     eng.set_ridge(s)
     if kern == "packed_valu":
         eng.set_mfma_min(0)
-    for b in range(len(parts)):
+    for b in range(len(L.block_sizes)):
         L.upload(eng, 0, b)
-    for b, (n, bw) in enumerate(parts):
-        band = bw is not None and -(-(256 + bw) // 512) * 512 < n
-        assert eng.ld_block_format(0, b) == (2 if band else 1), (b, n, bw)
+    if all(bw is None or bw >= 5 for _, bw in parts):   # one detected block per part
+        assert L.block_sizes == [n for n, _ in parts]
+        for b, (n, bw) in enumerate(parts):
+            band = bw is not None and -(-(256 + bw) // 512) * 512 < n
+            assert eng.ld_block_format(0, b) == (2 if band else 1), (b, n, bw)
+    else:   # R = I splits into 1-marker blocks, merged into >= 128-marker blocks
+        assert min(L.block_sizes[:-2]) >= 128 and L.block_sizes[-1] == 2050
+        assert {eng.ld_block_format(0, b) for b in range(len(L.block_sizes))} <= {1, 2}
     rs = np.random.RandomState(ncol)
     V = rs.normal(size=(ncol, A.shape[0]))
     Y = eng.ld_matvec(0, V)

@@ -67,12 +67,25 @@ def test_detect_blocks_sparse_pattern_inside_block():
 def test_blockld_regroup_and_common_partition():
     from sgvamp import BlockLD, common_partition
 
-    R = _blockdiag([3, 2, 4])
+    R = _blockdiag([130, 140, 150])
     L = BlockLD.from_dense(R)
-    assert L.block_sizes == [3, 2, 4]
-    assert common_partition([[3, 2, 4], [5, 4]]) == [5, 4]
-    G = L.regroup([5, 4])
-    np.testing.assert_array_equal(G.block(0), R[:5, :5])
-    np.testing.assert_array_equal(G.block(1), R[5:, 5:])
+    assert L.block_sizes == [130, 140, 150]
+    assert common_partition([[130, 140, 150], [270, 150]]) == [270, 150]
+    G = L.regroup([270, 150])
+    np.testing.assert_array_equal(G.block(0), R[:270, :270])
+    np.testing.assert_array_equal(G.block(1), R[270:, 270:])
     with pytest.raises(ValueError):
-        L.regroup([4, 5])
+        L.regroup([150, 270])
+    # blocks below 128 markers are merged (no 1-marker blocks padded to 128)
+    assert BlockLD.from_dense(_blockdiag([3, 2, 4])).block_sizes == [9]
+
+
+def test_coarsen_blocks_merges_tiny_blocks():
+    from partition import coarsen_blocks
+
+    assert coarsen_blocks([200, 250, 150]) == [200, 250, 150]      # golden CSR layout unchanged
+    c = coarsen_blocks([1] * 3000 + [2050])                        # R = I beside a band
+    assert sum(c) == 5050 and c[-2:] == [56, 2050] and min(c[:-2]) >= 128 and len(c) == 25
+    assert coarsen_blocks([1] * 100 + [5000] + [3] * 10) == [100, 5030]
+    assert coarsen_blocks([5] * 10) == [50]
+    assert coarsen_blocks([]) == []
