@@ -784,3 +784,41 @@ def test_c5_shape_divergence_matches_oracle(tmp_path):
         assert abs(l2[it] - m[2]) <= (1e-8 if l2[it] < 1.5 else 1e-5) * abs(m[2]), it
     assert l2[-1] > 100 * l2[2]          # the blow-up is in both
     eng.close()
+
+
+def test_mle_prior_many_cohorts_vs_oracle(tmp_path):
+    """--prior-update mle (src/sgvamp.py:139-194) with K = 10 cohorts (more than
+    one LMMSE group; the MLE sums over all cohorts on the device, fsolve on the
+    host) against the oracle on the same device-generated inputs."""
+    sizes = [600, 500]
+    nsamp, K = 700, 10
+    M = sum(sizes)
+    rs = np.random.RandomState(31)
+    cm = M // 10
+    beta = np.zeros(M)
+    beta[rs.choice(M, cm, replace=False)] = rs.normal(0, np.sqrt(0.8 / cm), cm)
+    eng = Engine(sizes, K=K)
+    g = eng.synth_ld_g(0, 55, nsamp, beta).sum(axis=0)
+    rvec = []
+    for k in range(K):
+        y = g + np.random.RandomState(300 + k).normal(0, np.sqrt(0.2), nsamp)
+        eng.synth_r(k, 55, nsamp, y)
+        rvec.append(eng.get_vector(hb.VEC_R, k).copy())
+    blocks = [eng.get_ld_block(0, b) for b in range(len(sizes))]
+    N = [float(nsamp)] * K
+    prior = dict(prior_vars=[0.0, 0.8 / cm / K], prior_probs=[0.9, 0.1])
+    x0 = beta * np.sqrt(nsamp)
+    v = VAMP(N=N, Nt=sum(N), M=M, K=K, rho=0.5, gamw=5.0, gam1=1e-6, a=[1 / K] * K,
+             out_dir=str(tmp_path), out_name="mle", seed=8, write_files=False, **prior)
+    v.attach_engine(eng, x0=x0)
+    its = 4
+    xh = v.infer(None, None, its, x0=x0, lmmse_damp=False, prior_update="mle")
+    L = vo.BlockLD(blocks)
+    t = vo.infer([L], [0] * K, rvec, N, its, rho=0.5, gamw=5.0, gam1=1e-6, x0=x0, seed=8,
+                 lmmse_damp=False, prior_update="mle",
+                 reducer=vo.Reducer("blocked", bounds=L.bounds), rs_recurrence=True, **prior)
+    for it in range(its):
+        assert maxrel(xh[it].ravel() / np.sqrt(sum(N)), np.asarray(t["xhat"][it])) < 1e-8, it
+    assert [h["cg_iters"] for h in v.history] == [[list(c) for c in x] for x in t["cg_iters"]]
+    assert [h.get("mle_warning") for h in v.history if h.get("mle_warning")] == t["mle_warnings"]
+    eng.close()
