@@ -214,14 +214,41 @@ constexpr int FIN_Q = 4;   // threads per panel row in the finalize kernels
 // part 0: out = c1*y + c2*in (and yout, R_s in), and the panel's partial dots
 // (wave butterfly, waves 0..3 in order) -> partials[pn.part * NC + c].
 // Called by every thread of a 256*FIN_Q workgroup.
+// The inputs of the epilogue (in[c] and dot[c] at this thread's row, for the
+// columns c = 4b + q its part writes) do not depend on the sums: fin_prefetch
+// loads them at kernel start, so their latency hides behind the partial loads.
+template <int NC>
+struct FinPre {
+  static constexpr int NB = (NC + FIN_Q - 1) / FIN_Q;
+  double in[NB], dot[NB];
+};
+template <int NC>
+__device__ __forceinline__ void fin_prefetch(const SymPanel& pn, const PassArgs& pa,
+                                             FinPre<NC>& pre) {
+  const int t = threadIdx.x & 255;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8);
+  const int64_t idx = pn.voff + pn.r0 + (t < pn.H ? t : 0);
+#pragma unroll
+  for (int b = 0; b < FinPre<NC>::NB; ++b) {
+    const int c = b * FIN_Q + q;
+    pre.in[b] = 0.0;
+    pre.dot[b] = 0.0;
+    if (c < NC) {
+      pre.in[b] = pa.in[c][idx];
+      if (pa.dot[c]) pre.dot[b] = pa.dot[c][idx];
+    }
+  }
+}
+
 template <int NC>
 __device__ __forceinline__ void fin_epilogue(const SymPanel& pn, const PassArgs& pa, double (&y)[NC],
-                                             double* __restrict__ partials) {
+                                             double* __restrict__ partials,
+                                             const FinPre<NC>& pre) {
   // columns in batches of FIN_Q: every part stages its sums of the batch, then
   // part q combines column 4b + q (parts in order 0..3: the same additions as
   // one part adding the others' values) and writes its outputs and partial dot
   // -- two barriers per batch instead of two per column, all 16 waves busy
-  constexpr int NB = (NC + FIN_Q - 1) / FIN_Q;
+  constexpr int NB = FinPre<NC>::NB;
   __shared__ double s_y[FIN_Q][FIN_Q][256];
   __shared__ double s_w[4][NC];
   const int t = threadIdx.x & 255;
@@ -242,11 +269,11 @@ __device__ __forceinline__ void fin_epilogue(const SymPanel& pn, const PassArgs&
       for (int p = 1; p < FIN_Q; ++p) v += s_y[p][q][t];
       double acc = 0.0;
       if (row) {
-        const double in = pa.in[c][idx];
+        const double in = pre.in[b];
         const double o = pa.c1[c] * v + pa.c2[c] * in;
         pa.out[c][idx] = o;
         if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * v + pa.ys0 * in;
-        if (pa.dot[c]) acc = pa.dot[c][idx] * o;
+        if (pa.dot[c]) acc = pre.dot[b] * o;
       }
       const double sm = wave_sum(acc);
       if (lane == 0) s_w[wid][c] = sm;

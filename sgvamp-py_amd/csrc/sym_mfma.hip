@@ -436,6 +436,8 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize_strip(
     const double* __restrict__ colpart, double* __restrict__ partials) {
   const SymPanel pn = panels[blockIdx.x];
   if (pa.run && !ldg(pa.run)) return;
+  FinPre<NC> pre;
+  fin_prefetch<NC>(pn, pa, pre);
   const int t = threadIdx.x & 255, q = threadIdx.x >> 8;
   const int tr = t < pn.H ? t : 0;
   double y[NC];
@@ -459,7 +461,7 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize_strip(
 #pragma unroll
     for (int c = 0; c < NC; ++c) y[c] += ldg(cp + c * MF_CW);
   }
-  fin_epilogue<NC>(pn, pa, y, partials);
+  fin_epilogue<NC>(pn, pa, y, partials, pre);
 }
 
 // Pk[i][c] = in[c][i] for c < ncol, 0 for ncol <= c < 16 (i over the padded vector)

@@ -152,6 +152,8 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize(const SymPanel* __
   __shared__ int s_ib[PCH];
   const SymPanel pn = panels[blockIdx.x];
   if (pa.run && !ldg(pa.run)) return;
+  FinPre<NC> pre;
+  fin_prefetch<NC>(pn, pa, pre);
   const int t = threadIdx.x & 255, q = threadIdx.x >> 8;
   double y[NC];
 #pragma unroll
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize(const SymPanel* __
       for (int c = 0; c < NC; ++c) y[c] += ldg(cp + (int64_t)c * cw);
     }
   }
-  fin_epilogue<NC>(pn, pa, y, partials);
+  fin_epilogue<NC>(pn, pa, y, partials, pre);
 }
 
 template <int NC, int NSEG>
