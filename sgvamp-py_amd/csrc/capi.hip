@@ -1601,10 +1601,12 @@ extern "C" int sgv_set_ld_block(sgv_ctx* c, int ld, int b, const double* host, i
 extern "C" int sgv_set_ld_block_csr(sgv_ctx* c, int ld, int b, const int64_t* indptr,
                                     const int64_t* indices, const double* data) {
   ENTER(c);
-  if (ld < 0 || ld >= c->nld || b < 0 || b >= c->nblk || !indptr || (!indices && indptr[c->bn[b]]) ||
-      (!data && indptr[c->bn[b]]))
+  if (ld < 0 || ld >= c->nld || b < 0 || b >= c->nblk || !indptr)
     return fail(c, SGV_ERR_ARG, "sgv_set_ld_block_csr: bad arguments (ld=%d b=%d)", ld, b);
   const int64_t n = c->bn[b];
+  if (indptr[n] > 0 && (!indices || !data))
+    return fail(c, SGV_ERR_ARG, "sgv_set_ld_block_csr: %lld entries without indices/data",
+                (long long)indptr[n]);
   if (indptr[0] != 0) return fail(c, SGV_ERR_ARG, "sgv_set_ld_block_csr: indptr[0] != 0");
   int64_t bw = 0;
   for (int64_t i = 0; i < n; ++i) {
