@@ -31,6 +31,8 @@ __global__ __launch_bounds__(256, OCC) void k_sym_pass(const SymItem* __restrict
   // per-wave column partials: lane l owns columns 2l, 2l+1 of every segment,
   // so read-modify-writes are private; waves are summed in order at the end
   __shared__ d2 cbw[4][NC][CW / 2];
+  // the item's row sums, stored as one contiguous 16-B-store burst at the end
+  __shared__ __attribute__((aligned(16))) double rbuf[SYM_H * NC];
 
   const SymItem it = items[blockIdx.x];
   if (pa.run && !ldg(pa.run)) return;   // no-op pass (pipelined CG past its stop test)
@@ -114,7 +116,18 @@ __global__ __launch_bounds__(256, OCC) void k_sym_pass(const SymItem* __restrict
     const int idx = (lane >> SH) & (P - 1);
     const int rr = idx / NC, cc = idx % NC;
     if ((lane & ((1 << SH) - 1)) == 0 && idx < RWI * NC && rbase + rr < it.H)
-      rowpart[((int64_t)it.item * SYM_H + rbase + rr) * NC + cc] = y;
+      rbuf[(rbase + rr) * NC + cc] = y;
+  }
+  __syncthreads();
+  {
+    const int n = it.H * NC;
+    double* dst = rowpart + (int64_t)it.item * SYM_H * NC;
+    for (int i = threadIdx.x; 2 * i < n; i += 256) {
+      if (2 * i + 1 < n)
+        *(d2*)(dst + 2 * i) = *(const d2*)(rbuf + 2 * i);
+      else
+        dst[2 * i] = rbuf[2 * i];
+    }
   }
 
   // column parts: waves 0..3 in order.  The item's whole NC x CW slot is
