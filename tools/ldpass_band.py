@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""LD-pass microbenchmark for sparse / windowed LD stored as packed bands
+(sgv_set_ld_block_csr): one band of M markers and bandwidth bw built on the host
+(oracle.vamp_oracle.banded_ld, a few taps so it is cheap at any size), uploaded as
+CSR, then kernel time per pass (HIP events) for 1..16 right-hand sides.  The
+stored bytes are the band's panels (round_up(256 + bw, 512) columns per 256-row
+panel); the "csr_equiv" rate counts the 12 B per stored nonzero (8-B value +
+4-B index) a CSR mat-vec would stream instead.
+
+  python tools/ldpass_band.py --M 200000 --bw 2000 --ncols 1,2,8,16"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sgvamp-py_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, default=200000)
+    ap.add_argument("--bw", type=int, default=2000)
+    ap.add_argument("--taps", type=int, default=12)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--ncols", default="1,2,8,16")
+    a = ap.parse_args()
+    from engine import Engine
+    from oracle import vamp_oracle as vo
+    from sgvamp import BlockLD
+
+    t0 = time.time()
+    A = vo.banded_ld(a.M, a.bw, seed=1, taps=a.taps)
+    L = BlockLD.from_csr(A)
+    eng = Engine(L.block_sizes, K=1)
+    for b in range(len(L.block_sizes)):
+        L.upload(eng, 0, b)
+    fmts = sorted({eng.ld_block_format(0, b) for b in range(len(L.block_sizes))})
+    print("[band] M=%d bw=%d nnz=%d blocks=%d formats=%s setup %.1f s" % (
+        a.M, a.bw, A.nnz, len(L.block_sizes), fmts, time.time() - t0), file=sys.stderr)
+    rs = np.random.RandomState(0)
+    for nc in [int(x) for x in a.ncols.split(",")]:
+        V = rs.normal(size=(nc, a.M))
+        eng.ld_matvec(0, V)
+        eng.timers(reset=True)
+        for _ in range(a.reps):
+            eng.ld_matvec(0, V)
+        t = eng.timers()
+        ms = t["ld_ms"] / t["ld_launches"]
+        print(json.dumps(dict(M=a.M, bw=a.bw, ncol=nc, ms_per_pass=ms,
+                              stored_GB=t["ld_bytes"] / t["ld_launches"] / 1e9,
+                              stored_GBs=t["ld_bytes"] / t["ld_launches"] / ms / 1e6,
+                              frac_of_8TBs=t["ld_bytes"] / t["ld_launches"] / ms / 1e6 / 8000.0,
+                              csr_equiv_GBs=12.0 * A.nnz / ms / 1e6)), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
