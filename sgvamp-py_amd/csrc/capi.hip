@@ -126,6 +126,15 @@ static bool em_fuse_default() {
 }
 static int sym_class_nc(int cls) { return std::min(16, 2 << (cls + 1)); }   // widest NC using cls
 
+// The one-workgroup reduction + control kernels (k_cg_reduce_ctl,
+// k_em_reduce_ctl) walk nv x nblk (value, block) pairs 128 at a time, each round
+// a chain of dependent loads; above one round the two-launch form (k_reduce_local
+// over nv workgroups, then the one-wave control kernel; the same bits) is
+// faster: at 64 blocks 58 / 40 us fused vs ~9 + 5 us (north-star trace).
+static bool fused_ctl_pays(int nv, int nblk) {
+  return nblk <= EM_CTL_MAXBLK && nv * nblk <= 128;
+}
+
 struct sgv_ctx {
   int dev = 0;
   hipStream_t st = nullptr;
@@ -951,8 +960,9 @@ static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const d
   const volatile CgState* last = nullptr;
   int executed = 0;
   // one rank: iteration it's r.r reduction and the control of it + 1 are one
-  // launch (k_cg_reduce_ctl), enqueued at the end of it; SGV_EM_FUSE=0 A/B
-  const bool fuse = !c->comm && !c->host_ag && c->nblk <= EM_CTL_MAXBLK && em_fuse_default();
+  // launch (k_cg_reduce_ctl), enqueued at the end of it, when that one
+  // workgroup's reduction is short (fused_ctl_pays); SGV_EM_FUSE=0 A/B
+  const bool fuse = !c->comm && !c->host_ag && fused_ctl_pays(MAXC, c->nblk) && em_fuse_default();
   for (int it = 0; it < maxiter; ++it) {
     const size_t np0 = c->pending.size();
     const double cnt0[5] = {c->ld_launches, c->ld_bytes, c->dense_bytes, c->rhs_bytes,
@@ -1891,7 +1901,7 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
     // SGV_EM_FUSE=0 A/B.  With a communicator: the replicated EM (em_rep_setup)
     // runs the same one-rank loop over every rank's gathered r1.
     const bool rep = c->em_rep;
-    const bool fuse = rep || (!c->comm && !c->host_ag && c->nblk <= EM_CTL_MAXBLK &&
+    const bool fuse = rep || (!c->comm && !c->host_ag && fused_ctl_pays(EM_NV, c->nblk) &&
                               em_fuse_default());
     const ChunkDesc* ech = rep ? c->d_chg : c->d_ch;
     const int* ebeg = rep ? c->d_chg_begin : c->d_ch_begin;

@@ -60,6 +60,29 @@ def main():
     for nc in (1, 2, 8, 16):
         print("matvec band nc=%d %s" % (nc, h(eng.ld_matvec(0, W[:nc]))))
     eng.close()
+    # many blocks (> 8): the two-launch reduction + control path at one rank
+    import hip_backend as hb
+    sizes = [300] * 20
+    M = sum(sizes)
+    beta = np.zeros(M)
+    beta[rs.choice(M, M // 10, replace=False)] = rs.normal(0, 0.01, M // 10)
+    for K in (1, 2):
+        eng = Engine(sizes, K=K)
+        g = eng.synth_ld_g(0, 5, 250, beta).sum(axis=0)
+        for k in range(K):
+            eng.synth_r(k, 5, 250, g + np.random.RandomState(k).normal(0, 0.4, 250))
+        with tempfile.TemporaryDirectory() as d:
+            v = VAMP(N=[250.0] * K, Nt=250.0 * K, M=M, K=K, rho=0.5, gamw=5.0, gam1=1e-6,
+                     a=[1.0 / K] * K, prior_vars=[0.0, 0.8 / (M // 10) / K],
+                     prior_probs=[0.9, 0.1], out_dir=d, out_name="many", seed=3,
+                     write_files=False)
+            v.attach_engine(eng, x0=beta * np.sqrt(250.0))
+            xh = v.infer(None, None, 5, x0=beta * np.sqrt(250.0), lmmse_damp=True,
+                         prior_update="em")
+            print("vamp many-blocks K=%d %s cg=%s" % (K, h(np.array(xh)),
+                                                     [r["cg_iters"] for r in v.history]))
+        eng.close()
+    del hb
     for name in ("k1_blocks_csr_s_damp", "k4_shared_s_damp", "k10_shared", "k2_mle_L3"):
         c = Case(name)
         f = c.flags
