@@ -169,8 +169,8 @@ struct sgv_ctx {
   int8_t* h_probe[2] = {nullptr, nullptr};
   hipEvent_t ev_probe[2] = {nullptr, nullptr};
   int8_t* d_probe = nullptr;
-  size_t probe_cap = 0;
-  int probe_slot = 0;
+  std::atomic<size_t> probe_cap{0};            // stored after the buffers (read by sgv_step_begin)
+  std::atomic<int> probe_slot{0};             // next slot (sgv_step_begin stages from the caller's thread)
   hipEvent_t ev_unpk[2] = {nullptr, nullptr};   // the slot's probes consumed (ctx stream)
   int pref_slot = -1;                           // probes prefetched by sgv_step
   const int8_t* pref_src = nullptr;
@@ -425,6 +425,20 @@ static int h2d(sgv_ctx* c, const void* host, size_t bytes) {
   return stream_wait(c);
 }
 
+// host half of a probe upload: the next pinned slot, once its previous copy
+// has finished (long done), takes the K x Mloc probes; returns the slot or -1.
+// Needs the buffers (probe_cap) in place; touches nothing a running step uses.
+static int probe_stage(sgv_ctx* c, const int8_t* probes) {
+  const int slot = c->probe_slot.fetch_xor(1);
+  if (hipEventSynchronize(c->ev_probe[slot]) != hipSuccess) {
+    fail(c, SGV_ERR_HIP, "probe slot wait failed");
+    return -1;
+  }
+  std::memcpy(c->h_probe[slot], probes, (size_t)c->K * c->Mloc);
+  return slot;
+}
+static int probe_issue(sgv_ctx* c, int slot, int* slot_out);
+
 // K x Mloc int8 probes -> d_probe slot, copied on the copy stream (no host wait);
 // returns the slot.  A slot's device half is consumed by the unpack kernels of
 // its step (ev_unpk) and reused two uploads later.
@@ -443,13 +457,17 @@ static int probe_upload(sgv_ctx* c, const int8_t* probes, int* slot_out) {
     if (c->d_probe) HIPCHK(hipFree(c->d_probe));
     c->d_probe = nullptr;
     HIPCHK(hipMalloc(&c->d_probe, 2 * bytes));
-    c->probe_cap = bytes;
+    c->probe_cap.store(bytes, std::memory_order_release);
   }
-  const int slot = c->probe_slot;
-  c->probe_slot ^= 1;
-  HIPCHK(hipEventSynchronize(c->ev_probe[slot]));   // this slot's previous copy (long done)
-  std::memcpy(c->h_probe[slot], probes, (size_t)c->K * c->Mloc);
-  HIPCHK(hipStreamWaitEvent(c->st_copy, c->ev_unpk[slot], 0));   // its previous unpack
+  const int slot = probe_stage(c, probes);
+  if (slot < 0) return SGV_ERR_HIP;
+  return probe_issue(c, slot, slot_out);
+}
+
+// device half of an upload staged by probe_stage: behind the slot's previous
+// unpack (ev_unpk), on the copy stream
+static int probe_issue(sgv_ctx* c, int slot, int* slot_out) {
+  HIPCHK(hipStreamWaitEvent(c->st_copy, c->ev_unpk[slot], 0));
   HIPCHK(hipMemcpyAsync(c->d_probe + slot * c->probe_cap, c->h_probe[slot],
                         (size_t)c->K * c->Mloc, hipMemcpyHostToDevice, c->st_copy));
   HIPCHK(hipEventRecord(c->ev_probe[slot], c->st_copy));
@@ -2497,13 +2515,12 @@ extern "C" int sgv_sync(sgv_ctx* c) {
 // one outer iteration in the shim (src/sgvamp.py:222-387 minus the files and
 // logs): the host returns to the caller once, not between the phases
 // ---------------------------------------------------------------------------
-extern "C" int sgv_step(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
-                        const double* sigmas, const double* a, double* lam_io, double* omegas_io,
-                        const double* gam1s, double rho, const double* gamw,
-                        const double* alpha1_prev, const double* alpha2_prev,
-                        const int8_t* probes, int cg_maxit, double rtol, int out_slot,
-                        double* res, int* ires, double* out, int* cg_out) {
-  ENTER(c);
+static int step_impl(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
+                     const double* sigmas, const double* a, double* lam_io, double* omegas_io,
+                     const double* gam1s, double rho, const double* gamw,
+                     const double* alpha1_prev, const double* alpha2_prev,
+                     const int8_t* probes, int cg_maxit, double rtol, int out_slot,
+                     double* res, int* ires, double* out, int* cg_out, int staged) {
   if (!sigmas || !a || !lam_io || !omegas_io || !gam1s || !gamw || !alpha1_prev ||
       !alpha2_prev || !probes || !res || !ires || !out || !cg_out || out_slot >= NOUT_SLOTS)
     return fail(c, SGV_ERR_ARG, "sgv_step: bad arguments");
@@ -2512,7 +2529,9 @@ extern "C" int sgv_step(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
   res[0] = 0.0;
   ires[0] = 0;
   // this step's probes go up now, behind nothing: the copy overlaps EM/denoiser
-  CHK(probe_upload(c, probes, &c->pref_slot));
+  // (a step begun behind another had its host copy made by sgv_step_begin)
+  if (staged >= 0) CHK(probe_issue(c, staged, &c->pref_slot));
+  else CHK(probe_upload(c, probes, &c->pref_slot));
   c->pref_src = probes;
   if (flags & SGV_STEP_EM) {   // :250-257
     CHK(sgv_em(c, gam1s, a, nslab, sigmas, em_maxit, lam_io, omegas_io, &ires[0], &res[0]));
@@ -2560,6 +2579,18 @@ extern "C" int sgv_step(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
   return SGV_OK;
 }
 
+extern "C" int sgv_step(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
+                        const double* sigmas, const double* a, double* lam_io, double* omegas_io,
+                        const double* gam1s, double rho, const double* gamw,
+                        const double* alpha1_prev, const double* alpha2_prev,
+                        const int8_t* probes, int cg_maxit, double rtol, int out_slot,
+                        double* res, int* ires, double* out, int* cg_out) {
+  ENTER(c);
+  return step_impl(c, it, flags, em_maxit, nslab, sigmas, a, lam_io, omegas_io, gam1s, rho, gamw,
+                   alpha1_prev, alpha2_prev, probes, cg_maxit, rtol, out_slot, res, ires, out,
+                   cg_out, -1);
+}
+
 // Hand-offs spin (a futex wake costs tens of microseconds, the GPU idles for
 // it): the worker spins up to ~2 ms for the next step before it blocks, and
 // sgv_step_end spins for the step it waits on.  Steps run in begin order.
@@ -2602,6 +2633,14 @@ extern "C" int sgv_step_begin(sgv_ctx* c, int it, int flags, int em_maxit, int n
   const int K = c->K;
   std::vector<double> v_sig(sigmas, sigmas + nslab), v_a(a, a + K), v_g1(gam1s, gam1s + K),
       v_gw(gamw, gamw + K), v_a1(alpha1_prev, alpha1_prev + K), v_a2(alpha2_prev, alpha2_prev + K);
+  // the probes' host copy is made here, while the step ahead runs on the GPU,
+  // so the worker starts this step with the device copy alone (the buffers
+  // come from the first step's upload; until then the worker stages them)
+  int staged = -1;
+  if (probes && c->probe_cap.load(std::memory_order_acquire) >= std::max<size_t>((size_t)K * c->Mloc, 8)) {
+    staged = probe_stage(c, probes);
+    if (staged < 0) return SGV_ERR_HIP;
+  }
   j.fn = [=]() mutable {
     if (flags & SGV_STEP_CHAIN) {
       const sgv_ctx::Chain& ch = c->chain;
@@ -2615,9 +2654,10 @@ extern "C" int sgv_step_begin(sgv_ctx* c, int it, int flags, int em_maxit, int n
       *lam_io = ch.lam;
       for (int l = 0; l < nslab; ++l) omegas_io[l] = ch.om[l];
     }
-    return sgv_step(c, it, flags & ~SGV_STEP_CHAIN, em_maxit, nslab, v_sig.data(), v_a.data(),
-                    lam_io, omegas_io, v_g1.data(), rho, v_gw.data(), v_a1.data(), v_a2.data(),
-                    probes, cg_maxit, rtol, out_slot, res, ires, out, cg_out);
+    ENTER(c);
+    return step_impl(c, it, flags & ~SGV_STEP_CHAIN, em_maxit, nslab, v_sig.data(), v_a.data(),
+                     lam_io, omegas_io, v_g1.data(), rho, v_gw.data(), v_a1.data(), v_a2.data(),
+                     probes, cg_maxit, rtol, out_slot, res, ires, out, cg_out, staged);
   };
   {
     std::lock_guard<std::mutex> lk(c->wmu);   // a worker about to block sees the job
