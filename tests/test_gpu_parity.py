@@ -122,6 +122,37 @@ def test_ld_matvec_symmetry_and_linearity_large():
     eng2.close()
 
 
+def test_north_star_full_size_pass_properties():
+    """The north-star LD (M = 1e6 in 64 blocks of 15,625, 63.5 GB packed) through
+    the bench's 8-column MFMA pass: symmetry u^T(Rv) = v^T(Ru) and linearity over
+    all of M, two columns against the one-column VALU pass, and the first and
+    last blocks against numpy on the blocks read back."""
+    sizes = [15625] * 64
+    M = sum(sizes)
+    eng = Engine(sizes, K=1)
+    eng.synth_ld_g(0, 7, 2000, np.zeros(M))
+    assert eng.ld_block_format(0, 0) == 1
+    rs = np.random.RandomState(3)
+    U = rs.normal(size=(8, M))
+    U[7] = 0.3 * U[0] - 1.7 * U[1]
+    Y = eng.ld_matvec(0, U)
+    for i, j in ((0, 1), (2, 5), (3, 6)):
+        assert abs(U[i] @ Y[j] - U[j] @ Y[i]) <= 1e-11 * abs(U[i] @ Y[j])
+    assert maxrel(Y[7], 0.3 * Y[0] - 1.7 * Y[1]) < 1e-11
+    eng.set_mfma_min(0)
+    for j in (0, 6):
+        assert maxrel(Y[j], eng.ld_matvec(0, U[j:j + 1])[0]) < 1e-12
+    eng.set_mfma_min(3)
+    for b in (0, 63):
+        B = eng.get_ld_block(0, b)
+        np.testing.assert_array_equal(B, B.T)
+        sl = slice(b * 15625, (b + 1) * 15625)
+        ref = U[:, sl] @ B                     # B symmetric: rows of (B U^T)^T
+        del B
+        assert maxrel(Y[:, sl], ref) < 1e-11
+    eng.close()
+
+
 # ---------------------------------------------------------------------------
 # CG (operator seam con_grad)
 # ---------------------------------------------------------------------------
