@@ -36,8 +36,10 @@ extern "C" {
 #define SGV_ERR_RCCL (-3)
 #define SGV_ERR_STATE (-4)
 
-#define SGV_MAX_COHORTS 32  /* cohorts per context; the LMMSE batches them 8 at a
-                               time (16 CG right-hand sides per LD pass)          */
+#define SGV_MAX_COHORTS 1024 /* cohorts per context (the reference's K is its MPI
+                                world size); the LMMSE batches them 8 at a time
+                                (16 CG right-hand sides per LD pass), the marker
+                                kernels (denoiser, EM, MLE) 32 per launch          */
 #define SGV_MAX_SLABS 8     /* L - 1 slab components of the prior      */
 
 /* vector ids for sgv_set_vector / sgv_get_vector */

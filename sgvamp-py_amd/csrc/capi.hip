@@ -198,8 +198,11 @@ struct sgv_ctx {
   // the last completed sgv_step's results, the inputs of a chained step
   struct Chain {
     int valid = 0;
-    double gam1[MAXK], gamw[MAXK], alpha1[MAXK], alpha2[MAXK], lam, om[MAXL];
+    std::vector<double> gam1, gamw, alpha1, alpha2;   // K each (sgv_create)
+    double lam, om[MAXL];
   } chain;
+  double* d_inner = nullptr;      // K > MAXK: the denoiser's np.inner over all cohorts
+  size_t inner_cap = 0;
   size_t pk_cap = 0;
   // chunk / row-group layouts
   int nch = 0;
@@ -1099,7 +1102,7 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   sgv_ctx* c = nullptr;
   if (!out) return fail(nullptr, SGV_ERR_ARG, "out is null");
   *out = nullptr;
-  if (K < 1 || K > MAXK) return fail(nullptr, SGV_ERR_ARG, "K=%d outside [1,%d]", K, MAXK);
+  if (K < 1 || K > MAXCOH) return fail(nullptr, SGV_ERR_ARG, "K=%d outside [1,%d]", K, MAXCOH);
   if (nld < 1 || nld > K) return fail(nullptr, SGV_ERR_ARG, "nld=%d outside [1,K]", nld);
   if (nblk < 1 || !blk_sizes) return fail(nullptr, SGV_ERR_ARG, "need >= 1 LD block");
   for (int k = 0; k < K; ++k)
@@ -1234,7 +1237,7 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   CREATE_HIP(hipMemcpy(c->d_counts, &nblk, sizeof(int), hipMemcpyHostToDevice));
   CREATE_HIP(hipMalloc(&c->d_tot, sizeof(double) * 64));
   CREATE_HIP(hipMalloc(&c->d_pq, sizeof(double) * 2 * MAXC));
-  CREATE_HIP(hipHostMalloc(&c->h_tot, sizeof(double) * 64, hipHostMallocCoherent));
+  CREATE_HIP(hipHostMalloc(&c->h_tot, sizeof(double) * std::max(64, K), hipHostMallocCoherent));
   CREATE_HIP(hipMalloc(&c->d_cgs, sizeof(CgState)));
   CREATE_HIP(hipMalloc(&c->d_rhonew, sizeof(double) * MAXC));
   CREATE_HIP(hipHostMalloc(&c->h_cgm, sizeof(CgState) * CG_RING, hipHostMallocCoherent));
@@ -1244,7 +1247,11 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   CREATE_HIP(hipEventCreateWithFlags(&c->ev_den, hipEventDisableTiming));
   CREATE_HIP(hipMalloc(&c->d_ems, sizeof(EmState)));
   CREATE_HIP(hipMalloc(&c->d_emtot, sizeof(double) * MAXNV));
-  CREATE_HIP(hipMalloc(&c->d_emtab, sizeof(double) * MAXK * EM_TAB));
+  CREATE_HIP(hipMalloc(&c->d_emtab, sizeof(double) * std::max(K, MAXK) * EM_TAB));
+  c->chain.gam1.assign(K, 0.0);
+  c->chain.gamw.assign(K, 0.0);
+  c->chain.alpha1.assign(K, 0.0);
+  c->chain.alpha2.assign(K, 0.0);
   CREATE_HIP(hipHostMalloc(&c->h_emm, sizeof(EmState) * CG_RING, hipHostMallocCoherent));
   CREATE_HIP(hipHostMalloc(&c->h_emi, sizeof(EmState)));
   for (int i = 0; i < CG_RING; ++i)
@@ -1318,6 +1325,7 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   if (c->h_r1g) (void)hipHostFree(c->h_r1g);
   if (c->d_emtot) (void)hipFree(c->d_emtot);
   if (c->d_emtab) (void)hipFree(c->d_emtab);
+  if (c->d_inner) (void)hipFree(c->d_inner);
   if (c->h_emm) (void)hipHostFree(c->h_emm);
   if (c->h_emi) (void)hipHostFree(c->h_emi);
   for (hipEvent_t e : c->ev_em)
@@ -1420,6 +1428,7 @@ static int gather_f64(sgv_ctx* c, const double* d_send, double* d_recv, size_t c
 // SGV_EM_REP=0/1 (with SGV_AB=1) forces either.
 constexpr double EM_REP_MAX_KM = 1048576.0;
 static bool em_rep_choice(const sgv_ctx* c) {
+  if (c->K > MAXK) return false;   // the replicated loop runs one cohort group
   const char* e = ab_env("SGV_EM_REP");
   if (e) return e[0] != '0';
   return (double)c->K * (double)c->Mtot <= EM_REP_MAX_KM;
@@ -1843,17 +1852,14 @@ static int denoise_enqueue(sgv_ctx* c, const double* gam1s, const double* a, dou
                            int damp) {
   DenoiseArgs da{};
   da.xhat1 = c->xhat1;
-  da.K = c->K;
   da.nslab = nslab;
   da.lam = lam;
   da.rho = rho;
   da.damp = damp;
+  da.write_x = 1;
   for (int k = 0; k < c->K; ++k) {
-    da.r1[k] = c->r1[k];
-    da.a[k] = a[k];
-    da.gam1[k] = gam1s[k];
-    da.ag[k] = a[k] * gam1s[k];                        // self.a * gam1s
-    da.sum_ag = (k == 0) ? da.ag[0] : da.sum_ag + da.ag[k];   // builtin sum (:95)
+    const double ag = a[k] * gam1s[k];                 // self.a * gam1s
+    da.sum_ag = (k == 0) ? ag : da.sum_ag + ag;        // builtin sum (:95)
   }
   for (int l = 0; l < nslab; ++l) {
     da.omegas[l] = omegas[l];
@@ -1861,8 +1867,34 @@ static int denoise_enqueue(sgv_ctx* c, const double* gam1s, const double* a, dou
     da.s2[l] = 1.0 / (da.sum_ag + 1.0 / sigmas[l]);     // :95
     da.sq[l] = std::sqrt(da.s2[l] / sigmas[l]);         // np.sqrt(sigma2_meta / sigmas)
   }
-  HIPCHK(launch_denoise(c->d_ch, c->nch, da, c->d_part, c->st));
-  CHK(reduce_dev(c, c->K, c->d_ch_begin, identity_map(), c->h_tot));
+  // more than MAXK cohorts: groups of MAXK.  np.inner over all of them first
+  // (one sequential sum continued group to group), then one launch per group
+  // for its cohorts' derivative sums; the first also writes xhat1
+  const int ng = (c->K + MAXK - 1) / MAXK;
+  auto group = [&](int g) {
+    da.K = std::min(MAXK, c->K - g * MAXK);
+    for (int k = 0; k < da.K; ++k) {
+      const int kk = g * MAXK + k;
+      da.r1[k] = c->r1[kk];
+      da.a[k] = a[kk];
+      da.gam1[k] = gam1s[kk];
+      da.ag[k] = a[kk] * gam1s[kk];
+    }
+  };
+  if (ng > 1) {
+    CHK(grow(c, &c->d_inner, &c->inner_cap, (size_t)std::max<int64_t>(c->Mpad, 1)));
+    for (int g = 0; g < ng; ++g) {
+      group(g);
+      HIPCHK(launch_den_inner(c->d_ch, c->nch, da, c->d_inner, g == 0 ? 1 : 0, c->st));
+    }
+    da.inner = c->d_inner;
+  }
+  for (int g = 0; g < ng; ++g) {
+    group(g);
+    da.write_x = g == 0 ? 1 : 0;
+    HIPCHK(launch_denoise(c->d_ch, c->nch, da, c->d_part, c->st));
+    CHK(reduce_dev(c, da.K, c->d_ch_begin, identity_map(), c->h_tot + g * MAXK));
+  }
   return SGV_OK;
 }
 
@@ -1888,18 +1920,34 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
   ENTER(c);
   if (nslab < 1 || nslab > MAXL || !gam1s || !a || !sigmas || !lam_io || !omegas_io)
     return fail(c, SGV_ERR_ARG, "sgv_em: bad arguments");
-  EmArgs ea{};
-  ea.K = c->K;
-  ea.nslab = nslab;
-  for (int k = 0; k < c->K; ++k) {
-    ea.r1[k] = c->r1[k];
-    ea.a[k] = a[k];
-    ea.gam1[k] = gam1s[k];
-    ea.scl = (k == 0) ? a[0] : ea.scl + a[k];
+  // more than MAXK cohorts: one k_em launch per group of MAXK, the later ones
+  // adding to the first's partials (each marker's cohort sum then runs group
+  // by group); np.average's weight sum covers all cohorts
+  const int ngr = (c->K + MAXK - 1) / MAXK;
+  std::vector<EmArgs> eg(ngr);
+  EmArgs& ea = eg[0];
+  double scl = 0.0;
+  for (int k = 0; k < c->K; ++k) scl = (k == 0) ? a[0] : scl + a[k];
+  for (int g = 0; g < ngr; ++g) {
+    EmArgs& e = eg[g];
+    e = EmArgs{};
+    e.K = std::min(MAXK, c->K - g * MAXK);
+    e.nslab = nslab;
+    for (int k = 0; k < e.K; ++k) {
+      e.r1[k] = c->r1[g * MAXK + k];
+      e.a[k] = a[g * MAXK + k];
+      e.gam1[k] = gam1s[g * MAXK + k];
+    }
+    e.scl = scl;
+    e.accum = g > 0 ? 1 : 0;
+    for (int l = 0; l < nslab; ++l) e.sigmas[l] = sigmas[l];
+    e.tab = c->d_emtab + (size_t)g * MAXK * EM_TAB;
+    HIPCHK(launch_em_prep(e, c->d_emtab + (size_t)g * MAXK * EM_TAB, c->st));
   }
-  for (int l = 0; l < nslab; ++l) ea.sigmas[l] = sigmas[l];
-  ea.tab = c->d_emtab;
-  HIPCHK(launch_em_prep(ea, c->d_emtab, c->st));
+  auto em_groups = [&](const ChunkDesc* ch, int nch, double* part) -> int {
+    for (int g = 0; g < ngr; ++g) HIPCHK(launch_em(ch, nch, eg[g], part, c->st));
+    return SGV_OK;
+  };
   double lam = *lam_io;
   double om[MAXL];
   for (int l = 0; l < nslab; ++l) om[l] = omegas_io[l];
@@ -1914,7 +1962,7 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
     hi->lam = lam;
     for (int l = 0; l < nslab; ++l) hi->om[l] = om[l];
     HIPCHK(hipMemcpyAsync(c->d_ems, hi, sizeof(EmState), hipMemcpyHostToDevice, c->st));
-    ea.st = c->d_ems;
+    for (EmArgs& e : eg) e.st = c->d_ems;
     // one rank: reduction + control in one launch (k_em_reduce_ctl, same bits);
     // SGV_EM_FUSE=0 A/B.  With a communicator: the replicated EM (em_rep_setup)
     // runs the same one-rank loop over every rank's gathered r1.
@@ -1931,13 +1979,13 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
     }
     auto enqueue = [&](int j) -> int {
       if (fuse) {
-        HIPCHK(launch_em(ech, ench, ea, epart, c->st));
+        CHK(em_groups(ech, ench, epart));
         const EmCtl f{ebeg, enb, nslab, c->h_emm + j % CG_RING, (double)c->Mtot, j, maxit};
         HIPCHK(launch_em_reduce_ctl(epart, c->d_ems, f, c->st));
         HIPCHK(hipEventRecord(c->ev_em[j % CG_RING], c->st));
         return SGV_OK;
       }
-      HIPCHK(launch_em(c->d_ch, c->nch, ea, c->d_part, c->st));
+      CHK(em_groups(c->d_ch, c->nch, c->d_part));
       CHK(reduce_dev(c, EM_NV, c->d_ch_begin, identity_map(), c->d_emtot));
       HIPCHK(launch_em_ctl(c->d_ems, c->h_emm + j % CG_RING, c->d_emtot, nslab, (double)c->Mtot,
                            j, maxit, c->st));
@@ -1961,9 +2009,11 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
   double om_err = 0.0, lam_err = 0.0;
   int steps = 0;
   for (int it = 0; it < maxit; ++it) {
-    ea.lam = lam;
-    for (int l = 0; l < nslab; ++l) ea.omegas[l] = om[l];
-    HIPCHK(launch_em(c->d_ch, c->nch, ea, c->d_part, c->st));
+    for (EmArgs& e : eg) {
+      e.lam = lam;
+      for (int l = 0; l < nslab; ++l) e.omegas[l] = om[l];
+    }
+    CHK(em_groups(c->d_ch, c->nch, c->d_part));
     double tot[EM_NV];
     CHK(reduce_host(c, EM_NV, c->d_ch_begin, tot));
     const double lam_new = tot[0] / (double)c->Mtot;   // np.mean (:134)
@@ -1996,14 +2046,16 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
 // MLE prior update (src/sgvamp.py:139-194): the K x M x L sums of
 // Lagrangian_der on the device; fsolve (MINPACK hybrd) stays on the host
 // ---------------------------------------------------------------------------
-static int mle_args(sgv_ctx* c, const double* gam1s, int L, const double* sigma2, MleArgs* m) {
+// cohort group g (MAXK cohorts from g * MAXK)
+static int mle_args(sgv_ctx* c, const double* gam1s, int L, const double* sigma2, int g,
+                    MleArgs* m) {
   if (!gam1s || !sigma2 || L < 1 || L > MAXL + 1) return fail(c, SGV_ERR_ARG, "bad MLE arguments");
   *m = MleArgs{};
-  m->K = c->K;
+  m->K = std::min(MAXK, c->K - g * MAXK);
   m->L = L;
-  for (int k = 0; k < c->K; ++k) {
-    m->r1[k] = c->r1[k];
-    m->ginv[k] = 1.0 / gam1s[k];                             // :146
+  for (int k = 0; k < m->K; ++k) {
+    m->r1[k] = c->r1[g * MAXK + k];
+    m->ginv[k] = 1.0 / gam1s[g * MAXK + k];                 // :146
   }
   for (int l = 0; l < L; ++l) m->sigma2[l] = sigma2[l];
   return SGV_OK;
@@ -2013,15 +2065,17 @@ extern "C" int sgv_mle_exp_max(sgv_ctx* c, const double* gam1s, int L, const dou
                                double* exp_max) {
   ENTER(c);
   if (!exp_max) return fail(c, SGV_ERR_ARG, "exp_max is null");
-  MleArgs m;
-  CHK(mle_args(c, gam1s, L, sigma2, &m));
-  HIPCHK(launch_mle_minsq(c->d_ch, c->nch, m, c->d_part, c->st));
-  double mn[MAXK];
-  CHK(reduce_host(c, MAXK, c->d_ch_begin, mn, /*op=min*/ 1));
   // :152: max over (k, m, l) of (-r1^2 / 2) / v_kl, attained at min_m r1_km^2
   double best = -std::numeric_limits<double>::infinity();
-  for (int k = 0; k < c->K; ++k)
-    for (int l = 0; l < L; ++l) best = std::max(best, -mn[k] / 2.0 / (m.sigma2[l] + m.ginv[k]));
+  for (int g = 0; g * MAXK < c->K; ++g) {
+    MleArgs m;
+    CHK(mle_args(c, gam1s, L, sigma2, g, &m));
+    HIPCHK(launch_mle_minsq(c->d_ch, c->nch, m, c->d_part, c->st));
+    double mn[MAXK];
+    CHK(reduce_host(c, MAXK, c->d_ch_begin, mn, /*op=min*/ 1));
+    for (int k = 0; k < m.K; ++k)
+      for (int l = 0; l < L; ++l) best = std::max(best, -mn[k] / 2.0 / (m.sigma2[l] + m.ginv[k]));
+  }
   *exp_max = best;
   return SGV_OK;
 }
@@ -2031,15 +2085,18 @@ extern "C" int sgv_mle_terms(sgv_ctx* c, const double* a, const double* gam1s, i
                              double* sums) {
   ENTER(c);
   if (!a || !omega || !sums) return fail(c, SGV_ERR_ARG, "bad MLE arguments");
-  MleArgs m;
-  CHK(mle_args(c, gam1s, L, sigma2, &m));
-  for (int k = 0; k < c->K; ++k) m.a[k] = a[k];
-  for (int l = 0; l < L; ++l) m.omega[l] = omega[l];
-  m.exp_max = exp_max;
-  HIPCHK(launch_mle_terms(c->d_ch, c->nch, m, c->d_part, c->st));
-  double tot[MAXL + 1];
-  CHK(reduce_host(c, MAXL + 1, c->d_ch_begin, tot));
-  for (int l = 0; l < L; ++l) sums[l] = tot[l];
+  // one launch per cohort group; the groups' totals are added in group order
+  for (int g = 0; g * MAXK < c->K; ++g) {
+    MleArgs m;
+    CHK(mle_args(c, gam1s, L, sigma2, g, &m));
+    for (int k = 0; k < m.K; ++k) m.a[k] = a[g * MAXK + k];
+    for (int l = 0; l < L; ++l) m.omega[l] = omega[l];
+    m.exp_max = exp_max;
+    HIPCHK(launch_mle_terms(c->d_ch, c->nch, m, c->d_part, c->st));
+    double tot[MAXL + 1];
+    CHK(reduce_host(c, MAXL + 1, c->d_ch_begin, tot));
+    for (int l = 0; l < L; ++l) sums[l] = g == 0 ? tot[l] : sums[l] + tot[l];
+  }
   return SGV_OK;
 }
 
@@ -2545,9 +2602,7 @@ static int step_impl(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
   if (out_slot >= 0) CHK(sgv_outputs_begin(c, out_slot));
   if (flags & SGV_STEP_METRICS) CHK(sgv_metrics_begin(c));
   CHK(event_spin(c, c->ev_den));
-  double der[MAXK];
-  for (int k = 0; k < K; ++k) der[k] = c->h_tot[k];
-  double alpha1[MAXK], gam2[MAXK];
+  std::vector<double> der(c->h_tot, c->h_tot + K), alpha1(K), gam2(K);
   for (int k = 0; k < K; ++k) {
     double a1 = der[k] / (double)c->Mtot;                           // np.mean (:285)
     if (flags & SGV_STEP_ALPHA1_DAMP) a1 = rho * a1 + (1 - rho) * alpha1_prev[k];   // :290-291
@@ -2557,7 +2612,7 @@ static int step_impl(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
     res[1 + K + k] = gam2[k];
   }
   int passes = 0;
-  CHK(sgv_lmmse(c, it, gamw, gam2, alpha1, alpha2_prev, probes, cg_maxit, rtol,
+  CHK(sgv_lmmse(c, it, gamw, gam2.data(), alpha1.data(), alpha2_prev, probes, cg_maxit, rtol,
                 (flags & SGV_STEP_LMMSE_DAMP) ? 1 : 0, rho, (flags & SGV_STEP_LEARN_GAMW) ? 1 : 0,
                 out, cg_out, &passes));
   ires[1] = passes;

@@ -11,7 +11,8 @@ constexpr int VTHREADS = 256;   // threads per workgroup of the vector kernels
 constexpr int CHUNK = 1024;     // markers per chunk (vector-kernel workgroup)
 constexpr int PADV = 128;       // per-block padding of device vectors and LD rows (doubles = 1 KiB)
 constexpr int MAXC = 16;        // right-hand-side columns per LD pass (2 x MAXKG cohorts)
-constexpr int MAXK = 32;        // cohorts
+constexpr int MAXK = 32;        // cohorts per launch of the marker kernels (more: cohort groups)
+constexpr int MAXCOH = 1024;    // cohorts per context (SGV_MAX_COHORTS)
 constexpr int MAXKG = 8;        // cohorts per LMMSE group (one batched CG loop, <= MAXC columns)
 constexpr int MAXL = 8;         // slab components (L - 1)
 
@@ -330,9 +331,17 @@ struct DenoiseArgs {
   double sq[MAXL];          // sqrt(sigma2_meta / sigmas)
   double rho;
   int damp;
+  // cohort groups (K > MAXK): np.inner over every cohort precomputed by
+  // launch_den_inner; only the first group writes xhat1 (with the damping)
+  const double* inner;
+  int write_x;
 };
 hipError_t launch_denoise(const ChunkDesc* d_ch, int nch, const DenoiseArgs& a, double* d_part,
                           hipStream_t st);
+// inner[i] = (first ? 0 : inner[i]) + sum over the a.K cohorts of r1_k[i] * ag_k,
+// in cohort order (continuing one sequential sum over the groups)
+hipError_t launch_den_inner(const ChunkDesc* d_ch, int nch, const DenoiseArgs& a, double* inner,
+                            int first, hipStream_t st);
 
 struct MleArgs {
   const double* r1[MAXK];
@@ -372,6 +381,7 @@ struct EmArgs {
   double lam;
   int K, nslab;
   double omegas[MAXL], sigmas[MAXL];
+  int accum;                // cohort groups after the first add to the partials
 };
 constexpr int EM_NV = MAXL + 2;   // [0] sum_j avg_k(pi); [1..L-1] omega numerators; [nslab+1] denominator
 hipError_t launch_em(const ChunkDesc* d_ch, int nch, const EmArgs& a, double* d_part,

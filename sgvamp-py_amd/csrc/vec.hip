@@ -70,10 +70,14 @@ __global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restric
     const int t = threadIdx.x + j * VTHREADS;
     if (t < ch.len) {
       const int64_t i = ch.voff + t;
+      if (a.inner) {
+        vr[j][0] = a.inner[i];
+      } else {
 #pragma unroll
-      for (int k = 0; k < KM; ++k)
-        if (k < a.K) vr[j][k] = a.r1[k][i];
-      if (a.damp) vxo[j] = a.xhat1[i];
+        for (int k = 0; k < KM; ++k)
+          if (k < a.K) vr[j][k] = a.r1[k][i];
+      }
+      if (a.damp && a.write_x) vxo[j] = a.xhat1[i];
     }
   }
 #pragma unroll
@@ -83,9 +87,13 @@ __global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restric
     const int64_t i = ch.voff + t;
     // np.inner(rs, a*gam1s) (:96)
     double inner = 0.0;
+    if (a.inner) {
+      inner = vr[j][0];
+    } else {
 #pragma unroll
-    for (int k = 0; k < KM; ++k)
-      if (k < a.K) inner = (k == 0) ? vr[j][0] * a.ag[0] : inner + vr[j][k] * a.ag[k];
+      for (int k = 0; k < KM; ++k)
+        if (k < a.K) inner = (k == 0) ? vr[j][0] * a.ag[0] : inner + vr[j][k] * a.ag[k];
+    }
     double mu[MAXL];
     int m = 0;
     double best = 0.0;
@@ -120,9 +128,11 @@ __global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restric
     const double Num = a.lam * sumN;
     const double EXP2 = exp(-0.5 * (mum * mum / s2m));   // :100
     const double Den = (1 - a.lam) * EXP2 + a.lam * sumD;
-    double x = Num / Den;
-    if (a.damp) x = a.rho * x + (1 - a.rho) * vxo[j];   // :275-276
-    a.xhat1[i] = x;
+    if (a.write_x) {
+      double x = Num / Den;
+      if (a.damp) x = a.rho * x + (1 - a.rho) * vxo[j];   // :275-276
+      a.xhat1[i] = x;
+    }
     // der_denoiser_meta for every cohort k (:112-114 with a[k]*gam1s[k])
 #pragma unroll
     for (int k = 0; k < KM; ++k)
@@ -156,6 +166,25 @@ hipError_t launch_denoise(const ChunkDesc* d_ch, int nch, const DenoiseArgs& a, 
   else if (a.K <= 16) L_DEN(16);
   else L_DEN(MAXK);
 #undef L_DEN
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(VTHREADS) void k_den_inner(const ChunkDesc* __restrict__ chs,
+                                                        DenoiseArgs a, double* __restrict__ inner,
+                                                        int first) {
+  const ChunkDesc ch = chs[blockIdx.x];
+  CHUNK_LOOP(ch) {
+    const int64_t i = ch.voff + t;
+    double s = first ? a.r1[0][i] * a.ag[0] : inner[i] + a.r1[0][i] * a.ag[0];
+    for (int k = 1; k < a.K; ++k) s = s + a.r1[k][i] * a.ag[k];
+    inner[i] = s;
+  }
+}
+
+hipError_t launch_den_inner(const ChunkDesc* d_ch, int nch, const DenoiseArgs& a, double* inner,
+                            int first, hipStream_t st) {
+  if (a.K < 1 || a.K > MAXK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_den_inner, dim3(nch), dim3(VTHREADS), 0, st, d_ch, a, inner, first);
   return hipGetLastError();
 }
 
@@ -246,7 +275,8 @@ __device__ __forceinline__ bool em_partials(const ChunkDesc* __restrict__ chs, c
     double x = sm[0][t];
 #pragma unroll
     for (int q = 1; q < EM_THREADS / WAVE; ++q) x += sm[q][t];
-    part[(int64_t)blockIdx.x * EM_NV + t] = x;
+    double* dst = part + (int64_t)blockIdx.x * EM_NV + t;
+    *dst = a.accum ? *dst + x : x;
   }
   return true;
 }

@@ -19,7 +19,7 @@ O_TRSIGMA2, O_ALPHA2, O_GAM1, O_Z, O_TRRSIGMA2, O_GAMW, O_XR, O_XRX = range(8)
 STEP_EM, STEP_DENOISE_DAMP, STEP_ALPHA1_DAMP, STEP_LMMSE_DAMP, STEP_LEARN_GAMW, STEP_METRICS, \
     STEP_CHAIN = 1, 2, 4, 8, 16, 32, 64
 OUT_SLOTS = 3
-MAX_COHORTS = 32
+MAX_COHORTS = 1024
 MAX_SLABS = 8
 
 _c_int_p = ctypes.POINTER(ctypes.c_int)

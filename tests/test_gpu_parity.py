@@ -853,3 +853,45 @@ def test_mle_prior_many_cohorts_vs_oracle(tmp_path):
     assert [h["cg_iters"] for h in v.history] == [[list(c) for c in x] for x in t["cg_iters"]]
     assert [h.get("mle_warning") for h in v.history if h.get("mle_warning")] == t["mle_warnings"]
     eng.close()
+
+
+@pytest.mark.parametrize("K,update", [(40, "em"), (40, "mle"), (70, "em")])
+def test_more_cohorts_than_one_launch_vs_oracle(K, update, tmp_path):
+    """More than 32 cohorts (the marker kernels' per-launch bound): the denoiser,
+    EM and MLE run in cohort groups of 32 (np.inner continued group to group,
+    EM partials added group after group, MLE totals in group order), the LMMSE
+    in groups of 8; against the oracle on the same device-generated inputs
+    (src/main.py:62,90-93: the reference's K is its MPI world size)."""
+    sizes = [600, 500]
+    nsamp = 700
+    M = sum(sizes)
+    rs = np.random.RandomState(41)
+    cm = M // 10
+    beta = np.zeros(M)
+    beta[rs.choice(M, cm, replace=False)] = rs.normal(0, np.sqrt(0.8 / cm), cm)
+    eng = Engine(sizes, K=K)
+    g = eng.synth_ld_g(0, 56, nsamp, beta).sum(axis=0)
+    rvec = []
+    for k in range(K):
+        y = g + np.random.RandomState(400 + k).normal(0, np.sqrt(0.2), nsamp)
+        eng.synth_r(k, 56, nsamp, y)
+        rvec.append(eng.get_vector(hb.VEC_R, k).copy())
+    blocks = [eng.get_ld_block(0, b) for b in range(len(sizes))]
+    N = [float(nsamp)] * K
+    prior = dict(prior_vars=[0.0, 0.8 / cm / K], prior_probs=[0.9, 0.1])
+    x0 = beta * np.sqrt(nsamp)
+    v = VAMP(N=N, Nt=sum(N), M=M, K=K, rho=0.5, gamw=5.0, gam1=1e-6, a=[1 / K] * K,
+             out_dir=str(tmp_path), out_name="wide", seed=9, write_files=False, **prior)
+    v.attach_engine(eng, x0=x0)
+    its = 4
+    xh = v.infer(None, None, its, x0=x0, lmmse_damp=False, prior_update=update)
+    L = vo.BlockLD(blocks)
+    t = vo.infer([L], [0] * K, rvec, N, its, rho=0.5, gamw=5.0, gam1=1e-6, x0=x0, seed=9,
+                 lmmse_damp=False, prior_update=update,
+                 reducer=vo.Reducer("blocked", bounds=L.bounds), rs_recurrence=True, **prior)
+    for it in range(its):
+        assert maxrel(xh[it].ravel() / np.sqrt(sum(N)), np.asarray(t["xhat"][it])) < 1e-8, it
+    assert [h["cg_iters"] for h in v.history] == [[list(c) for c in x] for x in t["cg_iters"]]
+    if update == "em":
+        assert [h.get("em_steps") for h in v.history][1:] == list(t["em_steps"])
+    eng.close()
