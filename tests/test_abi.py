@@ -42,6 +42,25 @@ def test_binding_covers_header():
     hb.load()  # types every symbol
 
 
+def test_binding_constants_match_header():
+    """The ctypes binding's constants are the header's #defines."""
+    import hip_backend as hb
+
+    text = open(os.path.join(ROOT, "include", "sgvamp_hip.h")).read()
+    defs = {m.group(1): int(m.group(2))
+            for m in re.finditer(r"^#define (SGV_\w+)\s+\(?(-?\d+)\)?", text, flags=re.M)}
+    pairs = {"SGV_OK": hb.SGV_OK, "SGV_MAX_COHORTS": hb.MAX_COHORTS,
+             "SGV_MAX_SLABS": hb.MAX_SLABS, "SGV_LMMSE_NOUT": hb.LMMSE_NOUT}
+    for n in ("R", "R1", "XHAT1", "XHAT2", "SIG2U", "X0"):
+        pairs["SGV_VEC_" + n] = getattr(hb, "VEC_" + n)
+    for n in ("TRSIGMA2", "ALPHA2", "GAM1", "Z", "TRRSIGMA2", "GAMW", "XR", "XRX"):
+        pairs["SGV_O_" + n] = getattr(hb, "O_" + n)
+    for n in ("EM", "DENOISE_DAMP", "ALPHA1_DAMP", "LMMSE_DAMP", "LEARN_GAMW", "METRICS", "CHAIN"):
+        pairs["SGV_STEP_" + n] = getattr(hb, "STEP_" + n)
+    for name, value in pairs.items():
+        assert defs[name] == value, (name, defs[name], value)
+
+
 def test_library_is_gfx950_only():
     """The code object embedded in the library targets gfx950 and nothing else."""
     data = open(LIB, "rb").read()
