@@ -233,3 +233,29 @@ def test_plink_exchange_vectorised_equals_reference_loop(tmp_path):
         got = mats[k]
         assert (got != want).nnz == 0
         np.testing.assert_array_equal(got.toarray(), want.toarray())
+
+
+def test_plink2np_converter(tmp_path):
+    """scripts/plink2np.py:22-49: BETA -> .npy as read (NaN kept); .ld pairs ->
+    CSR .npz in the .linear file's SNP order, unit diagonal, both triangles,
+    a pair listed twice summed; the .npz is what --ld-files reads."""
+    from plink2np import main as plink2np_main
+
+    lin = tmp_path / "c.assoc.linear"
+    with open(lin, "w") as f:
+        f.write(" CHR SNP BP A1 TEST NMISS BETA STAT P\n")
+        for snp, beta in [("rs3", 0.5), ("rs1", float("nan")), ("rs7", -1.25), ("rs2", 2.0)]:
+            f.write(" 1 %s 0 A ADD 100 %r 0 0\n" % (snp, beta))
+    write_ld(tmp_path / "c.ld", [("rs3", "rs1", 0.25), ("rs1", "rs2", -0.5), ("rs3", "rs1", 0.125)])
+    plink2np_main(["--ld-file", str(tmp_path / "c.ld"), "--r-file", str(lin)])
+    r = np.load(tmp_path / "c.npy")
+    np.testing.assert_array_equal(r[[0, 2, 3]], [0.5, -1.25, 2.0])
+    assert np.isnan(r[1])
+    R = scipy.sparse.load_npz(tmp_path / "c.npz").toarray()
+    E = np.eye(4)
+    E[0, 1] = E[1, 0] = 0.25 + 0.125
+    E[1, 3] = E[3, 1] = -0.5
+    np.testing.assert_array_equal(R, E)
+    L = load_ld(str(tmp_path / "c.npz"), 0.0)
+    assert L.block_sizes == [4]
+    np.testing.assert_array_equal(L.block(0), E)
