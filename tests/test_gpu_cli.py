@@ -234,3 +234,52 @@ def test_cli_banded_npz_vs_oracle(tmp_path):
     for it in range(its):
         xb = np.fromfile(out / ("band_xhat_it_%d.bin" % it))
         assert _maxrel(xb, np.asarray(t["xhat"][it]).ravel()) < 1e-8, it
+
+
+def test_simulate_writes_cli_inputs(tmp_path):
+    """simulate.py (simulation/sim_gen_phen_mult.py on the device): per cohort its
+    own genotypes, block-diagonal LD as a manifest of block files, r, y, beta and
+    .bim files; every LD block, r and y equal the CPU restatement of the
+    generator; main.py then runs on the files, matching the oracle on them."""
+    import json
+
+    import main
+    import simulate
+    from oracle import synth_oracle as so
+    from oracle import vamp_oracle as vo
+
+    M, N, K, seed = 2500, 600, 2, 11
+    sizes = [1000, 1000, 500]
+    out = str(tmp_path / "sim")
+    p = simulate.simulate(out, N, M, K=K, block_size=1000, seed=seed)
+    beta = np.load(p["beta"]).ravel()
+    assert np.count_nonzero(beta) == M // 2
+    lds, rs = [], []
+    for k in range(K):
+        w = np.random.RandomState(seed + 1000 + k).normal(0.0, np.sqrt(0.2), N)
+        Rb, r, g, _ = so.synth_problem(sizes, N, beta, seed + 1 + 7919 * k, w)
+        man = json.load(open(p["ld"][k]))
+        assert man["block_sizes"] == sizes
+        blocks = [np.load(os.path.join(str(tmp_path), fn)) for fn in man["files"]]
+        for B, Bref in zip(blocks, Rb):
+            assert _maxrel(B, Bref) < 1e-12
+        rk = np.load(p["r"][k]).ravel()
+        assert _maxrel(rk, r) < 1e-12
+        assert _maxrel(np.load(p["phen"][k]).ravel(), g + w) < 1e-12
+        lds.append(vo.BlockLD(blocks))
+        rs.append(rk)
+    cm = M // 2
+    o = tmp_path / "out"
+    o.mkdir()
+    its = 3
+    main.main(["--ld-files", ",".join(p["ld"]), "--r-files", ",".join(p["r"]),
+               "--bim-files", ",".join(p["bim"]), "--true-signal-file", p["beta"],
+               "--out-dir", str(o), "--out-name", "sim", "--N", "%d,%d" % (N, N),
+               "--M", "%d,%d" % (M, M), "--K", str(K), "--iterations", str(its),
+               "--prior-vars", "0,%r" % (0.8 / cm), "--prior-probs", "0.5,0.5", "--seed", "3"])
+    t = vo.infer(lds, [0, 1], rs, [float(N)] * K, its, rho=0.5, gamw=5.0, gam1=1e-6,
+                 prior_vars=[0.0, 0.8 / cm], prior_probs=[0.5, 0.5], seed=3,
+                 reducer=vo.Reducer("blocked", bounds=lds[0].bounds), rs_recurrence=True)
+    for it in range(its):
+        xb = np.fromfile(o / ("sim_xhat_it_%d.bin" % it))
+        assert _maxrel(xb, np.asarray(t["xhat"][it]).ravel()) < 1e-8, it
