@@ -153,6 +153,42 @@ def test_north_star_full_size_pass_properties():
     eng.close()
 
 
+def test_north_star_full_size_rerun_bitwise(tmp_path):
+    """The bench's north-star problem (M = 1e6 in 64 blocks of 15,625, K = 4
+    sharing the LD, N = 10,000, EM) for 3 iterations, twice on one engine: the
+    second infer() restarts (r1 = r, xhat2 = Sigma2_u = 0, the probe streams
+    from their seeds) and, with lam/omegas set back, reproduces the first run
+    bit for bit, CG and EM counts included; the trajectory stays finite."""
+    sizes = [15625] * 64
+    K, N = 4, 10000
+    M = sum(sizes)
+    rs = np.random.RandomState(2025)
+    cm = M // 2
+    beta = np.zeros(M)
+    beta[rs.choice(M, cm, replace=False)] = rs.normal(0, np.sqrt(0.8 / cm), cm)
+    eng = Engine(sizes, K=K)
+    g = eng.synth_ld_g(0, 2026, N, beta).sum(axis=0)
+    for k in range(K):
+        eng.synth_r(k, 2026, N, g + np.random.RandomState(3025 + k).normal(0, np.sqrt(0.2), N))
+    v = VAMP(N=[N] * K, Nt=N * K, M=M, K=K, rho=0.5, gamw=5.0, gam1=1e-6, a=[1 / K] * K,
+             prior_vars=[0.0, 0.8 / cm / K], prior_probs=[0.5, 0.5], out_dir=str(tmp_path),
+             out_name="ns", seed=7, write_files=False)
+    x0 = beta * np.sqrt(N)
+    v.attach_engine(eng, x0=x0)
+    lam0, om0 = v.lam, np.array(v.omegas, dtype=np.float64).copy()
+    its = 3
+    xa = [x.copy() for x in v.infer(None, None, its, x0=x0, lmmse_damp=False, prior_update="em")]
+    ha = [(h["cg_iters"], h.get("em_steps")) for h in v.history]
+    v.lam, v.omegas = lam0, om0.copy()
+    xb = v.infer(None, None, its, x0=x0, lmmse_damp=False, prior_update="em")
+    hb_ = [(h["cg_iters"], h.get("em_steps")) for h in v.history[its:]]   # history accumulates
+    assert ha == hb_
+    for it in range(its):
+        assert np.isfinite(xa[it]).all()
+        np.testing.assert_array_equal(xa[it], xb[it])
+    eng.close()
+
+
 # ---------------------------------------------------------------------------
 # CG (operator seam con_grad)
 # ---------------------------------------------------------------------------
