@@ -229,6 +229,34 @@ def test_cg_solve_vs_oracle():
     eng.close()
 
 
+def test_cg_solve_without_shift_exact_counts():
+    """c2 = 0 columns (A = c1 R_s, no gam2 shift) on full-rank blocks (N > n_b):
+    a few tens of iterations, iteration counts and info exact, x within 1e-7 --
+    the +-2 of test_cg_solve_vs_oracle is only for the rank-deficient ~60-
+    iteration column, whose stop test sits on summation-order rounding."""
+    sizes = [150, 90, 260]
+    blocks = rand_blocks(sizes, 12, nsamp=1200)
+    M = sum(sizes)
+    eng = Engine(sizes, K=1)
+    for b, B in enumerate(blocks):
+        eng.set_ld_block(0, b, B)
+    eng.set_ridge(0.05)
+    L = vo.BlockLD(blocks, s=0.05)
+    rs = np.random.RandomState(4)
+    c1 = np.array([1.0, 6.0, 0.5])
+    c2 = np.zeros(3)
+    Bm = rs.normal(size=(3, M))
+    X0 = np.zeros((3, M))
+    X0[2] = rs.normal(size=M) * 0.05
+    X, it, info = eng.cg_solve(0, c1, c2, Bm, X0, maxiter=500)
+    for j in range(3):
+        A = lambda p, j=j: c1[j] * L.matvec_Rs(p)
+        xr, info_r, it_r, _ = vo.cg_scipy(A, Bm[j], X0[j], 500, vo.Reducer())
+        assert (it[j], info[j]) == (it_r, info_r), (j, it[j], it_r)
+        assert maxrel(X[j], xr) < 1e-7, j
+    eng.close()
+
+
 # ---------------------------------------------------------------------------
 # element-wise kernels
 # ---------------------------------------------------------------------------
