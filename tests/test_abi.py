@@ -105,6 +105,14 @@ def test_product_does_not_import_oracle():
         assert "oracle" not in re.findall(r"^\s*(?:from|import)\s+(\w+)", src, flags=re.M), p
 
 
+def test_product_and_bench_do_not_import_torch():
+    """PyTorch is neither the product nor its launcher: the package and bench.py
+    import no torch module (the multi-rank bootstrap is comm.SocketComm)."""
+    for p in glob.glob(os.path.join(PKG, "*.py")) + [os.path.join(ROOT, "bench.py")]:
+        mods = re.findall(r"^\s*(?:from|import)\s+([\w.]+)", open(p).read(), flags=re.M)
+        assert not [m for m in mods if m.split(".")[0] == "torch"], p
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2025, 987654321])
 def test_probe_stream_matches_numpy_binomial(seed):
     """sgv_probe_draw (host only) reproduces src/sgvamp.py:326's
