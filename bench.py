@@ -76,6 +76,9 @@ def parse():
     p.add_argument("--prior", choices=["matched", "cli"], default="matched")
     p.add_argument("--ridge", type=float, default=0.0, help="--s of the CLI (C5: 0.1)")
     p.add_argument("--lmmse-damp", type=int, default=0, help="--lmmse-damp of the CLI (C5: 1)")
+    p.add_argument("--read-bw", type=int, default=1,
+                   help="1: after the timed steps, measure the GPU's streaming-read rate "
+                        "(roofline.box_stream_GBs)")
     p.add_argument("--ld-format", choices=["packed", "dense"], default="packed",
                    help="LD block storage: packed symmetric panels (default) or full squares")
     return p.parse_args()
@@ -260,6 +263,9 @@ def main():
     comm.barrier()
     dt = max(comm.allgather(t1 - t0))
     tm = eng.timers()
+    # this box's own streaming-read rate (after the timed region; context only:
+    # the roofline peak stays the guide's 8 TB/s); the slowest rank's
+    box_bw = min(comm.allgather(eng.read_bw(8 << 30, 5))) if args.read_bw else None
     for rec in recs:
         log("[bench] it=%d cg=%s em=%s passes=%d %.1f ms l2=%s waits(ms): probes %.2f outputs %.2f "
             "writes %.2f" % (
@@ -334,6 +340,8 @@ def main():
             "avg_launch_ms": avg_s * 1e3,
             "launches": int(launches),
             "traffic_source": traffic_src,
+            "box_stream_GBs": box_bw,
+            "frac_of_box_stream": (achieved / box_bw) if (achieved and box_bw) else None,
         },
         "ld_passes_per_step": passes / steps,
         "effective_ld_gbps_end_to_end": passes * ld_bytes_total / dt / 1e9,

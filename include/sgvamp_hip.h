@@ -316,6 +316,12 @@ int sgv_timers(sgv_ctx* ctx, double* t6, int reset);
 /* Synchronise the ctx stream. */
 int sgv_sync(sgv_ctx* ctx);
 
+/* The device's streaming-read rate (context for the LD passes' roofline): a
+ * temporary buffer of `bytes` (rounded down to 256 KiB) read once per repeat,
+ * every workgroup its own contiguous 256 KiB with 16-B nontemporal loads; the
+ * best of `reps` repeats in GB/s (1e9 B/s) -> *gbps. */
+int sgv_read_bw(sgv_ctx* ctx, int64_t bytes, int reps, double* gbps);
+
 #ifdef __cplusplus
 }
 #endif

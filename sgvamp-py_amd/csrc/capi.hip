@@ -2568,6 +2568,41 @@ extern "C" int sgv_sync(sgv_ctx* c) {
   return SGV_OK;
 }
 
+extern "C" int sgv_read_bw(sgv_ctx* c, int64_t bytes, int reps, double* gbps) {
+  ENTER(c);
+  const int64_t unit = (int64_t)256 * 1024;
+  bytes = bytes / unit * unit;
+  if (!gbps || bytes < unit || reps < 1) return fail(c, SGV_ERR_ARG, "sgv_read_bw: bad arguments");
+  CHK(stream_wait(c));
+  double* buf = nullptr;
+  double* out = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = SGV_OK;
+  if (hipMalloc(&buf, (size_t)bytes) != hipSuccess || hipMalloc(&out, 256 * sizeof(double)) != hipSuccess ||
+      hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+    rc = fail(c, SGV_ERR_HIP, "sgv_read_bw: allocation of %.2f GB failed", bytes / 1e9);
+  if (rc == SGV_OK && hipMemsetAsync(buf, 0, (size_t)bytes, c->st) != hipSuccess)
+    rc = fail(c, SGV_ERR_HIP, "sgv_read_bw: memset failed");
+  float best = 0.f;
+  for (int r = -1; rc == SGV_OK && r < reps; ++r) {   // r = -1: warm-up
+    float ms = 0.f;
+    if (hipEventRecord(e0, c->st) != hipSuccess ||
+        launch_read_probe(buf, (size_t)bytes, out, c->st) != hipSuccess ||
+        hipEventRecord(e1, c->st) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+        hipEventElapsedTime(&ms, e0, e1) != hipSuccess)
+      rc = fail(c, SGV_ERR_HIP, "sgv_read_bw: probe launch failed");
+    else if (r >= 0 && (best == 0.f || ms < best))
+      best = ms;
+  }
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  if (buf) (void)hipFree(buf);
+  if (out) (void)hipFree(out);
+  CHK(rc);
+  *gbps = (double)bytes / ((double)best * 1e-3) / 1e9;
+  return SGV_OK;
+}
+
 // ---------------------------------------------------------------------------
 // one outer iteration in the shim (src/sgvamp.py:222-387 minus the files and
 // logs): the host returns to the caller once, not between the phases

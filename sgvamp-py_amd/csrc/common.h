@@ -285,6 +285,9 @@ __device__ __forceinline__ void fin_epilogue(const SymPanel& pn, const PassArgs&
     partials[(int64_t)pn.part * NC + t] = ((s_w[0][t] + s_w[1][t]) + s_w[2][t]) + s_w[3][t];
 }
 
+// streaming-read probe over `bytes` of buf (diag.hip); out: >= 256 doubles
+hipError_t launch_read_probe(const double* buf, size_t bytes, double* out, hipStream_t st);
+
 // ---- launchers (defined in the .hip files) ------------------------------
 // LD pass: one workgroup per row group; partials[rg.part * nc + c].
 hipError_t launch_ld_pass(int nc, const BlkDesc* d_blks, const RowGroup* d_rg, int nrg,

@@ -293,5 +293,11 @@ class Engine:
     def sync(self):
         self.ctx.sgv_sync()
 
+    def read_bw(self, nbytes=8 << 30, reps=5):
+        """The device's streaming-read rate in GB/s (sgv_read_bw), best of reps."""
+        out = np.zeros(1)
+        self.ctx.sgv_read_bw(int(nbytes), int(reps), hb.dptr(out))
+        return float(out[0])
+
     def close(self):
         self.ctx.close()

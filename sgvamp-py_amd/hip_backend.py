@@ -84,6 +84,7 @@ _SIGS = {
     "sgv_probe_draw": [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int32),
                        ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _c_i8_p],
     "sgv_sync": [_vp],
+    "sgv_read_bw": [_vp, ctypes.c_int64, ctypes.c_int, _c_dbl_p],
 }
 _RESTYPES = {"sgv_destroy": None, "sgv_last_error": ctypes.c_char_p}
 EXPORTS = tuple(_SIGS)
