@@ -1,4 +1,7 @@
 #!/bin/bash
+# A/B of the tree's library against ab_lib/base.so on the LD-pass microbenchmark at the
+# north-star block structure, NC = 9/12/16 (the 16x16x4 / 4x4x4 C5 kernels), after the
+# LD-pass parity tests; two alternating repeats.
 cd /root/repo
 export TMPDIR=/tmp
 MB="tools/ldpass_bench.py --blocks 64 --block-size 15625 --formats packed --ncols 9,12,16 --reps 5"

@@ -1,4 +1,6 @@
 #!/bin/bash
+# rocm-smi power, clocks and temperature every 2 s during a 400-step north-star bench
+# (gpurun_out/pw_smi.log, pw_bench.log).
 cd /root/repo
 mkdir -p gpurun_out
 timeout -k 10 200 python bench.py --steps 400 --warmup 3 --cpu-baseline off --no-files > gpurun_out/pw_bench.log 2>&1 &
