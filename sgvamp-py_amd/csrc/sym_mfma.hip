@@ -202,6 +202,11 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
         // operations execute in order); the column MFMAs cover their latency
 #pragma unroll
         for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + (4 * r + n4) * MF_LDP + 2 * pc);
+        // the MFMA burst at raised wave priority: the SIMD's other wave, whose
+        // loads are in flight, takes the issue slots back when this one drains
+        // (NC = 4/8 0.7-1.5 % faster per pass on two boxes; NC = 16 1 % slower,
+        // not used there -- profiles/r02s10_prio_ab.txt)
+        __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -219,6 +224,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(rf[r].y, brow[t][1][q], drow[r][q]);
+        __builtin_amdgcn_s_setprio(0);
       }
       // row sums: the 4 blocks (lanes differing in bits 2,3), then the waves in order
       double* rb = red[gg & 1][wid];
