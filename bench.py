@@ -34,6 +34,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import sys
 import tempfile
 import time
@@ -113,7 +114,10 @@ def read_traffic(kernel_prefix, bytes_launch, K, M):
     summary for this kernel, K and M whose algorithmic bytes per launch agree
     with this run's within 1 %.  None when no summary was collected on this
     workload."""
-    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))   # by round label
+    # by round label, numbers compared as numbers (r02s10 after r02s7)
+    cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")),
+                   key=lambda p: [int(x) if x.isdigit() else x
+                                  for x in re.split(r"(\d+)", os.path.basename(p))])
     for path in reversed(cands):
         try:
             d = json.load(open(path))
