@@ -124,6 +124,15 @@ static bool em_fuse_default() {
   }();
   return v;
 }
+// SGV_CG_EXACT=0: the pipelined CG's pass of iteration it also carries the
+// columns that stop at it's own test (one iteration of look-ahead; A/B)
+static bool cg_exact_default() {
+  static const bool v = [] {
+    const char* e = ab_env("SGV_CG_EXACT");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
 static int sym_class_nc(int cls) { return std::min(16, 2 << (cls + 1)); }   // widest NC using cls
 
 // The one-workgroup reduction + control kernels (k_cg_reduce_ctl,
@@ -958,6 +967,14 @@ static int event_spin(sgv_ctx* c, hipEvent_t ev) {
 // alone (deterministic; a column stopping at it + 1's test rides along in that
 // pass unused).  When the test of `it` stops every column, that iteration's
 // kernels were no-ops: their pass timers and byte counts are dropped.
+// Exact column sets (default, from it = 1): the p update of `it` (a no-op for
+// the columns the device state has stopped) is enqueued first, then the host
+// waits for the test of `it` -- it completes while that p update runs -- and
+// enqueues the passes with the columns still active after it.  A CG #1 column
+// that stops one iteration before its CG #2 partner then leaves the pass
+// (north star: NC 8 -> 4, one pass in three once the iteration counts split);
+// a column's values do not depend on the others in its pass, so only the
+// work changes.
 static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const double* atol,
                        int maxiter, const int* active_in, int* iters, int* info, int* passes) {
   const int ncol = cc.ncol;
@@ -984,6 +1001,7 @@ static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const d
   // launch (k_cg_reduce_ctl), enqueued at the end of it, when that one
   // workgroup's reduction is short (fused_ctl_pays); SGV_EM_FUSE=0 A/B
   const bool fuse = !c->comm && !c->host_ag && fused_ctl_pays(MAXC, c->nblk) && em_fuse_default();
+  const bool exact = cg_exact_default();
   for (int it = 0; it < maxiter; ++it) {
     const size_t np0 = c->pending.size();
     const double cnt0[5] = {c->ld_launches, c->ld_bytes, c->dense_bytes, c->rhs_bytes,
@@ -1004,6 +1022,15 @@ static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const d
         pa.Rr[j] = cc.Rr[j];
       }
       HIPCHK(launch_cg_p(c->d_ch, c->nch, pa, c->st));
+    }
+    const bool pre = exact && it > 0;   // the test of `it` read before its passes
+    if (pre) {
+      CHK(event_spin(c, c->ev_cg[it % CG_RING]));
+      last = slot;
+      if (!last->any) break;            // only the (no-op) p update was enqueued
+      mask = 0;
+      for (int j = 0; j < ncol; ++j)
+        if (last->active[j]) mask |= 1u << j;
     }
     // q = A p (iterative.py:411): one pass per LD matrix over its columns
     for (int ld = 0; ld < c->nld; ++ld) {
@@ -1050,6 +1077,11 @@ static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const d
       HIPCHK(hipEventRecord(c->ev_cg[(it + 1) % CG_RING], c->st));
     } else {
       CHK(reduce_dev(c, MAXC, c->d_ch_begin, identity_map(), c->d_rhonew));
+    }
+    if (pre) {
+      ++executed;
+      if (passes) *passes += npass;
+      continue;
     }
     // the stop test of `it` (its first kernel) decides whether it did any work
     CHK(event_spin(c, c->ev_cg[it % CG_RING]));
