@@ -126,12 +126,9 @@ static bool em_fuse_default() {
 }
 // SGV_CG_EXACT=0: the pipelined CG's pass of iteration it also carries the
 // columns that stop at it's own test (one iteration of look-ahead; A/B)
-static bool cg_exact_default() {
-  static const bool v = [] {
-    const char* e = ab_env("SGV_CG_EXACT");
-    return !(e && e[0] == '0');
-  }();
-  return v;
+static int cg_exact_default() {
+  const char* e = ab_env("SGV_CG_EXACT");
+  return (e && e[0] == '0') ? 0 : 1;
 }
 static int sym_class_nc(int cls) { return std::min(16, 2 << (cls + 1)); }   // widest NC using cls
 
@@ -254,6 +251,7 @@ struct sgv_ctx {
   // pipelined CG (cg_loop_dev): device control state, its host mirror ring
   // (fine-grained pinned, one slot per in-flight iteration), init staging
   int cg_pipe = 1;
+  int cg_exact = 1;   // pipelined CG: passes carry only the columns active after their test
   CgState* d_cgs = nullptr;
   CgState* h_cgm = nullptr;       // [CG_RING]
   CgState* h_cgi = nullptr;
@@ -972,9 +970,10 @@ static int event_spin(sgv_ctx* c, hipEvent_t ev) {
 // waits for the test of `it` -- it completes while that p update runs -- and
 // enqueues the passes with the columns still active after it.  A CG #1 column
 // that stops one iteration before its CG #2 partner then leaves the pass
-// (north star: NC 8 -> 4, one pass in three once the iteration counts split);
-// a column's values do not depend on the others in its pass, so only the
-// work changes.
+// (north star: NC 8 -> 4, one pass in three once the iteration counts split;
+// the same iterates bit for bit there).  Where the smaller set crosses a kernel
+// boundary (NC <= 2 runs the VALU pass, 3..16 the MFMA pass) the surviving
+// columns' sums are formed in another order: equal to rounding.
 static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const double* atol,
                        int maxiter, const int* active_in, int* iters, int* info, int* passes) {
   const int ncol = cc.ncol;
@@ -1001,7 +1000,7 @@ static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const d
   // launch (k_cg_reduce_ctl), enqueued at the end of it, when that one
   // workgroup's reduction is short (fused_ctl_pays); SGV_EM_FUSE=0 A/B
   const bool fuse = !c->comm && !c->host_ag && fused_ctl_pays(MAXC, c->nblk) && em_fuse_default();
-  const bool exact = cg_exact_default();
+  const bool exact = c->cg_exact != 0;
   for (int it = 0; it < maxiter; ++it) {
     const size_t np0 = c->pending.size();
     const double cnt0[5] = {c->ld_launches, c->ld_bytes, c->dense_bytes, c->rhs_bytes,
@@ -1289,6 +1288,7 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   for (int i = 0; i < CG_RING; ++i)
     CREATE_HIP(hipEventCreateWithFlags(&c->ev_em[i], hipEventDisableTiming));
   c->cg_pipe = cg_pipe_default();
+  c->cg_exact = cg_exact_default();
   c->xnz.assign(2 * K, 0);
   c->rx0_valid.assign(2 * K, 0);
 #undef CREATE_HIP

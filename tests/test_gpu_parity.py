@@ -402,6 +402,32 @@ def test_cg_pipeline_matches_host_loop(name, tmp_path, monkeypatch):
             assert maxrel(b_, a_) < 1e-10
 
 
+@pytest.mark.parametrize("name", ["k1_defaults", "k2_shared", "k4_shared_s_damp", "k4_long50"])
+def test_cg_exact_columns_vs_lookahead(name, tmp_path, monkeypatch):
+    """Pipelined CG with exact column sets (default: each pass carries only the
+    columns still active after its own stop test) vs the one-iteration look-ahead
+    form (SGV_CG_EXACT=0: a column that stops at that test rides along): the
+    same CG and EM counts and iterates equal to rounding (bitwise where no pass
+    changes kernel family); the default path's match with the reference fixtures
+    is test_vamp_matches_reference_golden's."""
+    c = Case(name)
+    monkeypatch.setenv("SGV_AB", "1")
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("SGV_CG_EXACT", mode)
+        d = tmp_path / mode
+        d.mkdir()
+        v, xh = run_vamp_case(c, d)
+        out[mode] = (xh, [h["cg_iters"] for h in v.history], [h["cg_info"] for h in v.history],
+                     [h.get("em_steps") for h in v.history])
+        v.engine.close()
+    assert out["0"][1] == out["1"][1] and out["0"][2] == out["1"][2]
+    assert out["0"][3] == out["1"][3]
+    worst = max(maxrel(b_, a_) for a_, b_ in zip(out["0"][0], out["1"][0]))
+    print("%s: exact vs look-ahead max rel %.3g" % (name, worst))
+    assert worst < 1e-10
+
+
 @pytest.mark.parametrize("name", ["k1_defaults", "k1_L3", "k2_shared", "k4_shared_s_damp",
                                   "k2_mle_L3", "k1_blocks_csr_s_damp"])
 def test_step_driver_matches_phases(name, tmp_path, monkeypatch):
