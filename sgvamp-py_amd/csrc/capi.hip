@@ -1000,7 +1000,17 @@ static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const d
   // launch (k_cg_reduce_ctl), enqueued at the end of it, when that one
   // workgroup's reduction is short (fused_ctl_pays); SGV_EM_FUSE=0 A/B
   const bool fuse = !c->comm && !c->host_ag && fused_ctl_pays(MAXC, c->nblk) && em_fuse_default();
-  const bool exact = c->cg_exact != 0;
+  // exact sets pay only where fewer columns make a pass cheaper: the MFMA pass
+  // (>= 3 columns of one LD matrix, cost by groups of 4); the VALU pass costs
+  // the same at 1 and 2 columns (C2: 3.19 vs 3.21 ms), so K = 1 and distinct-LD
+  // pairs keep the look-ahead and its host read stays off the critical path
+  int widest = 0;
+  for (int j = 0; j < ncol; ++j) {
+    int n = 0;
+    for (int i = 0; i < ncol; ++i) n += cc.col_ld[i] == cc.col_ld[j];
+    widest = std::max(widest, n);
+  }
+  const bool exact = c->cg_exact != 0 && widest >= 3;
   for (int it = 0; it < maxiter; ++it) {
     const size_t np0 = c->pending.size();
     const double cnt0[5] = {c->ld_launches, c->ld_bytes, c->dense_bytes, c->rhs_bytes,
