@@ -135,7 +135,10 @@ int sgv_set_mfma_min(sgv_ctx* ctx, int nc_min);
  * update and convergence test run on the device, and iteration i+1 is enqueued
  * while iteration i runs (no host round trip between iterations); off, the
  * host tests every iteration.  Same iterates and counts; env SGV_CG_PIPE=0
- * sets the default off. */
+ * sets the default off.  On, a pass carries only the columns still active
+ * after its own stop test wherever that can narrow it (>= 3 columns on one LD
+ * matrix; the host reads the test while the p update runs); SGV_CG_EXACT=0
+ * (with SGV_AB=1) keeps the one-iteration look-ahead set instead. */
 int sgv_set_cg_pipeline(sgv_ctx* ctx, int on);
 /* Storage of LD blocks set or generated from now on: mode 1 (default) stores a
  * block that is exactly symmetric as packed upper-triangle panels (about half
