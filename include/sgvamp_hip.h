@@ -135,10 +135,11 @@ int sgv_set_mfma_min(sgv_ctx* ctx, int nc_min);
  * update and convergence test run on the device, and iteration i+1 is enqueued
  * while iteration i runs (no host round trip between iterations); off, the
  * host tests every iteration.  Same iterates and counts; env SGV_CG_PIPE=0
- * sets the default off.  On, a pass carries only the columns still active
- * after its own stop test wherever that can narrow it (>= 3 columns on one LD
- * matrix; the host reads the test while the p update runs); SGV_CG_EXACT=0
- * (with SGV_AB=1) keeps the one-iteration look-ahead set instead. */
+ * sets the default off.  On, at one rank, a pass of >= 3 columns over >= 24 GB
+ * of stored LD carries only the columns still active after its own stop test
+ * (the host reads the test while the p update runs); smaller passes and
+ * multi-rank runs keep the one-iteration look-ahead set.  SGV_CG_EXACT=0/1
+ * (with SGV_AB=1) forces either. */
 int sgv_set_cg_pipeline(sgv_ctx* ctx, int on);
 /* Storage of LD blocks set or generated from now on: mode 1 (default) stores a
  * block that is exactly symmetric as packed upper-triangle panels (about half

@@ -126,10 +126,15 @@ static bool em_fuse_default() {
 }
 // SGV_CG_EXACT=0: the pipelined CG's pass of iteration it also carries the
 // columns that stop at it's own test (one iteration of look-ahead; A/B)
-static int cg_exact_default() {
+static int cg_exact_default() {   // -1: by size (cg_loop_dev); 0 / 1 forced (A/B)
   const char* e = ab_env("SGV_CG_EXACT");
-  return (e && e[0] == '0') ? 0 : 1;
+  return !e ? -1 : (e[0] == '0' ? 0 : 1);
 }
+// exact CG column sets by size: a pass narrowed from 8 to 4 columns saves ~4 %
+// of its time (north star in the solver: 10.6-10.9 vs 11.0-11.5 ms) against
+// ~30 us of host read per CG iteration, so only passes of >= ~4 ms (24 GB
+// stored) narrow; one rank only -- the choice must be the same on every rank
+constexpr double CG_EXACT_MIN_BYTES = 24e9;
 static int sym_class_nc(int cls) { return std::min(16, 2 << (cls + 1)); }   // widest NC using cls
 
 // The one-workgroup reduction + control kernels (k_cg_reduce_ctl,
@@ -251,7 +256,8 @@ struct sgv_ctx {
   // pipelined CG (cg_loop_dev): device control state, its host mirror ring
   // (fine-grained pinned, one slot per in-flight iteration), init staging
   int cg_pipe = 1;
-  int cg_exact = 1;   // pipelined CG: passes carry only the columns active after their test
+  int cg_exact = -1;  // pipelined CG: passes carry only the columns active after their test
+                      // (-1: by size, cg_loop_dev)
   CgState* d_cgs = nullptr;
   CgState* h_cgm = nullptr;       // [CG_RING]
   CgState* h_cgi = nullptr;
@@ -1005,12 +1011,19 @@ static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const d
   // the same at 1 and 2 columns (C2: 3.19 vs 3.21 ms), so K = 1 and distinct-LD
   // pairs keep the look-ahead and its host read stays off the critical path
   int widest = 0;
+  double wide_bytes = 0.0;   // largest pass of >= 3 columns (this rank's blocks)
   for (int j = 0; j < ncol; ++j) {
     int n = 0;
     for (int i = 0; i < ncol; ++i) n += cc.col_ld[i] == cc.col_ld[j];
     widest = std::max(widest, n);
+    if (n >= 3 && c->cg_exact < 0 && !c->comm && !c->host_ag) {
+      CHK(ensure_plan(c, cc.col_ld[j]));
+      wide_bytes = std::max(wide_bytes, c->plan[cc.col_ld[j]].stored_bytes);
+    }
   }
-  const bool exact = c->cg_exact != 0 && widest >= 3;
+  const bool exact = widest >= 3 && (c->cg_exact > 0 || (c->cg_exact < 0 && !c->comm &&
+                                                         !c->host_ag &&
+                                                         wide_bytes >= CG_EXACT_MIN_BYTES));
   for (int it = 0; it < maxiter; ++it) {
     const size_t np0 = c->pending.size();
     const double cnt0[5] = {c->ld_launches, c->ld_bytes, c->dense_bytes, c->rhs_bytes,
