@@ -22,11 +22,14 @@ causal markers, h2 = 0.8).  A "step" is one VAMP outer iteration
 (src/sgvamp.py:222-387): EM prior update, denoiser, both CG solves, gamw
 learning, output files.  Inputs are resident in HBM before timing starts.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
-the LD blocks are sharded over the N ranks (strong scaling, one problem);
-CG dot products are ordered per-block sums exchanged with RCCL all-gathers.
-The launcher only sets RANK/WORLD_SIZE/MASTER_*: the host communicator is the
-build's own TCP rendezvous (sgvamp-py_amd/comm.py), torch is never imported.
+Multi-GPU: ``python bench.py --gpus N`` starts N ranks itself, one process per
+GPU (sgvamp-py_amd/launch.py: child processes, started before anything touches
+the GPU); an external one-process-per-GPU launcher (RANK/WORLD_SIZE/LOCAL_RANK,
+mpirun, srun) is accepted too, and then --gpus must equal its world size.  The
+LD blocks are sharded over the N ranks (strong scaling, one problem); CG dot
+products are ordered per-block sums exchanged with RCCL all-gathers.  The host
+communicator is the build's own TCP rendezvous (sgvamp-py_amd/comm.py), torch
+is never imported.
 
 Prints ONE JSON line on rank 0 (other output goes to stderr).
 """
@@ -54,7 +57,9 @@ def log(*a):
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPU ranks (default: the launcher's world size, else 1); N > 1 without "
+                        "a launcher starts N local ranks")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--blocks", type=int, default=64)
@@ -80,6 +85,9 @@ def parse():
     p.add_argument("--read-bw", type=int, default=1,
                    help="1: after the timed steps, measure the GPU's streaming-read rate "
                         "(roofline.box_stream_GBs)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="start the ranks and report each one's rank/device as one JSON line, "
+                        "without touching the GPU (checks the launch)")
     p.add_argument("--ld-format", choices=["packed", "dense"], default="packed",
                    help="LD block storage: packed symmetric panels (default) or full squares")
     return p.parse_args()
@@ -203,15 +211,29 @@ def cpu_baseline(eng, args, ref_flags, recs, x0):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    from launch import relaunch
+
+    rc = relaunch(args.gpus)               # before anything touches the GPU
+    if rc is not None:
+        sys.exit(rc)
     import hip_backend as hb  # noqa: F401  (fails loudly if the library is missing)
     from comm import world_from_env
     from engine import Engine
     from sgvamp import VAMP
 
     comm = world_from_env()
-    rank = comm.Get_rank()
-    device = 0 if args.share_device else int(os.environ.get("LOCAL_RANK", "0"))
+    rank, world = comm.Get_rank(), comm.Get_size()
+    device = 0 if args.share_device else comm.local_rank
+    if args.dry_run:
+        keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+                "SGV_LAUNCHED_BY", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID")
+        ranks = comm.allgather(dict(rank=rank, world=world, local_rank=comm.local_rank,
+                                    device=device, pid=os.getpid(),
+                                    env={k: os.environ[k] for k in keys if k in os.environ}))
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks": ranks}), flush=True)
+        comm.close()
+        return
     sizes = [args.block_size] * args.blocks
     K = args.K
     t_setup = time.perf_counter()

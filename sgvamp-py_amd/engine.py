@@ -47,8 +47,8 @@ class Engine:
         self.Mloc = int(offs[self.b1] - offs[self.b0])
         self.local_sizes = self.block_sizes[self.b0:self.b1]
         self.sl = slice(self.marker0, self.marker0 + self.Mloc)
-        if device is None:   # one process per GPU: the node-local rank (LOCAL_RANK)
-            device = int(os.environ.get("LOCAL_RANK", "0")) if self.nranks > 1 else 0
+        if device is None:   # one process per GPU: the node-local rank (comm.launch_from_env)
+            device = int(getattr(self.comm, "local_rank", 0)) if self.nranks > 1 else 0
         self.ctx = hb.Context(device, self.K, self.ld_of, self.local_sizes, self.b0,
                               len(self.block_sizes), self.M)
         self.exchange = exchange or os.environ.get("SGV_EXCHANGE", "rccl")

@@ -5,10 +5,12 @@ Same flags, defaults, validation messages, log lines and output files
 {name}_cohort_{k}.csv, {name}_metrics.csv).  Differences:
 
 * one process per GPU instead of one MPI rank per cohort: a single process
-  handles all K cohorts (python main.py ...); for several GPUs start G
-  processes with RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR and MASTER_PORT set
-  (any one-process-per-GPU launcher does) and the LD blocks are sharded over
-  the G ranks (host rendezvous: comm.SocketComm);
+  handles all K cohorts (python main.py ...); ``--gpus G`` starts G local
+  ranks (launch.py) and the LD blocks are sharded over them.  The reference's
+  own launch (mpirun -np K python main.py ..., src/main.py:16-18) also works:
+  its K processes become K GPU ranks of ONE job (comm.launch_from_env maps
+  Open MPI / Hydra / srun ranks; rank 0 alone writes the shared files), not K
+  copies of it;
 * --seed (extension): seeds the Hutchinson probes per cohort, RandomState(seed+k)
   (the reference draws from the unseeded global RNG, src/sgvamp.py:326);
 * --bim-files may be omitted when every cohort has the same marker order;
@@ -60,17 +62,25 @@ def build_parser():
     parser.add_argument("-bim_files", "--bim-files", help="Path to files containing list of snps", default=None)
     # extensions
     parser.add_argument("--seed", help="Seed of the Hutchinson probes (RandomState(seed + k))", default=None)
-    parser.add_argument("--device", help="HIP device (default: LOCAL_RANK)", default=None)
+    parser.add_argument("--device", help="HIP device (default: the node-local rank)", default=None)
+    parser.add_argument("--gpus", help="GPU ranks to start on this node (default: the launcher's "
+                        "world size, else 1)", default=None)
     return parser
 
 
 def main(argv=None):
+    args = build_parser().parse_args(argv)
+    if argv is None:            # command line: --gpus N starts the ranks (before any GPU call)
+        from launch import relaunch
+
+        rc = relaunch(None if args.gpus is None else int(args.gpus))
+        if rc is not None:
+            sys.exit(rc)
     comm = world_from_env()
     rank = comm.Get_rank()
     logging.basicConfig(format="%(message)s", level=logging.DEBUG)   # main.py:21
     if rank == 0:
         logging.info(" ### VAMP for summary statistics ###\n")
-    args = build_parser().parse_args(argv)
 
     # main.py:54-97
     ld_fpaths, r_fpaths = args.ld_files, args.r_files

@@ -63,12 +63,22 @@ class _GlooBlocks:
 
 def _rank(rank, world, port, case_name, q, kind):
     try:
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                          WORLD_SIZE=str(world), SGV_COMM_PORT=str(port))
+        if kind == "mpirun":   # only what Open MPI's mpirun -np 2 sets (src/main.py:16-18)
+            for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+                os.environ.pop(k, None)
+            os.environ.update(OMPI_COMM_WORLD_RANK=str(rank), OMPI_COMM_WORLD_SIZE=str(world),
+                              OMPI_COMM_WORLD_LOCAL_RANK=str(rank),
+                              OMPI_COMM_WORLD_LOCAL_SIZE=str(world),
+                              OMPI_MCA_ess_base_jobid="job%d" % port, SGV_COMM_PORT=str(port))
+        else:
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                              WORLD_SIZE=str(world), SGV_COMM_PORT=str(port))
         from comm import world_from_env
         from partition import marker_offsets, partition_blocks
 
-        comm = world_from_env() if kind == "socket" else _TestGlooComm()
+        comm = world_from_env() if kind in ("socket", "mpirun") else _TestGlooComm()
+        if kind == "mpirun":
+            assert (comm.Get_rank(), comm.Get_size(), comm.local_rank) == (rank, world, rank)
         uid = comm.bcast(b"\x01" * 128 if rank == 0 else None, root=0)
         assert uid == b"\x01" * 128
         c = Case(case_name)
@@ -102,10 +112,13 @@ def _single(case_name):
                         reducer=red, **c.kwargs())
 
 
-@pytest.mark.parametrize("kind", ["socket", "gloo"])
+@pytest.mark.parametrize("kind", ["socket", "gloo", "mpirun"])
 @pytest.mark.parametrize("case_name", ["k2_shared", "k1_blocks_csr_s_damp", "k4_shared_s_damp",
                                        "k1_mle", "k2_mle_L3"])
 def test_two_rank_sharded_run_is_bit_identical(case_name, kind):
+    """kind "mpirun": the ranks see only Open MPI's variables -- the reference's
+    own launch becomes one job of two GPU ranks with the same partition and the
+    one-rank result bit for bit (not two one-rank jobs writing the same files)."""
     world = 2
     ctx = mp.get_context("fork")
     q = ctx.Queue()
