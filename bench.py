@@ -348,6 +348,8 @@ def main():
             "K": K, "M": eng.M, "ld_blocks": args.blocks, "block_size": args.block_size,
             "s": args.ridge, "lmmse_damp": bool(args.lmmse_damp),
             "N": args.nsamp, "parallelism": "LD blocks sharded over %d GPU rank(s)" % world,
+            "share_device": bool(args.share_device),
+            "cg_column_sets": "exact" if eng.cg_exact else "look-ahead",
         },
         "roofline": {
             "bound": "hbm",

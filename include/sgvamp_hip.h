@@ -135,12 +135,19 @@ int sgv_set_mfma_min(sgv_ctx* ctx, int nc_min);
  * update and convergence test run on the device, and iteration i+1 is enqueued
  * while iteration i runs (no host round trip between iterations); off, the
  * host tests every iteration.  Same iterates and counts; env SGV_CG_PIPE=0
- * sets the default off.  On, at one rank, a pass of >= 3 columns over >= 24 GB
- * of stored LD carries only the columns still active after its own stop test
- * (the host reads the test while the p update runs); smaller passes and
- * multi-rank runs keep the one-iteration look-ahead set.  SGV_CG_EXACT=0/1
- * (with SGV_AB=1) forces either. */
+ * sets the default off.  Column sets of the pipelined CG: see sgv_set_cg_exact. */
 int sgv_set_cg_pipeline(sgv_ctx* ctx, int on);
+/* Column sets of the pipelined CG's passes.  mode 1 ("exact"): a pass over an
+ * LD matrix shared by >= 3 columns carries only the columns still active after
+ * its own stop test (the host reads the test while the p update runs); mode 0:
+ * one iteration of look-ahead (a column stopping at that test rides along
+ * unused).  The two modes can round differently where the narrower set runs
+ * another pass kernel, so every rank of a run must use the same mode -- it is
+ * the run's choice, not a rank's: Python's Engine sets it from the GLOBAL LD
+ * size (>= 24 GB packed-triangle bytes), identical for 1 and N ranks.  mode -1
+ * (default): by this rank's stored bytes at one rank, look-ahead with a
+ * communicator.  SGV_CG_EXACT=0/1 (with SGV_AB=1) overrides every mode. */
+int sgv_set_cg_exact(sgv_ctx* ctx, int mode);
 /* Storage of LD blocks set or generated from now on: mode 1 (default) stores a
  * block that is exactly symmetric as packed upper-triangle panels (about half
  * the bytes per pass: the LD matrix of src/main.py:199-265 is symmetric by

@@ -256,6 +256,60 @@ class BlockLD:
         return (1 - self.s) * self.matvec_R(v) + self.s * v
 
 
+class PanelLD:
+    """Block-diagonal LD held as the upper triangle of each block in panels of
+    ``H`` rows -- panel g of a block stores rows r0 = H*g .. r0+h-1 over columns
+    r0 .. n-1, its h x h diagonal block in full (the device's packed layout,
+    DESIGN.md section 3) -- so a full-size configuration (M = 1e6: 63.5 GB
+    instead of 125 GB dense) fits the test host.  Same operator as BlockLD on
+    the same blocks (R_s = (1-s) R + s I, src/main.py:265); only the summation
+    order of the products differs.  ``matmat_R`` takes several columns at once
+    (one BLAS call per panel and part, not per column)."""
+
+    def __init__(self, s=0.0, H=256):
+        self.s, self.H = s, H
+        self.blocks = []          # (offset, n, [panel arrays])
+        self.sizes = []
+
+    @property
+    def bounds(self):
+        return np.cumsum([0] + self.sizes)
+
+    def add_block(self, B):
+        """Append the next diagonal block (a dense symmetric n x n array; only
+        its upper triangle is kept)."""
+        n = B.shape[0]
+        off = int(sum(self.sizes))
+        panels = [np.ascontiguousarray(B[r0:min(r0 + self.H, n), r0:], dtype=np.float64)
+                  for r0 in range(0, n, self.H)]
+        self.blocks.append((off, n, panels))
+        self.sizes.append(n)
+
+    def matmat_R(self, V):
+        V = np.asarray(V, dtype=np.float64)
+        Y = np.zeros_like(V)
+        for off, n, panels in self.blocks:
+            Vb, Yb = V[off:off + n], Y[off:off + n]
+            for g, P in enumerate(panels):
+                r0 = g * self.H
+                h = P.shape[0]
+                Yb[r0:r0 + h] += P @ Vb[r0:]                     # rows of the panel
+                if P.shape[1] > h:
+                    Yb[r0 + h:] += P[:, h:].T @ Vb[r0:r0 + h]    # their transposes
+        return Y
+
+    def matvec_R(self, v):
+        return self.matmat_R(np.asarray(v)[:, None])[:, 0]
+
+    def matmat_Rs(self, V):
+        if self.s == 0.0:
+            return self.matmat_R(V)
+        return (1 - self.s) * self.matmat_R(V) + self.s * V
+
+    def matvec_Rs(self, v):
+        return self.matmat_Rs(np.asarray(v)[:, None])[:, 0]
+
+
 class CsrLD:
     """A general sparse LD matrix R (scipy CSR, any sparsity pattern): the
     reference's own operator for .npz and PLINK .ld inputs (src/main.py:199-200,
@@ -382,6 +436,60 @@ def cg_track(matvec_rs, gw, gam2, b, x0, rsx0, maxiter, red, rtol=1e-5):
     return x, rsx, maxiter, maxiter, nmv
 
 
+def cg_track_batch(ld_cols, gws, gam2s, B, X0, RSX0, maxiter, red, rtol=1e-5):
+    """cg_track on several columns in lockstep: every column runs scipy 1.15.3's
+    cg (iterative.py:375-422) with its own stop test, scalars and iteration
+    count, exactly as alone; only the LD products of the columns still iterating
+    on one LD matrix are taken together, Y = R_s P, one multi-column product per
+    LD matrix and iteration (``ld_cols``: list of (ld, [column indices]) with an
+    ``ld.matmat_Rs``).  Returns (X, RSX, info, n_iter, n_matvec) per column."""
+    nc = len(B)
+    X = [np.array(x, dtype=np.float64).ravel().copy() for x in X0]
+    RSX = [np.array(x, dtype=np.float64).ravel().copy() for x in RSX0]
+    Bv = [np.asarray(b, dtype=np.float64).ravel() for b in B]
+    info, n_it, n_mv = [maxiter] * nc, [maxiter] * nc, [0] * nc
+    atol, R, P, rho_prev, active = [0.0] * nc, [None] * nc, [None] * nc, [None] * nc, []
+    for j in range(nc):
+        bnrm2 = red.norm(Bv[j])
+        atol[j] = max(0.0, rtol * bnrm2)
+        if bnrm2 == 0:
+            X[j], RSX[j], info[j], n_it[j] = Bv[j].copy(), np.zeros_like(Bv[j]), 0, 0
+            continue
+        R[j] = Bv[j] - (gws[j] * RSX[j] + gam2s[j] * X[j]) if X[j].any() else Bv[j].copy()
+        active.append(j)
+    for it in range(maxiter):
+        still = []
+        for j in active:
+            if red.norm(R[j]) < atol[j]:
+                info[j], n_it[j] = 0, it
+                continue
+            rho_cur = red.dot(R[j], R[j])
+            if it > 0:
+                P[j] *= rho_cur / rho_prev[j]
+                P[j] += R[j]
+            else:
+                P[j] = R[j].copy()
+            rho_prev[j] = rho_cur
+            still.append(j)
+        active = still
+        if not active:
+            break
+        for ld, cols in ld_cols:
+            cols = [j for j in cols if j in active]
+            if not cols:
+                continue
+            Y = ld.matmat_Rs(np.stack([P[j] for j in cols], axis=1))
+            for i, j in enumerate(cols):
+                y = Y[:, i]
+                q = gws[j] * y + gam2s[j] * P[j]
+                n_mv[j] += 1
+                alpha = rho_prev[j] / red.dot(P[j], q)
+                X[j] += alpha * P[j]
+                RSX[j] += alpha * y
+                R[j] -= alpha * q
+    return X, RSX, info, n_it, n_mv
+
+
 # ----------------------------------------------------------------------------
 # probe vectors (the reference's global RNG, seeded per cohort rank)
 # ----------------------------------------------------------------------------
@@ -403,8 +511,15 @@ def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-
           prior_vars=(0.0, 1.0), prior_probs=(0.99, 0.01), x0=None, cg_maxit=500,
           em_prior_maxit=100, learn_gamw=True, lmmse_damp=False, prior_update="em",
           update_prior_from=1, seed=0, reducer=None, M_total=None, probe=None,
-          rs_recurrence=False):
+          rs_recurrence=False, batched=False):
     """All K cohorts of src/sgvamp.py:196-389 in one process.
+
+    batched: run the 2K CG solves of an iteration in lockstep (cg_track_batch:
+    each column exactly scipy's cg, the LD products of the columns on one LD
+    matrix taken together) -- the same per-column arithmetic apart from the
+    products' summation order, at the cost of max(CG iterations) LD sweeps
+    instead of their sum; needs rs_recurrence and LD objects with matmat_Rs.
+    For full-size configurations (tests/test_gpu_configs.py).
 
     rs_recurrence: carry R_s x through both CG solves (cg_track) instead of the
     direct products of the warm start and gamw learning (:352, :359) -- the
@@ -468,7 +583,61 @@ def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-
         traj["r1"].append([v / np.sqrt(Nt) for v in r1])                # :283
         der = der_denoiser_meta(r1s, gam1s, a, lam, omegas, sigmas)     # :285
         it_cg, it_info, passes = [], [], 0
-        for k in range(K):
+        if batched:
+            if not rs_recurrence:
+                raise ValueError("batched CG needs rs_recurrence=True")
+            pre = []
+            for k in range(K):                     # :285-313 for every cohort first
+                alpha1 = red.mean(der[k], M_tot)
+                if it > 0:
+                    alpha1 = rho * alpha1 + (1 - rho) * alpha1_k[k]
+                alpha1_k[k] = alpha1
+                gam2 = gam1_k[k] * (1 - alpha1) / alpha1
+                r2 = (xhat1 - alpha1 * r1[k]) / (1 - alpha1)
+                mu2 = gamw_k[k] * r[k] + gam2 * r2
+                pre.append((alpha1, gam2, r2, mu2, probes(k, it)))   # :326 (own stream)
+            cols = {}
+            for k in range(K):
+                cols.setdefault(ld_of[k], []).extend([2 * k, 2 * k + 1])
+            X, RSX, info, nit, nmv = cg_track_batch(
+                [(lds[l], c) for l, c in cols.items()],
+                [gamw_k[k] for k in range(K) for _ in (0, 1)],
+                [pre[k][1] for k in range(K) for _ in (0, 1)],
+                [v for k in range(K) for v in (pre[k][3], pre[k][4])],
+                [v for k in range(K) for v in (xhat2[k], sig2u_prev[k])],
+                [v for k in range(K) for v in (rs_x2[k], rs_s2u[k])], cg_maxit, red)
+            for k in range(K):
+                alpha1, gam2, r2, _, u = pre[k]
+                x2, rx2, s2u, rs2 = X[2 * k], RSX[2 * k], X[2 * k + 1], RSX[2 * k + 1]
+                x2_prev = xhat2[k]
+                if lmmse_damp:                                          # :322-323
+                    rx2 = rho * rx2 + (1 - rho) * rs_x2[k]
+                    x2 = rho * x2 + (1 - rho) * x2_prev
+                rs_x2[k], xhat2[k] = rx2, x2
+                sig2u_prev[k], rs_s2u[k] = s2u, rs2
+                uf = u.astype(np.float64)
+                TrSigma2 = red.dot(uf, s2u)                             # :338
+                alpha2 = gam2 * TrSigma2 / M_tot                        # :340
+                if lmmse_damp:
+                    alpha2 = rho * alpha2 + (1 - rho) * alpha2_k[k]     # :345-346
+                alpha2_k[k] = alpha2
+                gam1_k[k] = gam2 * (1 - alpha2) / alpha2                # :347
+                r1[k] = (x2 - alpha2 * r2) / (1 - alpha2)               # :348
+                gw = gamw_k[k]
+                if learn_gamw:                                          # :350-364
+                    N = N_list[k]
+                    z = N - 2 * red.dot(x2, r[k]) + red.dot(x2, rx2)
+                    if z < 0:
+                        z = 0
+                    TrRSigma2 = red.dot(uf, rs2)
+                    gw = 1 / (z / N + TrRSigma2 / N)
+                traj["gamws"][k].append(gw)                             # :373
+                gamw_k[k] = max(gw, 1.0)                                # :374
+                traj["csv"][k].append([it, gamw_k[k], gam1_k[k], gam2, alpha1, alpha2, lam])
+                it_cg.append((nit[2 * k], nit[2 * k + 1]))
+                it_info.append((info[2 * k], info[2 * k + 1]))
+                passes += nmv[2 * k] + nmv[2 * k + 1]
+        for k in range(0 if batched else K):
             alpha1 = red.mean(der[k], M_tot)
             if it > 0:
                 alpha1 = rho * alpha1 + (1 - rho) * alpha1_k[k]         # :290-291

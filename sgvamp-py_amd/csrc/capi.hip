@@ -125,7 +125,8 @@ static bool em_fuse_default() {
   return v;
 }
 // SGV_CG_EXACT=0: the pipelined CG's pass of iteration it also carries the
-// columns that stop at it's own test (one iteration of look-ahead; A/B)
+// columns that stop at it's own test (one iteration of look-ahead; A/B);
+// sgv_set_cg_exact sets the run's mode (the Engine: from the global LD size)
 static int cg_exact_default() {   // -1: by size (cg_loop_dev); 0 / 1 forced (A/B)
   const char* e = ab_env("SGV_CG_EXACT");
   return !e ? -1 : (e[0] == '0' ? 0 : 1);
@@ -133,7 +134,9 @@ static int cg_exact_default() {   // -1: by size (cg_loop_dev); 0 / 1 forced (A/
 // exact CG column sets by size: a pass narrowed from 8 to 4 columns saves ~4 %
 // of its time (north star in the solver: 10.6-10.9 vs 11.0-11.5 ms) against
 // ~30 us of host read per CG iteration, so only passes of >= ~4 ms (24 GB
-// stored) narrow; one rank only -- the choice must be the same on every rank
+// stored) narrow.  The choice must be the same on every rank and for every
+// rank count (the modes can round differently): with a communicator the
+// default (-1) is look-ahead, and the Engine sets the mode from the global size
 constexpr double CG_EXACT_MIN_BYTES = 24e9;
 static int sym_class_nc(int cls) { return std::min(16, 2 << (cls + 1)); }   // widest NC using cls
 
@@ -1644,6 +1647,14 @@ extern "C" int sgv_set_rs_recurrence(sgv_ctx* c, int on) {
 extern "C" int sgv_set_cg_pipeline(sgv_ctx* c, int on) {
   ENTER(c);
   c->cg_pipe = on ? 1 : 0;
+  return SGV_OK;
+}
+
+extern "C" int sgv_set_cg_exact(sgv_ctx* c, int mode) {
+  ENTER(c);
+  if (mode < -1 || mode > 1) return fail(c, SGV_ERR_ARG, "cg exact mode must be -1, 0 or 1");
+  const int forced = cg_exact_default();   // an A/B override wins
+  c->cg_exact = forced >= 0 ? forced : mode;
   return SGV_OK;
 }
 

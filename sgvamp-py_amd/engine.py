@@ -13,6 +13,18 @@ import numpy as np
 import hip_backend as hb
 from partition import marker_offsets, partition_blocks
 
+CG_EXACT_MIN_BYTES = 24e9   # capi.hip: exact CG column sets from passes of this size
+SYM_H = 256                 # rows per packed panel (common.h)
+
+
+def cg_exact_mode(block_sizes):
+    """The run's CG column-set mode (sgv_set_cg_exact) from the GLOBAL LD: exact
+    sets when a pass streams >= 24 GB of packed triangle, else look-ahead.  A
+    function of the global block sizes only, so every rank of a run and every
+    rank count make the same choice (the modes can round differently)."""
+    tri = sum(float(n) * (n + SYM_H) / 2.0 * 8.0 for n in block_sizes)
+    return 1 if tri >= CG_EXACT_MIN_BYTES else 0
+
 
 class Engine:
     def __init__(self, block_sizes, K, ld_of=None, comm=None, device=None, exchange=None):
@@ -51,6 +63,8 @@ class Engine:
             device = int(getattr(self.comm, "local_rank", 0)) if self.nranks > 1 else 0
         self.ctx = hb.Context(device, self.K, self.ld_of, self.local_sizes, self.b0,
                               len(self.block_sizes), self.M)
+        self.cg_exact = cg_exact_mode(self.block_sizes)
+        self.ctx.sgv_set_cg_exact(self.cg_exact)    # an SGV_CG_EXACT A/B override wins
         self.exchange = exchange or os.environ.get("SGV_EXCHANGE", "rccl")
         if self.exchange not in ("rccl", "host"):
             raise ValueError("exchange must be 'rccl' or 'host', got %r" % self.exchange)

@@ -39,6 +39,7 @@ _SIGS = {
     "sgv_comm_init_host": [_vp, ctypes.c_int, ctypes.c_int, _c_int_p, ctypes.c_void_p, _vp],
     "sgv_set_mfma_min": [_vp, ctypes.c_int],
     "sgv_set_cg_pipeline": [_vp, ctypes.c_int],
+    "sgv_set_cg_exact": [_vp, ctypes.c_int],
     "sgv_set_rs_recurrence": [_vp, ctypes.c_int],
     "sgv_reset_solver": [_vp],
     "sgv_outputs_begin": [_vp, ctypes.c_int],

@@ -30,11 +30,15 @@ def _free_port():
     (2, ["k2_shared", "k1_blocks_csr_s_damp", "k4_shared_s_damp", "k1_L3", "k1_mle"], "auto"),
     (3, ["k2_shared", "k1_blocks_csr_s_damp"], "auto"),
     (2, ["k2_shared", "k4_shared_s_damp", "k10_shared"], "per-step"),
+    (2, ["k4_shared_s_damp", "k10_shared", "k4_long50"], "cg-exact"),
 ])
 def test_sharded_ranks_match_golden(world, cases, em):
     """em: "auto" = the size rule (these small cases: replicated EM, r1 gathered
     once per loop); "per-step" forces one exchange per EM step (the rule's choice
-    above about a million cohort-markers, e.g. the north star)."""
+    above about a million cohort-markers, e.g. the north star); "cg-exact" forces
+    the exact CG column sets (the global-size rule's choice for >= 24 GB of LD,
+    e.g. the north star and C5), so one rank and two ranks must agree bitwise in
+    that mode too (tools/two_rank_gpu.py reruns each case on one rank)."""
     port = _free_port()
     procs = []
     for r in range(world):
@@ -42,6 +46,8 @@ def test_sharded_ranks_match_golden(world, cases, em):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SGV_EXCHANGE="host")
         if em == "per-step":
             env.update(SGV_AB="1", SGV_EM_REP="0")
+        if em == "cg-exact":
+            env.update(SGV_AB="1", SGV_CG_EXACT="1")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "two_rank_gpu.py")]
                                       + cases, env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))

@@ -105,3 +105,49 @@ def test_probe_stream_matches_global_rng():
     first = binomial(p=1 / 2, n=1, size=500) * 2 - 1
     s.draw(0, 500)
     np.testing.assert_array_equal(s.draw(1, 500), first)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_batched_panel_oracle_matches_reference(name):
+    """The full-size checker (tests/test_gpu_configs.py): the 2K CG solves of an
+    iteration in lockstep (cg_track_batch, one multi-column LD product per LD
+    matrix) over the packed-panel LD (PanelLD, half the host memory) -- pinned to
+    the reference's fixtures at the same bar as the one-column-at-a-time oracle,
+    and equal to it to rounding with identical CG and EM counts."""
+    c = Case(name)
+    if any(not np.array_equal(B, B.T) for blocks in c.ld_blocks for B in blocks):
+        pytest.skip("PanelLD holds symmetric blocks only")
+    lds = []
+    for blocks in c.ld_blocks:
+        L = vo.PanelLD(s=c.flags["s"], H=64)      # small panels: several per block
+        for B in blocks:
+            L.add_block(B)
+        lds.append(L)
+    with np.errstate(all="ignore"):
+        t = vo.infer(lds, c.ld_of, list(c.r), c.N, c.flags["iterations"], x0=c.x0,
+                     rs_recurrence=True, batched=True, **c.kwargs())
+    ref = run_oracle(c, rs_recurrence=True)
+    np.testing.assert_array_equal(np.array(t["cg_iters"]).transpose(1, 0, 2), c.cg_iters)
+    np.testing.assert_array_equal(np.array(t["cg_info"]).transpose(1, 0, 2), c.cg_info)
+    assert list(t["em_steps"]) == list(c.em_steps)
+    for it in range(c.flags["iterations"]):
+        assert maxrel(t["xhat"][it], c.xhat[it]) < 1e-10, it
+        assert maxrel(t["xhat"][it], ref["xhat"][it]) < 1e-10, it
+    np.testing.assert_allclose(np.array(t["csv"]), c.cohort_csv, rtol=1e-5, atol=0)
+
+
+def test_panel_ld_products():
+    rs = np.random.RandomState(0)
+    blocks = []
+    for n in (1, 70, 300, 129):
+        X = rs.normal(size=(2 * n, n))
+        blocks.append(X.T @ X)
+    L = vo.PanelLD(s=0.1, H=32)
+    for B in blocks:
+        L.add_block(B)
+    D = vo.BlockLD(blocks, s=0.1)
+    V = rs.normal(size=(sum(b.shape[0] for b in blocks), 5))
+    Y = L.matmat_Rs(V)
+    for j in range(5):
+        assert maxrel(Y[:, j], D.matvec_Rs(V[:, j])) < 1e-13
+    assert maxrel(L.matvec_Rs(V[:, 0]), Y[:, 0]) < 1e-14
