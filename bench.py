@@ -68,7 +68,7 @@ def parse():
     p.add_argument("--K", type=int, default=4)
     p.add_argument("--seed", type=int, default=2025)
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    p.add_argument("--cpu-blocks", type=int, default=2,
+    p.add_argument("--cpu-blocks", type=int, default=4,
                    help="LD blocks of the CPU-baseline sample (see cpu_baseline)")
     p.add_argument("--cpu-iters", type=int, default=3)
     p.add_argument("--no-files", action="store_true", help="skip the per-iteration output files")
@@ -150,24 +150,57 @@ def matvecs_per_step(recs, learn_gamw=True):
     return tot / max(len(recs), 1)
 
 
-def cpu_baseline(eng, args, ref_flags, recs, x0):
-    """The oracle (the build's NumPy restatement of the reference, OpenBLAS
-    threads) timed on a bounded sample of the SAME workload and extrapolated to
-    the full one with the GPU run's own CG counts.
+# The reference's per-marker Python loops (measured by
+# importing src/sgvamp.py): denoiser_meta + der_denoiser_meta per marker and
+# iteration (src/sgvamp.py:273,285), and one EM step (:116-136) per 200k
+# markers per cohort count (1 core each).
+REF_DENOISE_S_PER_MARKER = 17.7e-6 + 27.7e-6
+REF_EM_S_PER_200K = {1: 0.013, 4: 0.034, 8: 0.064}
 
-    Sample: LD blocks 0 .. cpu_blocks-1 (dense f64, as the reference stores
-    them) with all K cohorts' r and x0 restricted to those markers, run for
-    cpu_iters outer iterations.  The oracle's LD mat-vecs are timed separately
-    (one call = one column over the sample's blocks).  Full-workload step time
-    = (non-LD time per step) x (M / sample markers) + (mat-vec time per block)
-    x (LD blocks) x (single-column mat-vecs per step of the reference with the
-    CG counts recorded in the timed GPU steps).  The reference itself never
-    travels to the GPU box; its CPU cost model is that of this restatement."""
+
+def _ref_em_step_s(M, K):
+    ks = sorted(REF_EM_S_PER_200K)
+    k0 = max([k for k in ks if k <= K] or [ks[0]])
+    k1 = min([k for k in ks if k >= K] or [ks[-1]])
+    t0, t1 = REF_EM_S_PER_200K[k0], REF_EM_S_PER_200K[k1]
+    t = t0 if k1 == k0 else t0 + (t1 - t0) * (K - k0) / (k1 - k0)
+    return t * M / 200000.0
+
+
+def usable_cores():
+    """CPUs this process may run on (the box's share), not the machine's count."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(eng, args, ref_flags, recs, x0):
+    """Two CPU figures for the same workload, neither run on the GPU box by
+    the reference itself (it never travels there):
+
+    * ``value`` -- the oracle (the build's NumPy restatement of the reference,
+      OpenBLAS on every usable core) TIMED on a bounded sample of the workload
+      and extrapolated.  Sample: LD blocks 0 .. cpu_blocks-1 (dense f64, as the
+      reference stores them) with all K cohorts' r and x0 on those markers, run
+      for cpu_iters outer iterations; its LD mat-vecs timed separately.  Full
+      step = (non-LD time per step) x (M / sample markers) + (mat-vec time per
+      block) x (LD blocks) x (single-column mat-vecs per step of the reference
+      with the CG counts recorded in the timed GPU steps).  When the sample is
+      the whole problem the measured step is reported beside the model
+      (``measured_step_s``, ``model_error``).
+    * ``reference_formula`` -- the reference's own cost structure (SURVEY.md
+      section 8d(i)): its mat-vecs streamed at the dgemv rate this box just
+      measured (dense blocks; its .npz CSR path runs single-threaded at ~4 GB/s,
+      ~10x slower), plus its per-marker denoiser loops (45.4 us per marker and
+      iteration on each MPI rank, the K ranks in parallel), plus its EM steps
+      (the GPU run's step counts, one core per rank)."""
     import threadpoolctl
 
     from oracle import vamp_oracle as vo
     import hip_backend as hb
 
+    cores = usable_cores()
     S = max(1, min(args.cpu_blocks, len(eng.block_sizes)))
     n = int(sum(eng.block_sizes[:S]))
     blocks = [eng.get_ld_block(0, b) for b in range(S)]
@@ -185,28 +218,53 @@ def cpu_baseline(eng, args, ref_flags, recs, x0):
 
     L.matvec_R = timed
     its = args.cpu_iters
-    t0 = time.perf_counter()
-    vo.infer([L], [0] * eng.K, r_list, [args.nsamp] * eng.K, its, x0=x0[:n],
-             reducer=vo.Reducer(), seed=args.seed, **ref_flags)
-    dt = time.perf_counter() - t0
-    info = threadpoolctl.threadpool_info()
-    threads = max([i.get("num_threads", 1) for i in info if i.get("internal_api") in
-                   ("openblas", "mkl", "blis")] or [1])
+    with threadpoolctl.threadpool_limits(limits=cores):
+        info = threadpoolctl.threadpool_info()
+        threads = max([i.get("num_threads", 1) for i in info if i.get("internal_api") in
+                       ("openblas", "mkl", "blis")] or [1])
+        t0 = time.perf_counter()
+        traj = vo.infer([L], [0] * eng.K, r_list, [args.nsamp] * eng.K, its, x0=x0[:n],
+                        reducer=vo.Reducer(), seed=args.seed, **ref_flags)
+        dt = time.perf_counter() - t0
     mv_block = t_mv[0] / max(t_mv[1], 1) / S
+    dense_block_bytes = sum(b * b for b in eng.block_sizes[:S]) * 8.0 / S
+    dgemv_GBs = dense_block_bytes / mv_block / 1e9
     other = (dt - t_mv[0]) / its * (eng.M / float(n))
     nmv = matvecs_per_step(recs, ref_flags.get("learn_gamw", True))
     step = other + mv_block * len(eng.block_sizes) * nmv
-    return dict(value=1.0 / step, unit="VAMP it/s", cores=int(threads), kind="port",
-                host_cpus=os.cpu_count(), extrapolated=True,
-                sample="extrapolated: oracle/vamp_oracle.py (NumPy + OpenBLAS, %d threads) on LD "
-                       "blocks 0-%d (%d markers, %.1f GB dense), all %d cohorts, %d iterations "
-                       "in %.2f s: %.1f ms per single-column mat-vec per LD block, %.1f ms of "
-                       "non-LD work per step scaled to M=%d; full step = %.1f ms non-LD + %d "
-                       "blocks x %.1f mat-vecs per step (the reference's count with the GPU "
-                       "run's CG iterations) = %.2f s" % (
-                           threads, S - 1, n, sum(b * b for b in eng.block_sizes[:S]) * 8 / 1e9, eng.K, its, dt,
-                           mv_block * 1e3, other * 1e3, eng.M, other * 1e3,
-                           len(eng.block_sizes), nmv, step))
+    out = dict(value=1.0 / step, unit="VAMP it/s", cores=int(threads), kind="port",
+               host_cpus=os.cpu_count(), usable_cpus=cores, extrapolated=S < len(eng.block_sizes),
+               sample="oracle/vamp_oracle.py (NumPy + OpenBLAS, %d threads) on LD blocks 0-%d (%d "
+                      "markers, %.1f GB dense), all %d cohorts, %d iterations in %.2f s: %.1f ms per "
+                      "single-column mat-vec per LD block (%.0f GB/s), %.1f ms of non-LD work per "
+                      "step scaled to M=%d; full step = %.1f ms non-LD + %d blocks x %.1f mat-vecs "
+                      "per step (the reference's count with the GPU run's CG iterations) = %.2f s" % (
+                          threads, S - 1, n, dense_block_bytes * S / 1e9, eng.K, its, dt,
+                          mv_block * 1e3, dgemv_GBs, other * 1e3, eng.M, other * 1e3,
+                          len(eng.block_sizes), nmv, step))
+    if S == len(eng.block_sizes):
+        # the sample is the whole problem: the model against the measured step
+        # (the oracle's own CG counts instead of the GPU run's)
+        meas = dt / its
+        out.update(measured_step_s=meas, model_step_s=step, model_error=step / meas - 1.0,
+                   oracle_cg_iters=traj["cg_iters"])
+    # the reference's cost structure, with this box's dgemv rate
+    M, K = eng.M, eng.K
+    dense_pass = sum(float(b) * b for b in eng.block_sizes) * 8.0
+    em_steps = np.mean([r.get("em_steps") or 0 for r in recs])
+    t_mv_ref = nmv * dense_pass / (dgemv_GBs * 1e9)
+    t_den = M * REF_DENOISE_S_PER_MARKER
+    t_em = em_steps * _ref_em_step_s(M, K)
+    t_ref = t_mv_ref + t_den + t_em
+    out["reference_formula"] = dict(
+        value=1.0 / t_ref, unit="VAMP it/s", kind="reference cost model (extrapolated)",
+        step_s=t_ref, matvec_s=t_mv_ref, denoiser_loops_s=t_den, em_s=t_em,
+        formula="%.1f single-column mat-vecs x %.1f GB dense / %.0f GB/s (this box's dgemv) "
+                "+ %d markers x 45.4 us (src/sgvamp.py:273,285 per-marker loops, K ranks in "
+                "parallel) + %.1f EM steps x %.0f ms (src/sgvamp.py:116-136 at M=%d, K=%d)" % (
+                    nmv, dense_pass / 1e9, dgemv_GBs, M, em_steps, _ref_em_step_s(M, K) * 1e3,
+                    M, K))
+    return out
 
 
 def main():
@@ -291,7 +349,15 @@ def main():
     tm = eng.timers()
     # this box's own streaming-read rate (after the timed region; context only:
     # the roofline peak stays the guide's 8 TB/s); the slowest rank's
-    box_bw = min(comm.allgather(eng.read_bw(8 << 30, 5))) if args.read_bw else None
+    box_bw = None
+    if args.read_bw:
+        try:
+            bw = eng.read_bw(8 << 30, 5)
+        except Exception as e:  # noqa: BLE001 -- context only: the bench line stays valid
+            log("[bench] streaming-read probe failed: %s" % e)
+            bw = 0.0
+        bws = comm.allgather(bw)
+        box_bw = min(bws) if min(bws) > 0 else None
     for rec in recs:
         log("[bench] it=%d cg=%s em=%s passes=%d %.1f ms l2=%s waits(ms): probes %.2f outputs %.2f "
             "writes %.2f" % (

@@ -2664,7 +2664,10 @@ extern "C" int sgv_read_bw(sgv_ctx* c, int64_t bytes, int reps, double* gbps) {
   if (e1) (void)hipEventDestroy(e1);
   if (buf) (void)hipFree(buf);
   if (out) (void)hipFree(out);
-  CHK(rc);
+  if (rc != SGV_OK) {
+    (void)hipGetLastError();   // clear it: the next launch_* would report this failure
+    return rc;
+  }
   *gbps = (double)bytes / ((double)best * 1e-3) / 1e9;
   return SGV_OK;
 }

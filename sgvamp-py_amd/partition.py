@@ -68,20 +68,26 @@ def coarsen_blocks(sizes, min_size=128):
     padded vector segment) into blocks of at least min_size: a diagonal or
     near-diagonal LD (e.g. a PLINK .ld without pairs: R = I) would otherwise
     become M blocks of one marker, each padded to 128 in every device vector.
-    Blocks already >= min_size are kept as they are; the merged blocks hold zeros
-    between their parts (same matrix, coarser partition)."""
-    out, acc = [], 0
+    Blocks already >= min_size are kept as they are -- a small run is never
+    merged into one (that would grow its n x n storage and change its row
+    stride) -- and the merged blocks hold zeros between their parts (same
+    matrix, coarser partition).  A trailing small run joins the previous block
+    only when that one is itself merged from small blocks."""
+    out, merged, acc, nacc = [], [], 0, 0
     for n in sizes:
         n = int(n)
         if acc and n >= min_size:     # a pending run of small blocks stays apart from a big one
             out.append(acc)
-            acc = 0
+            merged.append(True)
+            acc, nacc = 0, 0
         acc += n
+        nacc += 1
         if acc >= min_size:
             out.append(acc)
-            acc = 0
+            merged.append(nacc > 1)
+            acc, nacc = 0, 0
     if acc:
-        if out and acc < min_size:
+        if out and merged[-1]:
             out[-1] += acc
         else:
             out.append(acc)

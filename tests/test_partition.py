@@ -86,6 +86,11 @@ def test_coarsen_blocks_merges_tiny_blocks():
     assert coarsen_blocks([200, 250, 150]) == [200, 250, 150]      # golden CSR layout unchanged
     c = coarsen_blocks([1] * 3000 + [2050])                        # R = I beside a band
     assert sum(c) == 5050 and c[-2:] == [56, 2050] and min(c[:-2]) >= 128 and len(c) == 25
-    assert coarsen_blocks([1] * 100 + [5000] + [3] * 10) == [100, 5030]
+    # a small run is never merged into a big block (its n x n storage would grow)
+    assert coarsen_blocks([1] * 100 + [5000] + [3] * 10) == [100, 5000, 30]
+    assert coarsen_blocks([5, 20000]) == [5, 20000]
+    assert coarsen_blocks([20000, 5]) == [20000, 5]
+    assert coarsen_blocks([20000, 100, 100, 5]) == [20000, 205]      # joins a merged block
+    assert coarsen_blocks([60, 70, 5]) == [135]
     assert coarsen_blocks([5] * 10) == [50]
     assert coarsen_blocks([]) == []
