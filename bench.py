@@ -66,6 +66,9 @@ def parse():
     p.add_argument("--block-size", type=int, default=15625)
     p.add_argument("--nsamp", type=int, default=10000)
     p.add_argument("--K", type=int, default=4)
+    p.add_argument("--distinct-ld", action="store_true",
+                   help="one LD matrix per cohort (the reference's per-rank ld_fpaths_list[rank], "
+                        "src/main.py:173,199-202) instead of K cohorts sharing one")
     p.add_argument("--seed", type=int, default=2025)
     p.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     p.add_argument("--cpu-blocks", type=int, default=4,
@@ -95,20 +98,27 @@ def parse():
 
 def make_problem(eng, comm, args):
     """beta and noise on the host (RandomState, as the reference recipe);
-    genotypes, LD blocks, g and r on the device."""
+    genotypes, LD blocks, g and r on the device.  Cohorts sharing an LD matrix
+    share its genotypes (their own noise); with one LD matrix per cohort
+    (--distinct-ld, the reference's native layout: ld_fpaths_list[rank],
+    src/main.py:173,199-202) cohort k has its own genotypes, the same beta."""
     M, N = eng.M, args.nsamp
     rs = np.random.RandomState(args.seed)
     cm = int(M * 0.5)                                   # sim_gen_phen_mult.py:28-32
     beta = np.zeros(M)
     beta[rs.choice(M, cm, replace=False)] = rs.normal(0, np.sqrt(0.8 / cm), cm)
-    geno_seed = args.seed + 1
-    g_loc = eng.synth_ld_g(0, geno_seed, N, beta)       # (nblk_local, N)
-    g_all = np.concatenate(comm.allgather(g_loc)) if comm.Get_size() > 1 else g_loc
-    g = g_all[0].copy()
-    for b in range(1, g_all.shape[0]):                  # global block order
-        g = g + g_all[b]
+    gs = {}
+    for ld in range(eng.nld):
+        geno_seed = args.seed + 1 + 7919 * ld
+        g_loc = eng.synth_ld_g(ld, geno_seed, N, beta)      # (nblk_local, N)
+        g_all = np.concatenate(comm.allgather(g_loc)) if comm.Get_size() > 1 else g_loc
+        g = g_all[0].copy()
+        for b in range(1, g_all.shape[0]):                  # global block order
+            g = g + g_all[b]
+        gs[ld] = (geno_seed, g)
     ys = []
     for k in range(eng.K):
+        geno_seed, g = gs[eng.ld_of[k]]
         w = np.random.RandomState(args.seed + 1000 + k).normal(0.0, np.sqrt(0.2), N)
         y = g + w
         eng.synth_r(k, geno_seed, N, y)
@@ -168,7 +178,12 @@ def _ref_em_step_s(M, K):
 
 
 def usable_cores():
-    """CPUs this process may run on (the box's share), not the machine's count."""
+    """The host threads this process is given: OMP_NUM_THREADS when the box
+    sets it (its CPU share: 16 per GPU on the MI355X pool, whose os.cpu_count()
+    reports the whole machine), else the CPUs it may run on."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
     try:
         return len(os.sched_getaffinity(0))
     except AttributeError:
@@ -201,29 +216,32 @@ def cpu_baseline(eng, args, ref_flags, recs, x0):
     import hip_backend as hb
 
     cores = usable_cores()
-    S = max(1, min(args.cpu_blocks, len(eng.block_sizes)))
+    # host memory: at most cpu_blocks dense blocks over all LD matrices
+    S = max(1, min(args.cpu_blocks // eng.nld, len(eng.block_sizes)))
     n = int(sum(eng.block_sizes[:S]))
-    blocks = [eng.get_ld_block(0, b) for b in range(S)]
     r_list = [eng.get_vector(hb.VEC_R, k)[:n].copy() for k in range(eng.K)]
-    L = vo.BlockLD(blocks, s=args.ridge)
     t_mv = [0.0, 0]
-    raw = L.matvec_R
+    lds = []
+    for ld in range(eng.nld):
+        L = vo.BlockLD([eng.get_ld_block(ld, b) for b in range(S)], s=args.ridge)
+        raw = L.matvec_R
 
-    def timed(v):
-        t = time.perf_counter()
-        out = raw(v)
-        t_mv[0] += time.perf_counter() - t
-        t_mv[1] += 1
-        return out
+        def timed(v, raw=raw):
+            t = time.perf_counter()
+            out = raw(v)
+            t_mv[0] += time.perf_counter() - t
+            t_mv[1] += 1
+            return out
 
-    L.matvec_R = timed
+        L.matvec_R = timed
+        lds.append(L)
     its = args.cpu_iters
     with threadpoolctl.threadpool_limits(limits=cores):
         info = threadpoolctl.threadpool_info()
         threads = max([i.get("num_threads", 1) for i in info if i.get("internal_api") in
                        ("openblas", "mkl", "blis")] or [1])
         t0 = time.perf_counter()
-        traj = vo.infer([L], [0] * eng.K, r_list, [args.nsamp] * eng.K, its, x0=x0[:n],
+        traj = vo.infer(lds, eng.ld_of, r_list, [args.nsamp] * eng.K, its, x0=x0[:n],
                         reducer=vo.Reducer(), seed=args.seed, **ref_flags)
         dt = time.perf_counter() - t0
     mv_block = t_mv[0] / max(t_mv[1], 1) / S
@@ -233,7 +251,10 @@ def cpu_baseline(eng, args, ref_flags, recs, x0):
     nmv = matvecs_per_step(recs, ref_flags.get("learn_gamw", True))
     step = other + mv_block * len(eng.block_sizes) * nmv
     out = dict(value=1.0 / step, unit="VAMP it/s", cores=int(threads), kind="port",
-               host_cpus=os.cpu_count(), usable_cpus=cores, extrapolated=S < len(eng.block_sizes),
+               host_cpus=os.cpu_count(), cores_given=cores,
+               cores_note="threads = the box's CPU share (OMP_NUM_THREADS), not the machine's "
+                          "%d CPUs" % (os.cpu_count() or 0),
+               extrapolated=S < len(eng.block_sizes),
                sample="oracle/vamp_oracle.py (NumPy + OpenBLAS, %d threads) on LD blocks 0-%d (%d "
                       "markers, %.1f GB dense), all %d cohorts, %d iterations in %.2f s: %.1f ms per "
                       "single-column mat-vec per LD block (%.0f GB/s), %.1f ms of non-LD work per "
@@ -250,7 +271,7 @@ def cpu_baseline(eng, args, ref_flags, recs, x0):
                    oracle_cg_iters=traj["cg_iters"])
     # the reference's cost structure, with this box's dgemv rate
     M, K = eng.M, eng.K
-    dense_pass = sum(float(b) * b for b in eng.block_sizes) * 8.0
+    dense_pass = sum(float(b) * b for b in eng.block_sizes) * 8.0   # one LD matrix
     em_steps = np.mean([r.get("em_steps") or 0 for r in recs])
     t_mv_ref = nmv * dense_pass / (dgemv_GBs * 1e9)
     t_den = M * REF_DENOISE_S_PER_MARKER
@@ -295,7 +316,8 @@ def main():
     sizes = [args.block_size] * args.blocks
     K = args.K
     t_setup = time.perf_counter()
-    eng = Engine(sizes, K, ld_of=[0] * K, comm=comm, device=device,
+    ld_of = list(range(K)) if args.distinct_ld else [0] * K
+    eng = Engine(sizes, K, ld_of=ld_of, comm=comm, device=device,
                  exchange="host" if args.share_device else
                  (None if args.exchange == "auto" else args.exchange))
     eng.set_ld_packing(args.ld_format == "packed")
@@ -374,11 +396,14 @@ def main():
     bytes_launch = ld_bytes_launch + tm["rhs_bytes"] / launches
     achieved = bytes_launch / avg_s / 1e9 if avg_s > 0 else None
     dense_equiv = (tm["dense_bytes"] / launches + tm["rhs_bytes"] / launches) / avg_s / 1e9
-    mfma = args.ld_format == "packed" and 2 * K >= 3     # NC >= 3: the f64 MFMA pass
+    nc_pass = 2 * K // eng.nld                         # columns per LD pass
+    mfma = args.ld_format == "packed" and nc_pass >= 3  # NC >= 3: the f64 MFMA pass
     traffic, traffic_src = read_traffic(("k_sym_mfma" if mfma else "k_sym_pass")
                                         if args.ld_format == "packed" else "k_ld_pass",
                                         bytes_launch, K, eng.M)
-    if eng.M == 200000 and args.ridge == 0 and not args.lmmse_damp:
+    if args.distinct_ld and K > 1:
+        cname = "distinct per-cohort LD (the reference's ld_fpaths_list[rank] layout)"
+    elif eng.M == 200000 and args.ridge == 0 and not args.lmmse_damp:
         cname = {1: "C2 (BASELINE.json configs[1])", 4: "C3 (BASELINE.json configs[2])"}.get(K, "custom")
     elif eng.M == 1000000 and K == 4 and args.ridge == 0 and not args.lmmse_damp:
         cname = ("north-star configuration (BASELINE.json north_star: LD mat-vec at M=1e6, K=4) "
@@ -406,12 +431,15 @@ def main():
         "data": "synthetic: device generator following simulation/sim_gen_phen_mult.py "
                 "(Bin(2,0.4) genotypes, 50%% causal, h2=0.8), seed %d" % args.seed,
         "config": {
-            "workload": "%s: K=%d cohort(s) sharing one LD, M=%d markers in %d LD blocks "
+            "workload": "%s: K=%d cohort(s) %s, M=%d markers in %d LD blocks "
                         "of %d, N=%d per cohort, reference CLI default flags, output files written "
-                        "each iteration, prior %s %s" % (cname, K, eng.M, args.blocks,
+                        "each iteration, prior %s %s" % (cname, K, "with one LD matrix each"
+                                                         if args.distinct_ld else "sharing one LD",
+                                                         eng.M, args.blocks,
                                                          args.block_size, args.nsamp,
                                                          prior["prior_vars"], prior["prior_probs"]),
             "K": K, "M": eng.M, "ld_blocks": args.blocks, "block_size": args.block_size,
+            "ld_matrices": eng.nld,
             "s": args.ridge, "lmmse_damp": bool(args.lmmse_damp),
             "N": args.nsamp, "parallelism": "LD blocks sharded over %d GPU rank(s)" % world,
             "share_device": bool(args.share_device),

@@ -68,7 +68,7 @@ struct LdPlan {
 // A/B tuning switches: an environment override is honoured only with
 // SGV_AB=1 (and then announced once on stderr); without it a set override is
 // ignored with a warning, so no stray variable changes a production run.
-static const char* ab_env(const char* name) {
+const char* sgv::ab_env(const char* name) {
   const char* v = std::getenv(name);
   if (!v) return nullptr;
   const char* ab = std::getenv("SGV_AB");

@@ -285,6 +285,9 @@ __device__ __forceinline__ void fin_epilogue(const SymPanel& pn, const PassArgs&
     partials[(int64_t)pn.part * NC + t] = ((s_w[0][t] + s_w[1][t]) + s_w[2][t]) + s_w[3][t];
 }
 
+// A/B tuning switch from the environment, honoured only with SGV_AB=1 (capi.hip)
+const char* ab_env(const char* name);
+
 // streaming-read probe over `bytes` of buf (diag.hip); out: >= 256 doubles
 hipError_t launch_read_probe(const double* buf, size_t bytes, double* out, hipStream_t st);
 
