@@ -26,7 +26,7 @@
 // Each 16 x 32 sub-tile is loaded from HBM once, 16 B per lane:
 //   col fragment  lane l: R[row 4a + (l>>4)][col pair (l&15), + e]   (a = 0..3)
 //       A_b[m][k] = R[row k][pair 4b+m]: Dcol[pair][c] += R[j][i] P[j][c]
-// and written to a per-wave LDS tile (rows padded to 34 doubles) from which
+// and written to a per-wave LDS tile (16 x 32, XOR-swizzled 16-B pieces) from which
 //   row fragment  lane l: R[row 4q + (l&3)][col pair (l>>4) + 4b, + e] (q = 0..3)
 //       A_b[m][k] = R[row m][pair k+4b]: Drow[row][c] += R[j][i] P[i][c]
 // is read back without bank conflicts.  Each 4x4x4 block contracts its own 4
@@ -51,7 +51,7 @@ __device__ __forceinline__ void lds_order() {
 }
 
 constexpr int MF_CW = 512;   // chunk width (class 1 items)
-constexpr int MF_LDP = 34;   // staging row pitch (doubles): conflict-free both ways
+constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conflict-free both ways
 
 // Strips: a workgroup owns one 512-column chunk over up to S panels of one
 // parity (g0, g0 + 2, ...: the panels whose items share that chunk's column
@@ -328,260 +328,6 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   }
 }
 
-// ---------------------------------------------------------------------------
-// The same pass with the R sub-tiles streamed HBM -> LDS by LDS-DMA
-// (global_load_lds_dwordx4: no VGPR destination) into a per-wave ring of D
-// 4-KiB slots, and the column-part B operands (P at the row group's 16 rows,
-// the Pk rows) by two more DMAs per row group.  Every operand then reaches the
-// MFMAs through ds_read_b128: the column fragment, and the row fragment that
-// the register version rebuilt through a ds_write of the tile.  The prefetch
-// ring no longer holds registers, and the wave's only in-loop waits are its
-// own counted vmcnt (the DMA'd data is wave-private, so no barrier orders it).
-//
-// LDS image of one 16 x 32 sub-tile: 16-B piece (row r, column pair p) at slot
-// 16 r + (p ^ (r & 3)).  One DMA instruction writes slots 64a .. 64a + 63
-// lane-linearly (rows 4a .. 4a + 3), so lane l fetches row 4a + (l >> 4), pair
-// (l & 15) ^ ((l >> 4) & 3) -- a permutation inside each 256-B row segment,
-// still fully coalesced.  Both fragment reads are conflict-free: the column
-// fragment reads whole rows, and the row fragment's 16 lanes of a quarter-wave
-// (rows 4q + (l & 3), pairs 4((l >> 2) & 3) + (l >> 4)) land on 16 distinct
-// slots mod 16.  MFMA operands, their order and every sum are those of
-// k_sym_mfma: the results are bitwise the same.
-//
-// Waits: the LDS-DMA of step s + D goes out after step s's fragments were read
-// (lgkmcnt(0): no DMA overwrites a slot that is still being read), so at step
-// s's wait the ops issued after R(s) are R(s+1 .. s+D-1) and, in the first D
-// steps of a row group, that group's Pk DMA (issued at its first step) --
-// constants once the 4 steps of a row group are unrolled.  The row-sum
-// exchange between the waves uses a raw s_barrier (a __syncthreads would wait
-// vmcnt(0) and drain the ring); the row-partial stores at a panel's end drain
-// it once (vmcnt(0): stores and loads share the counter and are not assumed
-// to retire in order).
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-__device__ __forceinline__ void lds_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
-__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
-template <int NG, int D>
-__global__ __launch_bounds__(256, 2) void k_sym_mfma_glds(const SymStrip* __restrict__ strips,
-                                                         const SymItem* __restrict__ sitems,
-                                                         const double* __restrict__ pk, int ncol,
-                                                         double* __restrict__ rowpart,
-                                                         double* __restrict__ colpart,
-                                                         const int* __restrict__ run) {
-  constexpr int NW = 4;
-  constexpr int WC = MF_CW / NW;   // columns per wave (128)
-  constexpr int NT = WC / 32;      // 32-column steps per wave (4)
-  static_assert(D >= 1 && D <= NT, "ring depth: the Pk DMA accounting assumes D <= 4");
-  // one __shared__ array (a second object can make hipcc wait vmcnt(0) before
-  // the first ds_read of every step)
-  constexpr int OFF_RED = 0;                          // [2][NW][256]
-  constexpr int OFF_RBUF = OFF_RED + 2 * NW * 256;    // [SYM_H][4 * NG]
-  constexpr int OFF_WAVE = OFF_RBUF + SYM_H * 4 * NG;
-  constexpr int WAVE_SZ = D * 512 + 2 * 256;          // ring + two Pk-row buffers
-  __shared__ __attribute__((aligned(16))) double smem[OFF_WAVE + NW * WAVE_SZ];
-  const SymStrip sp = strips[blockIdx.x];
-  if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
-  const int lane = threadIdx.x & (WAVE - 1);
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-  const int lo = lane & 15, hi = lane >> 4, bq = (lane >> 2) & 3, n4 = lane & 3;
-  const int pc = hi + 4 * bq;
-  SymItem cur = sitems[sp.it0];
-  const int c0 = cur.c0, ncc = cur.nc;
-  const double* pkb = pk + (int64_t)cur.voff * 16;
-  const int cw0 = wid * WC;
-  const bool dhalf = cw0 < SYM_H;
-  double* ring = smem + OFF_WAVE + wid * WAVE_SZ;
-  double* pkbuf = ring + D * 512;
-  double* rbuf = smem + OFF_RBUF;
-
-  double brow[NT][2][NG];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int col = cw0 + 32 * t + 2 * pc + e;
-#pragma unroll
-      for (int q = 0; q < NG; ++q) {
-        const double v = ldg(pkb + (int64_t)(c0 + (col < ncc ? col : 0)) * 16 + 4 * q + n4);
-        brow[t][e][q] = col < ncc ? v : 0.0;
-      }
-    }
-  double dcol[NT][2][NG];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int e = 0; e < 2; ++e)
-#pragma unroll
-      for (int q = 0; q < NG; ++q) dcol[t][e][q] = 0.0;
-  wait_vm<0>();   // brow is in registers before the first DMA goes out
-
-  // this lane's DMA source piece in a sub-tile: row 4a + hi, pair lo ^ (hi & 3)
-  const int dpair = lo ^ (hi & 3);
-  // R sub-tile (row group g, step t) of a panel (b0 = element (r0, c0)) into ring slot
-  auto dma_r = [&](uint64_t b0, int64_t ws, int H, int g, int t, double* slot) {
-    asm volatile("" : "+s"(b0));
-    const int xc = cw0 + 32 * t + 2 * dpair;
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int rB = 16 * g + 4 * a + hi;
-      const double* src = (const double*)b0 + (int64_t)(rB < H ? rB : H - 1) * ws +
-                          (xc < ncc ? xc : 0);
-      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(slot + 128 * a), 16, 0, 0);
-    }
-  };
-  // the Pk rows of row group g of a panel (first row r0): 16 rows x 16 doubles
-  auto dma_pk = [&](int r0, int H, int g, double* buf) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int rB = 16 * g + 8 * i + (lane >> 3);
-      const double* src = pkb + (int64_t)(r0 + (rB < H ? rB : H - 1)) * 16 + 2 * (lane & 7);
-      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(buf + 128 * i), 16, 0, 0);
-    }
-  };
-  auto pbase = [&](const SymItem& x) { return (uint64_t)(x.P + (x.c0 - x.r0)); };
-
-  uint64_t curb = pbase(cur);
-  // prologue: the Pk rows of the first row group, then steps 0 .. D-1
-  dma_pk(cur.r0, cur.H, 0, pkbuf);
-#pragma unroll
-  for (int p = 0; p < D; ++p) dma_r(curb, cur.w, cur.H, 0, p, ring + 512 * p);
-
-  int gg = 0;
-#pragma unroll 1
-  for (int s = 0; s < sp.npan; ++s) {
-    const bool more = s + 1 < sp.npan;
-    const SymItem nx = sitems[sp.it0 + (more ? s + 1 : s)];
-    const uint64_t nxb = more ? pbase(nx) : (uint64_t)pkb;
-    const int ng = (cur.H + 15) / 16;
-    const bool dz = dhalf && cur.r0 == c0;            // diagonal block: no column part
-#pragma unroll 1
-    for (int g = 0; g < ng; ++g, ++gg) {
-      const bool same = g + 1 < ng;
-      const uint64_t gb = same ? curb : nxb;
-      const int64_t gw = same ? cur.w : (more ? nx.w : 0);
-      const int gH = same ? cur.H : (more ? nx.H : 1);
-      const int gn = same ? g + 1 : 0;
-      const int gr0 = same ? cur.r0 : nx.r0;
-      double* pkc = pkbuf + 256 * (gg & 1);
-      // the next row group's Pk rows (its first step needs them): DMA now
-      dma_pk(gr0, gH, gn, pkbuf + 256 * ((gg + 1) & 1));
-      double bcol[4][NG];
-      double drow[4][NG];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int q = 0; q < NG; ++q) drow[r][q] = 0.0;
-#pragma unroll
-      for (int t = 0; t < NT; ++t) {
-        double* slot = ring + 512 * ((4 * gg + t) % D);
-        // R(step) has landed: 4 (D - 1) later R pieces, + this group's Pk DMA
-        // while it is younger than R(step), may still be in flight
-        if (t < D)
-          wait_vm<4 * (D - 1) + 2>();
-        else
-          wait_vm<4 * (D - 1)>();
-        d2 cf[4], rf[4];
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-          cf[a] = *(const d2*)(slot + 128 * a + 2 * (16 * hi + (lo ^ (hi & 3))));
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int rr = 4 * r + n4;
-          rf[r] = *(const d2*)(slot + 32 * rr + 2 * (pc ^ n4));
-        }
-        if (t == 0) {
-#pragma unroll
-          for (int a = 0; a < 4; ++a)
-#pragma unroll
-            for (int q = 0; q < NG; ++q) {
-              const int rB = 16 * g + 4 * a + hi;
-              const double v = pkc[(4 * a + hi) * 16 + 4 * q + n4];
-              bcol[a][q] = (rB < cur.H && !dz) ? v : 0.0;
-            }
-        }
-        wait_lgkm0();   // fragments in registers: the slot may be refilled
-        // step + D: this group's t + D, or the next group's t + D - NT
-        if (t + D < NT)
-          dma_r(curb, cur.w, cur.H, g, t + D, slot);
-        else
-          dma_r(gb, gw, gH, gn, t + D - NT, slot);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int q = 0; q < NG; ++q) {
-            dcol[t][0][q] = MFMA4(cf[a].x, bcol[a][q], dcol[t][0][q]);
-            dcol[t][1][q] = MFMA4(cf[a].y, bcol[a][q], dcol[t][1][q]);
-          }
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(rf[r].x, brow[t][0][q], drow[r][q]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(rf[r].y, brow[t][1][q], drow[r][q]);
-        __builtin_amdgcn_s_setprio(0);
-      }
-      double* rb = smem + OFF_RED + ((gg & 1) * NW + wid) * 256;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int q = 0; q < NG; ++q) {
-          double v = drow[r][q];
-          v = v + row_ror<12>(v);
-          v = v + row_ror<8>(v);
-          if (bq == 0) rb[((4 * r + hi) << 4) + 4 * q + n4] = v;
-        }
-      lds_barrier();
-      {
-        const int t = threadIdx.x, row = t >> 4, cc = t & 15;
-        if (16 * g + row < cur.H && cc < ncol) {
-          const double* red = smem + OFF_RED + (gg & 1) * NW * 256;
-          double v = red[t];
-#pragma unroll
-          for (int w = 1; w < NW; ++w) v += red[w * 256 + t];
-          rbuf[(16 * g + row) * ncol + cc] = v;
-        }
-      }
-    }
-    {   // the item's H x ncol row sums, contiguous in rowpart
-      lds_barrier();
-      const int n = cur.H * ncol;
-      double* dst = rowpart + (int64_t)cur.item * SYM_H * ncol;
-      for (int i = threadIdx.x; 2 * i < n; i += NW * 64) {
-        if (2 * i + 1 < n)
-          *(d2*)(dst + 2 * i) = *(const d2*)(rbuf + 2 * i);
-        else
-          dst[2 * i] = rbuf[2 * i];
-      }
-      // stores and DMAs share vmcnt: drain once per panel, then the counted
-      // waits of the next panel hold again.  The barrier keeps rbuf's reads
-      // ahead of the next panel's writes to it.
-      wait_vm<0>();
-      lds_barrier();
-    }
-    cur = nx;
-    curb = nxb;
-  }
-  wait_vm<0>();   // no DMA into LDS outlives the workgroup
-#pragma unroll
-  for (int q = 0; q < NG; ++q) {
-    const int cc = 4 * q + n4;
-    if (cc < ncol) {
-      double* out = colpart + ((int64_t)sp.slot * ncol + cc) * MF_CW;
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-        *(d2*)(out + cw0 + 32 * t + 2 * pc) = d2{dcol[t][0][q], dcol[t][1][q]};
-    }
-  }
-}
-
 // 13..16 right-hand sides: v_mfma_f64_16x16x4f64 (one 16-column group, 140
 // cycles per 16x16x4) keeps fewer accumulators and B operands in registers
 // than four 4x4x4 groups, which spill at 4 waves.  Same strips as above:
@@ -805,24 +551,6 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run);
 }
 
-template <int NG, int D>
-static void launch_mf_glds(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
-                           const double* d_pk, int nc, double* rowpart, double* colpart,
-                           const int* run, hipStream_t st) {
-  hipLaunchKernelGGL((k_sym_mfma_glds<NG, D>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                     d_sitems, d_pk, nc, rowpart, colpart, run);
-}
-
-// SGV_MF_GLDS (A/B, with SGV_AB=1): 0 = register-staged k_sym_mfma, D = 1..4 =
-// the LDS-DMA variant with a D-slot ring per wave (NC <= 8)
-static int mf_glds_depth() {
-  static const int v = [] {
-    const char* e = ab_env("SGV_MF_GLDS");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                            const PassArgs& pa, int64_t mpad, double* d_pk, double* rowpart,
                            double* colpart, hipStream_t st) {
@@ -833,21 +561,6 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
   // 9..16 columns: one 16x16x4 group beats three/four 4x4x4 groups (register
   // pressure) and splitting the groups over two wave sets (the repeat R reads do
   // not come from cache): measured in DESIGN.md
-  const int gd = mf_glds_depth();
-  if (gd > 0 && nc <= 8) {
-    const bool g1 = nc <= 4;
-    switch (gd) {
-      case 1: g1 ? launch_mf_glds<1, 1>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, st)
-                 : launch_mf_glds<2, 1>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, st); break;
-      case 2: g1 ? launch_mf_glds<1, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, st)
-                 : launch_mf_glds<2, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, st); break;
-      case 3: g1 ? launch_mf_glds<1, 3>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, st)
-                 : launch_mf_glds<2, 3>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, st); break;
-      default: g1 ? launch_mf_glds<1, 4>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, st)
-                  : launch_mf_glds<2, 4>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, st); break;
-    }
-    return hipGetLastError();
-  }
   switch ((nc + 3) / 4) {
     // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
     case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, st); break;
