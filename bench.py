@@ -264,10 +264,15 @@ def cpu_baseline(eng, args, ref_flags, recs, x0):
                           mv_block * 1e3, dgemv_GBs, other * 1e3, eng.M, other * 1e3,
                           len(eng.block_sizes), nmv, step))
     if S == len(eng.block_sizes):
-        # the sample is the whole problem: the model against the measured step
-        # (the oracle's own CG counts instead of the GPU run's)
+        # the sample is the whole problem: the model against the measured
+        # steps, with the mat-vec count of the oracle's own iterations (0 ..
+        # cpu_iters-1: no warm-start residual at iteration 0)
         meas = dt / its
-        out.update(measured_step_s=meas, model_step_s=step, model_error=step / meas - 1.0,
+        gw = 2 if ref_flags.get("learn_gamw", True) else 0
+        nmv_o = sum(n1 + n2 + (2 if it > 0 else 0) + gw
+                    for it, per_k in enumerate(traj["cg_iters"]) for n1, n2 in per_k) / its
+        model_o = other + mv_block * len(eng.block_sizes) * nmv_o
+        out.update(measured_step_s=meas, model_step_s=model_o, model_error=model_o / meas - 1.0,
                    oracle_cg_iters=traj["cg_iters"])
     # the reference's cost structure, with this box's dgemv rate
     M, K = eng.M, eng.K
