@@ -190,6 +190,41 @@ def usable_cores():
         return os.cpu_count() or 1
 
 
+def _oracle_sample(eng, args, ref_flags, x0, S):
+    """The oracle on LD blocks 0 .. S-1 of every LD matrix (dense f64, as the
+    reference stores them) with all cohorts' r and x0 on those markers, for
+    cpu_iters outer iterations; LD mat-vecs timed separately.  Returns the
+    wall time, the mat-vec time per single-column product per block, the
+    non-LD time per step scaled to M, and the oracle's own mat-vecs per step."""
+    from oracle import vamp_oracle as vo
+    import hip_backend as hb
+
+    n = int(sum(eng.block_sizes[:S]))
+    r_list = [eng.get_vector(hb.VEC_R, k)[:n].copy() for k in range(eng.K)]
+    t_mv = [0.0, 0]
+    lds = []
+    for ld in range(eng.nld):
+        L = vo.BlockLD([eng.get_ld_block(ld, b) for b in range(S)], s=args.ridge)
+        raw = L.matvec_R
+
+        def timed(v, raw=raw):
+            t = time.perf_counter()
+            out = raw(v)
+            t_mv[0] += time.perf_counter() - t
+            t_mv[1] += 1
+            return out
+
+        L.matvec_R = timed
+        lds.append(L)
+    its = args.cpu_iters
+    t0 = time.perf_counter()
+    traj = vo.infer(lds, eng.ld_of, r_list, [args.nsamp] * eng.K, its, x0=x0[:n],
+                    reducer=vo.Reducer(), seed=args.seed, **ref_flags)
+    dt = time.perf_counter() - t0
+    return dict(n=n, dt=dt, traj=traj, mv_block=t_mv[0] / max(t_mv[1], 1) / S,
+                other=(dt - t_mv[0]) / its * (eng.M / float(n)), nmv=t_mv[1] / its)
+
+
 def cpu_baseline(eng, args, ref_flags, recs, x0):
     """Two CPU figures for the same workload, neither run on the GPU box by
     the reference itself (it never travels there):
@@ -212,42 +247,23 @@ def cpu_baseline(eng, args, ref_flags, recs, x0):
       (the GPU run's step counts, one core per rank)."""
     import threadpoolctl
 
-    from oracle import vamp_oracle as vo
-    import hip_backend as hb
-
     cores = usable_cores()
+    its = args.cpu_iters
     # host memory: at most cpu_blocks dense blocks over all LD matrices
     S = max(1, min(args.cpu_blocks // eng.nld, len(eng.block_sizes)))
-    n = int(sum(eng.block_sizes[:S]))
-    r_list = [eng.get_vector(hb.VEC_R, k)[:n].copy() for k in range(eng.K)]
-    t_mv = [0.0, 0]
-    lds = []
-    for ld in range(eng.nld):
-        L = vo.BlockLD([eng.get_ld_block(ld, b) for b in range(S)], s=args.ridge)
-        raw = L.matvec_R
-
-        def timed(v, raw=raw):
-            t = time.perf_counter()
-            out = raw(v)
-            t_mv[0] += time.perf_counter() - t
-            t_mv[1] += 1
-            return out
-
-        L.matvec_R = timed
-        lds.append(L)
-    its = args.cpu_iters
     with threadpoolctl.threadpool_limits(limits=cores):
         info = threadpoolctl.threadpool_info()
         threads = max([i.get("num_threads", 1) for i in info if i.get("internal_api") in
                        ("openblas", "mkl", "blis")] or [1])
-        t0 = time.perf_counter()
-        traj = vo.infer(lds, eng.ld_of, r_list, [args.nsamp] * eng.K, its, x0=x0[:n],
-                        reducer=vo.Reducer(), seed=args.seed, **ref_flags)
-        dt = time.perf_counter() - t0
-    mv_block = t_mv[0] / max(t_mv[1], 1) / S
+        smp = _oracle_sample(eng, args, ref_flags, x0, S)
+        # the sample is the whole problem: validate the extrapolation from a
+        # two-block sub-sample against it (same basis: the full oracle run's
+        # mat-vecs per step)
+        sub = _oracle_sample(eng, args, ref_flags, x0, 2) \
+            if S == len(eng.block_sizes) and S > 2 else None
+    n, dt, mv_block, other = smp["n"], smp["dt"], smp["mv_block"], smp["other"]
     dense_block_bytes = sum(b * b for b in eng.block_sizes[:S]) * 8.0 / S
     dgemv_GBs = dense_block_bytes / mv_block / 1e9
-    other = (dt - t_mv[0]) / its * (eng.M / float(n))
     nmv = matvecs_per_step(recs, ref_flags.get("learn_gamw", True))
     step = other + mv_block * len(eng.block_sizes) * nmv
     out = dict(value=1.0 / step, unit="VAMP it/s", cores=int(threads), kind="port",
@@ -263,17 +279,15 @@ def cpu_baseline(eng, args, ref_flags, recs, x0):
                           threads, S - 1, n, dense_block_bytes * S / 1e9, eng.K, its, dt,
                           mv_block * 1e3, dgemv_GBs, other * 1e3, eng.M, other * 1e3,
                           len(eng.block_sizes), nmv, step))
-    if S == len(eng.block_sizes):
-        # the sample is the whole problem: the model against the measured
-        # steps, with the mat-vec count of the oracle's own iterations (0 ..
-        # cpu_iters-1: no warm-start residual at iteration 0)
+    if sub is not None:
         meas = dt / its
-        gw = 2 if ref_flags.get("learn_gamw", True) else 0
-        nmv_o = sum(n1 + n2 + (2 if it > 0 else 0) + gw
-                    for it, per_k in enumerate(traj["cg_iters"]) for n1, n2 in per_k) / its
-        model_o = other + mv_block * len(eng.block_sizes) * nmv_o
-        out.update(measured_step_s=meas, model_step_s=model_o, model_error=model_o / meas - 1.0,
-                   oracle_cg_iters=traj["cg_iters"])
+        model = sub["other"] + sub["mv_block"] * len(eng.block_sizes) * smp["nmv"]
+        out.update(measured_step_s=meas, model_from_2_blocks_step_s=model,
+                   model_error=model / meas - 1.0, oracle_cg_iters=smp["traj"]["cg_iters"],
+                   model_note="the extrapolation the sample line uses, from LD blocks 0-1 "
+                              "(%d markers), against the oracle measured on the whole problem; "
+                              "both with the whole run's %.1f mat-vecs per step"
+                              % (sub["n"], smp["nmv"]))
     # the reference's cost structure, with this box's dgemv rate
     M, K = eng.M, eng.K
     dense_pass = sum(float(b) * b for b in eng.block_sizes) * 8.0   # one LD matrix
