@@ -826,7 +826,7 @@ static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa) {
       HIPCHK(launch_sym_finalize_strip(nc, pl.d_spanels, pl.npanels, pa, c->d_rowpart,
                                        c->d_colpart, c->d_part, c->st));
       c->aux_bytes += 2.0 * 8.0 * nc * ((double)pl.nitems[cls] * SYM_H + (double)pl.nstrips * 512);
-      c->aux_bytes += 8.0 * (double)c->Mpad * (16 + nc);   // Pk pack
+      c->aux_bytes += 8.0 * (double)c->Mpad * ((nc <= 4 ? 4 : nc <= 8 ? 8 : 16) + nc);   // Pk pack
     } else {
       HIPCHK(launch_sym_pass(nc, cls, pl.d_items[cls], pl.nitems[cls], pa, c->d_rowpart,
                              c->d_colpart, c->st));

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
                                                          const double* __restrict__ pk, int ncol,
                                                          double* __restrict__ rowpart,
                                                          double* __restrict__ colpart,
-                                                         const int* __restrict__ run) {
+                                                         const int* __restrict__ run, int pks) {
   static_assert(NW == 4, "waves 0 and 1 own the diagonal half of a chunk");
   constexpr int WC = MF_CW / NW;   // columns per wave (128)
   constexpr int NT = WC / 32;      // 32-column steps per wave
@@ -99,7 +99,8 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   const int pc = hi + 4 * bq;                          // this lane's column pair in a fragment
   SymItem cur = sitems[sp.it0];
   const int c0 = cur.c0, ncc = cur.nc;                 // the strip's chunk
-  const double* pkb = pk + (int64_t)cur.voff * 16;    // Pk of this block (block-relative index)
+  const int PKS = pks;             // Pk row stride (k_pack): 4 NG, or 16 (A/B)
+  const double* pkb = pk + (int64_t)cur.voff * PKS;   // Pk of this block (block-relative index)
   const int cw0 = wid * WC;                            // first chunk column of this wave
   const bool dhalf = cw0 < SYM_H;                      // wave inside a diagonal panel's diag block
   double* sb = stg[wid];
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
       const int col = cw0 + 32 * t + 2 * pc + e;
 #pragma unroll
       for (int q = 0; q < NG; ++q) {
-        const double v = ldg(pkb + (int64_t)(c0 + (col < ncc ? col : 0)) * 16 + 4 * q + n4);
+        const double v = ldg(pkb + (int64_t)(c0 + (col < ncc ? col : 0)) * PKS + 4 * q + n4);
         brow[t][e][q] = col < ncc ? v : 0.0;
       }
     }
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
       const int rB = 16 * g + 4 * a + hi;
 #pragma unroll
       for (int q = 0; q < NG; ++q) {
-        const double v = ldg(pkb + (int64_t)(r0 + (rB < H ? rB : 0)) * 16 + 4 * q + n4);
+        const double v = ldg(pkb + (int64_t)(r0 + (rB < H ? rB : 0)) * PKS + 4 * q + n4);
         bc[a][q] = (rB < H && !zero) ? v : 0.0;
       }
     }
@@ -518,14 +519,18 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize_strip(
   fin_epilogue<NC>(pn, pa, y, partials, pre);
 }
 
-// Pk[i][c] = in[c][i] for c < ncol, 0 for ncol <= c < 16 (i over the padded vector)
-__global__ __launch_bounds__(256) void k_pack16(PassArgs pa, int ncol, int64_t mpad,
-                                                double* __restrict__ pk) {
+// Pk[i][c] = in[c][i] for c < ncol, 0 for ncol <= c < PKS (i over the padded
+// vector).  PKS = the columns the pass kernel's groups read: 4 (NC <= 4), 8
+// (NC <= 8), 16 -- a row is one cache line's worth of what is read, so the
+// pass's Pk reads (L2 misses on M = 1e6) carry no unused columns
+template <int PKS>
+__global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpad,
+                                              double* __restrict__ pk) {
   if (pa.run && !ldg(pa.run)) return;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= mpad * 16) return;
-  const int64_t i = t >> 4;
-  const int c = (int)(t & 15);
+  if (t >= mpad * PKS) return;
+  const int64_t i = t / PKS;
+  const int c = (int)(t % PKS);
   pk[t] = c < ncol ? pa.in[c][i] : 0.0;
 }
 
@@ -542,29 +547,40 @@ static bool mf_pw() {
 template <int NG, int NW, int PD>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
-                      const int* run, hipStream_t st) {
+                      const int* run, int pks, hipStream_t st) {
   if (mf_pw())
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true>), dim3(nstrips), dim3(NW * 64), 0, st,
-                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run);
+                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, false>), dim3(nstrips), dim3(NW * 64), 0, st,
-                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run);
+                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
 }
 
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                            const PassArgs& pa, int64_t mpad, double* d_pk, double* rowpart,
                            double* colpart, hipStream_t st) {
   if (nc < 1 || nc > 16) return hipErrorInvalidValue;
-  const int64_t n16 = mpad * 16;
-  hipLaunchKernelGGL(k_pack16, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, st, pa, nc,
-                     mpad, d_pk);
+  // SGV_PK16=1 (A/B, SGV_AB=1): the round-2 16-column Pk rows for every NC
+  static const bool pk16 = [] {
+    const char* e = ab_env("SGV_PK16");
+    return e && e[0] == '1';
+  }();
+  const int pks = (nc > 8 || pk16) ? 16 : nc <= 4 ? 4 : 8;
+  const int64_t npk = mpad * pks;
+  const dim3 pg((unsigned)((npk + 255) / 256));
+  if (pks == 4)
+    hipLaunchKernelGGL(k_pack<4>, pg, dim3(256), 0, st, pa, nc, mpad, d_pk);
+  else if (pks == 8)
+    hipLaunchKernelGGL(k_pack<8>, pg, dim3(256), 0, st, pa, nc, mpad, d_pk);
+  else
+    hipLaunchKernelGGL(k_pack<16>, pg, dim3(256), 0, st, pa, nc, mpad, d_pk);
   // 9..16 columns: one 16x16x4 group beats three/four 4x4x4 groups (register
   // pressure) and splitting the groups over two wave sets (the repeat R reads do
   // not come from cache): measured in DESIGN.md
   switch ((nc + 3) / 4) {
     // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
-    case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, st); break;
-    case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, st); break;
+    case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, st); break;
+    case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, st); break;
     default:
       hipLaunchKernelGGL(k_sym_mfma16, dim3(nstrips), dim3(256), 0, st, d_strips, d_sitems, d_pk,
                          nc, rowpart, colpart, pa.run);

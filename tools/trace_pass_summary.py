@@ -4,7 +4,7 @@ the bench line's HIP-event average (roofline.avg_launch_ms).
 The pipelined CG enqueues one pass past its stop test; that pass exits at once
 (~5 us), and rocprofv3's --stats average mixes it in.  This summary keeps the
 passes that ran: k_sym_mfma / k_sym_pass / k_ld_pass dispatches of >= 100 us,
-each with the k_pack16 before it and the finalize after it.
+each with the k_pack (k_pack16 before round 3) before it and the finalize after it.
     python tools/trace_pass_summary.py TRACE.csv [BENCH.json]
 """
 import csv
@@ -21,7 +21,7 @@ def main():
     passes = []
     for i, (s, e, n) in enumerate(rows):
         if any(m in n for m in MAIN) and "finalize" not in n and e - s >= 100_000:
-            t0 = rows[i - 1][0] if i and "k_pack16" in rows[i - 1][2] else s
+            t0 = rows[i - 1][0] if i and "k_pack" in rows[i - 1][2] else s
             t1 = rows[i + 1][1] if i + 1 < len(rows) and "finalize" in rows[i + 1][2] else e
             passes.append(((e - s) / 1e6, (t1 - t0) / 1e6, n.split("(")[0]))
     if not passes:
