@@ -135,11 +135,15 @@ def test_cli_plink_ld_equals_npz(tmp_path):
         np.testing.assert_array_equal(a, b)
 
 
-def test_cli_two_ranks_bitwise_equal_one_rank(tmp_path):
-    """main.py under torchrun-style env with 2 ranks (LD blocks sharded; both ranks
-    on device 0 with the host exchange, since RCCL refuses two ranks per device):
-    every output .bin file is bitwise the single-process one (ordered per-block
-    reductions), and the per-cohort CSV is identical."""
+@pytest.mark.parametrize("launch", ["env", "mpirun", "gpus"])
+def test_cli_two_ranks_bitwise_equal_one_rank(tmp_path, launch):
+    """main.py as 2 ranks (LD blocks sharded; both ranks on device 0 with the
+    host exchange, since RCCL refuses two ranks per device), launched three
+    ways: RANK/WORLD_SIZE set per process ("env"), only Open MPI's variables --
+    the reference's own `mpirun -np 2 python main.py` (src/main.py:16-18) --
+    ("mpirun"), and `main.py --gpus 2` starting its ranks itself ("gpus").  Every
+    output .bin file is bitwise the single-process one (ordered per-block
+    reductions) and the per-cohort CSV is identical: one job, not two copies."""
     import socket
     import subprocess
     import sys
@@ -184,12 +188,26 @@ def test_cli_two_ranks_bitwise_equal_one_rank(tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     code = ("import sys; sys.path.insert(0, %r); import main; main.main(sys.argv[1:])"
             % os.path.join(root, "sgvamp-py_amd"))
+    base = {k: v for k, v in os.environ.items()
+            if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    base["SGV_EXCHANGE"] = "host"
     procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE="2",
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SGV_EXCHANGE="host")
-        procs.append(subprocess.Popen([sys.executable, "-c", code] + argv(two), env=env,
-                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    if launch == "gpus":
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(root, "sgvamp-py_amd", "main.py")] + argv(two)
+            + ["--gpus", "2", "--device", "0"], env=base, stdout=subprocess.PIPE,
+            stderr=subprocess.STDOUT, text=True))
+    for r in range(2 if launch != "gpus" else 0):
+        if launch == "env":
+            env = dict(base, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE="2",
+                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        else:
+            env = dict(base, OMPI_COMM_WORLD_RANK=str(r), OMPI_COMM_WORLD_SIZE="2",
+                       OMPI_COMM_WORLD_LOCAL_RANK=str(r), OMPI_COMM_WORLD_LOCAL_SIZE="2",
+                       OMPI_MCA_ess_base_jobid="cli%d" % port, SGV_COMM_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-c", code] + argv(two) + ["--device", "0"],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True))
     for p in procs:
         out, _ = p.communicate(timeout=240)
         assert p.returncode == 0, out[-3000:]
