@@ -40,6 +40,26 @@ namespace sgv {
 
 #define MFMA4(a, b, c) __builtin_amdgcn_mfma_f64_4x4x4f64((a), (b), (c), 0, 0, 0)
 
+// Diagnostic build only (make EXTRA=-DSGV_MF_TRACE, tools/strip_trace.py): each
+// workgroup (strip) of the last NC <= 8 MFMA pass records its start / end wall
+// clock (100 MHz) and CU, to see how the launch fills the device.  Not in the
+// product library.
+#ifdef SGV_MF_TRACE
+constexpr int MF_TRACE_MAX = 1 << 16;
+__device__ unsigned long long g_mf_trace[3 * MF_TRACE_MAX];
+#define MF_TRACE_BEGIN const unsigned long long tr_t0 = wall_clock64();
+#define MF_TRACE_END                                                          \
+  __syncthreads();                                                            \
+  if (threadIdx.x == 0 && blockIdx.x < MF_TRACE_MAX) {                        \
+    g_mf_trace[3 * blockIdx.x] = tr_t0;                                       \
+    g_mf_trace[3 * blockIdx.x + 1] = wall_clock64();                          \
+    g_mf_trace[3 * blockIdx.x + 2] = (unsigned long long)__smid();            \
+  }
+#else
+#define MF_TRACE_BEGIN
+#define MF_TRACE_END
+#endif
+
 // wave-local LDS ordering point: lanes of one wave exchange data through the
 // tile.  The LDS executes a wave's DS instructions in order, so the write ->
 // read (and read -> next write) order only has to survive compilation: a
@@ -67,7 +87,7 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // per panel when the item's row partials are written -- the same additions as
 // the per-row-group exchange through red[] (PW = false), with one barrier pair
 // per panel instead of a barrier per 16-row group.
-template <int NG, int NW, int PD, bool PW>
+template <int NG, int NW, int PD, bool PW, bool SKIP>
 __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
                                                          const SymItem* __restrict__ sitems,
                                                          const double* __restrict__ pk, int ncol,
@@ -93,6 +113,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   double* rbuf = rowbuf + 2 * NW * 256;
   const SymStrip sp = strips[blockIdx.x];
   if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
+  MF_TRACE_BEGIN
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lo = lane & 15, hi = lane >> 4, bq = (lane >> 2) & 3, n4 = lane & 3;
@@ -103,6 +124,13 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   const double* pkb = pk + (int64_t)cur.voff * PKS;   // Pk of this block (block-relative index)
   const int cw0 = wid * WC;                            // first chunk column of this wave
   const bool dhalf = cw0 < SYM_H;                      // wave inside a diagonal panel's diag block
+  // SKIP: a wave's 32-column steps at or past the chunk's last column (the
+  // ragged last chunk of a panel: 4 % of the north star's steps) take no LDS or
+  // MFMA work -- their row-part B operands are 0 and their column sums are never
+  // read, so every kept sum is bitwise the same; nor do the column MFMAs of the
+  // diagonal-block waves of a diagonal panel (B = 0 there).  The loads stay, so
+  // the load count is the same on every path.
+  const int nta = SKIP ? min(NT, max(0, (ncc - cw0 + 31) / 32)) : NT;
   double* sb = stg[wid];
 
   // row-part B operands: P at this wave's columns, reused by every row group
@@ -194,6 +222,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int q = 0; q < NG; ++q) drow[r][q] = 0.0;
+      const bool colz = SKIP && dhalf && cur.r0 == c0;   // this panel's column B operands are 0
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         d2 cf[4], rf[4];
@@ -207,6 +236,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
           load_cf(gb, gw, gH, gn, t + PD - NT, cfq[slot]);
           if (t + PD == NT) load_bcol(gr0, gH, gz, gn, bcn);
         }
+        if (t >= nta) continue;                        // wave-uniform: past the chunk
         lds_order();                                   // previous step's tile reads issued
 #pragma unroll
         for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[a];
@@ -220,13 +250,15 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
         // (NC = 4/8 0.7-1.5 % faster per pass on two boxes; NC = 16 1 % slower,
         // not used there -- profiles/r02s10_prio_ab.txt)
         __builtin_amdgcn_s_setprio(1);
+        if (!colz) {
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+          for (int a = 0; a < 4; ++a)
 #pragma unroll
-          for (int q = 0; q < NG; ++q) {
-            dcol[t][0][q] = MFMA4(cf[a].x, bcol[a][q], dcol[t][0][q]);
-            dcol[t][1][q] = MFMA4(cf[a].y, bcol[a][q], dcol[t][1][q]);
-          }
+            for (int q = 0; q < NG; ++q) {
+              dcol[t][0][q] = MFMA4(cf[a].x, bcol[a][q], dcol[t][0][q]);
+              dcol[t][1][q] = MFMA4(cf[a].y, bcol[a][q], dcol[t][1][q]);
+            }
+        }
         // x halves of all 4*NG chains, then the y halves: a chain's two MFMAs are
         // 4*NG issues apart instead of back to back (same per-chain order)
 #pragma unroll
@@ -327,6 +359,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
         *(d2*)(out + cw0 + 32 * t + 2 * pc) = d2{dcol[t][0][q], dcol[t][1][q]};
     }
   }
+  MF_TRACE_END
 }
 
 // 13..16 right-hand sides: v_mfma_f64_16x16x4f64 (one 16-column group, 140
@@ -340,6 +373,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int MF_WC = MF_CW / 4;
 constexpr int MF_NT = MF_WC / 32;
 
+template <bool SKIP>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -359,6 +393,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
   const double* pkb = pk + (int64_t)cur.voff * 16;    // Pk of this block (block-relative index)
   const int cw0 = wid * MF_WC;                         // first chunk column of this wave
   const bool dhalf = cw0 < SYM_H;
+  const int nta = SKIP ? min(MF_NT, max(0, (ncc - cw0 + 31) / 32)) : MF_NT;   // as k_sym_mfma
 
   double* sb = stg[wid];
   // row-part B operands (P at this wave's columns), reused by every row group
@@ -423,6 +458,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
 #pragma unroll
       for (int a = 0; a < 4; ++a) bcol[a] = bcn[a];
       d4 drow0 = d4{0.0, 0.0, 0.0, 0.0}, drow1 = drow0;
+      const bool colz = SKIP && dhalf && cur.r0 == c0;
 #pragma unroll
       for (int t = 0; t < MF_NT; ++t) {
         d2 cf[4], rf[4];
@@ -435,16 +471,19 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
           load_cf(gb, gw, gH, gn, 0, cfn);
           load_bcol(gr0, gH, gz, gn, bcn);
         }
+        if (t >= nta) continue;
         lds_order();                                   // previous step's tile reads done
 #pragma unroll
         for (int a = 0; a < 4; ++a) *(d2*)(sb + (4 * a + hi) * LDP + 2 * lo) = cf[a];
         lds_order();                                   // tile written
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) rf[s2] = *(const d2*)(sb + lo * LDP + 8 * s2 + 2 * hi);
+        if (!colz) {
 #pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          dcol[t][0] = MFMA16(cf[a].x, bcol[a], dcol[t][0]);
-          dcol[t][1] = MFMA16(cf[a].y, bcol[a], dcol[t][1]);
+          for (int a = 0; a < 4; ++a) {
+            dcol[t][0] = MFMA16(cf[a].x, bcol[a], dcol[t][0]);
+            dcol[t][1] = MFMA16(cf[a].y, bcol[a], dcol[t][1]);
+          }
         }
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) {
@@ -544,15 +583,29 @@ static bool mf_pw() {
   return v;
 }
 
+// SGV_MF_SKIP (A/B, with SGV_AB=1): default 1 = no LDS/MFMA work on steps past
+// the chunk (bitwise the same products; the 8-block share 2-4 % faster per pass,
+// the 64-block north star unchanged -- profiles/r03/skip_ab.jsonl); 0 = every step
+static bool mf_skip() {
+  static const bool v = [] {
+    const char* e = ab_env("SGV_MF_SKIP");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 template <int NG, int NW, int PD>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
                       const int* run, int pks, hipStream_t st) {
-  if (mf_pw())
-    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true>), dim3(nstrips), dim3(NW * 64), 0, st,
+  if (mf_pw() && mf_skip())
+    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true>), dim3(nstrips), dim3(NW * 64), 0, st,
+                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (mf_pw())
+    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, false>), dim3(nstrips), dim3(NW * 64), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else
-    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, false>), dim3(nstrips), dim3(NW * 64), 0, st,
+    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, false, false>), dim3(nstrips), dim3(NW * 64), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
 }
 
@@ -582,12 +635,24 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
     case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, st); break;
     case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, st); break;
     default:
-      hipLaunchKernelGGL(k_sym_mfma16, dim3(nstrips), dim3(256), 0, st, d_strips, d_sitems, d_pk,
-                         nc, rowpart, colpart, pa.run);
+      if (mf_skip())
+        hipLaunchKernelGGL(k_sym_mfma16<true>, dim3(nstrips), dim3(256), 0, st, d_strips, d_sitems,
+                           d_pk, nc, rowpart, colpart, pa.run);
+      else
+        hipLaunchKernelGGL(k_sym_mfma16<false>, dim3(nstrips), dim3(256), 0, st, d_strips, d_sitems,
+                           d_pk, nc, rowpart, colpart, pa.run);
       break;
   }
   return hipGetLastError();
 }
+
+#ifdef SGV_MF_TRACE
+extern "C" int sgv_diag_mf_trace(unsigned long long* out, int n) {
+  if (n > MF_TRACE_MAX) n = MF_TRACE_MAX;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mf_trace), sizeof(unsigned long long) * 3 * n) ==
+                 hipSuccess ? n : -1;
+}
+#endif
 
 hipError_t launch_sym_finalize_strip(int nc, const SymPanel* d_panels, int npanels,
                                      const PassArgs& pa, const double* rowpart,

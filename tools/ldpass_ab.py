@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--ncols", default="4,8")
     ap.add_argument("--nsamp", type=int, default=2000)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rhs", default="normal", choices=["normal", "zero", "ones"],
+                    help="right-hand sides (zero/ones: the pass's data-dependent power, not its products)")
     a = ap.parse_args()
     for shape in a.shapes.split(","):
         nb, n = (int(x) for x in shape.split("x"))
@@ -37,6 +39,10 @@ def main():
         rs = np.random.RandomState(0)
         for nc in [int(x) for x in a.ncols.split(",")]:
             V = rs.normal(size=(nc, M))
+            if a.rhs == "zero":
+                V[:] = 0.0
+            elif a.rhs == "ones":
+                V[:] = 1.0
             Y = eng.ld_matvec(0, V)                       # warm
             eng.timers(reset=True)
             for _ in range(a.reps):
