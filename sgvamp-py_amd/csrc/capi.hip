@@ -630,6 +630,12 @@ static bool sym_lpt() {
   return !(e && e[0] == '0');
 }
 
+// MFMA-pass finalize panels dispatched most work first (env SGV_FIN_LPT=0: panel order)
+static bool fin_lpt() {
+  const char* e = ab_env("SGV_FIN_LPT");
+  return e && e[0] == '1';
+}
+
 // panels per MFMA strip (env SGV_MFMA_STRIP, read when a plan is built; 1 =
 // one (panel, chunk) item per workgroup)
 static int mfma_strip_len() {
@@ -692,6 +698,14 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
   }
   std::stable_sort(strips.begin(), strips.end(),
                    [](const SymStrip& a, const SymStrip& b) { return a.npan > b.npan; });
+  // finalize dispatch order (a panel's sums do not depend on it): most row and
+  // column parts first, so the one-item panels at the blocks' ends fill the tail
+  if (fin_lpt())
+    std::stable_sort(sp.begin(), sp.end(), [](const SymPanel& a, const SymPanel& b) {
+      const int wa = (a.item_end - a.item_begin) + (a.own_se - a.own_sb) + (a.oth_se - a.oth_sb);
+      const int wb = (b.item_end - b.item_begin) + (b.own_se - b.own_sb) + (b.oth_se - b.oth_sb);
+      return wa > wb;
+    });
   pl->nstrips = (int)strips.size();
   CHK(upload_table(c, strips, &pl->d_strips));
   CHK(upload_table(c, sitems, &pl->d_sitems));
