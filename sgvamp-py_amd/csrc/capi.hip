@@ -630,10 +630,11 @@ static bool sym_lpt() {
   return !(e && e[0] == '0');
 }
 
-// MFMA-pass finalize panels dispatched most work first (env SGV_FIN_LPT=0: panel order)
+// MFMA-pass finalize panels dispatched most work first (bitwise the same; NC = 16
+// -0.8 % per pass, profiles/r03/fin_lpt_ab.jsonl); env SGV_FIN_LPT=0: panel order
 static bool fin_lpt() {
   const char* e = ab_env("SGV_FIN_LPT");
-  return e && e[0] == '1';
+  return !(e && e[0] == '0');
 }
 
 // panels per MFMA strip (env SGV_MFMA_STRIP, read when a plan is built; 1 =

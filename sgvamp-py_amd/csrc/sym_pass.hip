@@ -204,11 +204,13 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize(const SymPanel* __
   fin_epilogue<NC>(pn, pa, y, partials, pre);
 }
 
-// SGV_SYM_SKIP (A/B, with SGV_AB=1): 1 = sweep only the stored segments of a chunk
+// SGV_SYM_SKIP (A/B, with SGV_AB=1): default 1 = sweep only the stored segments of a
+// chunk (bitwise the same; north-star blocks NC = 2 -2.5 %, profiles/r03/sym_skip_ab.jsonl);
+// 0 = every segment
 static bool sym_skip() {
   static const bool v = [] {
     const char* e = ab_env("SGV_SYM_SKIP");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return v;
 }
