@@ -208,6 +208,10 @@ int sgv_probe_draw(uint32_t* key, int32_t* pos, int64_t n, int64_t lo, int64_t h
  *   sgv_lmmse (damping iff SGV_STEP_LMMSE_DAMP, gamw learning iff
  *   SGV_STEP_LEARN_GAMW): out, cg_out as sgv_lmmse; ires[1] = LD passes.
  * res holds 1 + 2K + 4 doubles, ires 2 ints.
+ * flags & SGV_STEP_MLE: sgv_mle_update instead of sgv_em (lam_io, omegas_io and the
+ *                        context's gam updated; ires[0] = its status, res[0] = gam
+ *                        after it, NaN while the reference's is None); the context's
+ *                        gam starts as None (sgv_create) and is set by sgv_set_mle_gam.
  * SGV_STEP_CHAIN (sgv_step_begin only): gam1s, gamw (clamped to >= 1, :374),
  * alpha1_prev, alpha2_prev, *lam_io and omegas_io are taken, when the step
  * starts, from the results of the step queued before it -- so a step can be
@@ -219,6 +223,7 @@ int sgv_probe_draw(uint32_t* key, int32_t* pos, int64_t n, int64_t lo, int64_t h
 #define SGV_STEP_LEARN_GAMW 16
 #define SGV_STEP_METRICS 32
 #define SGV_STEP_CHAIN 64
+#define SGV_STEP_MLE 128
 int sgv_step(sgv_ctx* ctx, int it, int flags, int em_maxit, int nslab, const double* sigmas,
              const double* a, double* lam_io, double* omegas_io, const double* gam1s,
              double rho, const double* gamw, const double* alpha1_prev,
@@ -279,6 +284,34 @@ int sgv_mle_exp_max(sgv_ctx* ctx, const double* gam1s /* K */, int L, const doub
 int sgv_mle_terms(sgv_ctx* ctx, const double* a /* K */, const double* gam1s /* K */, int L,
                   const double* sigma2 /* L */, const double* omega /* L */, double exp_max,
                   double* sums /* L */);
+/* The whole MLE prior update in the library, src/sgvamp.py:162-194: x0 from
+ * lam, omegas (nslab of them) and gam (*gam_io NaN = the reference's None: x0[-1]
+ * = 1), sgv_fsolve on Lagrangian_der (:139-160, the sums from sgv_mle_terms),
+ * then the reference's acceptance tests and normalisation.  *status_out: 0 =
+ * lam_io, omegas_io, gam_io updated; SGV_MLE_NOT_CONVERGED (fsolve's ier != 1)
+ * or SGV_MLE_NEGATIVE (a non-positive mixture weight): nothing changed, the
+ * reference's "No prior update!" cases. */
+#define SGV_MLE_NOT_CONVERGED 1
+#define SGV_MLE_NEGATIVE 2
+int sgv_mle_update(sgv_ctx* ctx, const double* gam1s /* K */, const double* a /* K */, int nslab,
+                   const double* sigmas /* nslab */, double* lam_io, double* omegas_io,
+                   double* gam_io, int* status_out);
+
+/* scipy.optimize.fsolve(fcn, x0, full_output=True) with its defaults (MINPACK
+ * hybrd: xtol 1.49012e-08, maxfev 200 (n + 1), forward-difference Jacobian with
+ * epsfcn = machine epsilon, factor 100, automatic scaling), host only: fcn
+ * writes F(x) to fvec and returns 0, or a negative value to stop the solver.
+ * x_io: x0 in, the last accepted iterate out; fvec_out (may be null): F there;
+ * *nfev_out (may be null): function evaluations.  Returns MINPACK's info
+ * (1 = converged, 2-5 = the other terminations, < 0 = fcn's stop value, 0 =
+ * bad arguments) -- the reference's `ier` (src/sgvamp.py:179-181). */
+/* The MLE update's Lagrange multiplier that SGV_STEP_MLE steps use and update
+ * (the reference's self.gam, src/sgvamp.py:31,178,194; NaN = None). */
+int sgv_set_mle_gam(sgv_ctx* ctx, double gam);
+
+typedef int (*sgv_fsolve_fn)(void* user, int n, const double* x, double* fvec);
+int sgv_fsolve(int n, sgv_fsolve_fn fcn, void* user, double* x_io, double* fvec_out,
+               int* nfev_out);
 
 /* The per-iteration output vectors without a host wait (src/sgvamp.py:281,283):
  * sgv_outputs_begin queues this rank's slices of xhat1 and r1[0..K-1] (unscaled,

@@ -215,6 +215,8 @@ struct sgv_ctx {
     std::vector<double> gam1, gamw, alpha1, alpha2;   // K each (sgv_create)
     double lam, om[MAXL];
   } chain;
+  // the MLE prior update's Lagrange multiplier (src/sgvamp.py:31,194,211; NaN = None)
+  double mle_gam = std::numeric_limits<double>::quiet_NaN();
   double* d_inner = nullptr;      // K > MAXK: the denoiser's np.inner over all cohorts
   size_t inner_cap = 0;
   size_t pk_cap = 0;
@@ -1652,6 +1654,12 @@ extern "C" int sgv_reset_solver(sgv_ctx* c) {
   return SGV_OK;
 }
 
+extern "C" int sgv_set_mle_gam(sgv_ctx* c, double gam) {
+  ENTER(c);
+  c->mle_gam = gam;
+  return SGV_OK;
+}
+
 extern "C" int sgv_set_rs_recurrence(sgv_ctx* c, int on) {
   ENTER(c);
   c->rs_rec = on ? 1 : 0;
@@ -2178,6 +2186,75 @@ extern "C" int sgv_mle_terms(sgv_ctx* c, const double* a, const double* gam1s, i
     CHK(reduce_host(c, MAXL + 1, c->d_ch_begin, tot));
     for (int l = 0; l < L; ++l) sums[l] = g == 0 ? tot[l] : sums[l] + tot[l];
   }
+  return SGV_OK;
+}
+
+// The MLE prior update, src/sgvamp.py:162-194, with scipy's fsolve restated in
+// hybrd.cpp; each function evaluation is one device pass over the r1 vectors
+// (sgv_mle_terms), the rest the reference's host arithmetic in its order.
+struct MleFn {
+  sgv_ctx* c;
+  const double* gam1s;
+  const double* a;
+  int L;
+  const double* sigma2;
+  const double* omega0;
+  double exp_max;
+  int rc;
+};
+
+static int mle_lagrangian(void* user, int n, const double* x, double* y) {
+  MleFn& f = *(MleFn*)user;
+  const int L = f.L;
+  double S[MAXL + 1];
+  f.rc = sgv_mle_terms(f.c, f.a, f.gam1s, L, f.sigma2, x, f.exp_max, S);   // omega = x[:L]
+  if (f.rc != SGV_OK) return -1;
+  const double gam = x[L];
+  for (int l = 0; l < L; ++l) y[l] = (S[l] + (f.omega0[l] - 1.0) / x[l]) + gam;   // :159
+  double sw = 0.0;                                                                   // :160
+  for (int l = 0; l < L; ++l) sw += x[l];
+  y[L] = sw - 1.0;
+  (void)n;
+  return 0;
+}
+
+extern "C" int sgv_mle_update(sgv_ctx* c, const double* gam1s, const double* a, int nslab,
+                              const double* sigmas, double* lam_io, double* omegas_io,
+                              double* gam_io, int* status_out) {
+  ENTER(c);
+  if (!gam1s || !a || !sigmas || !lam_io || !omegas_io || !gam_io || !status_out ||
+      nslab < 1 || nslab > MAXL)
+    return fail(c, SGV_ERR_ARG, "sgv_mle_update: bad arguments");
+  const int L = nslab + 1;
+  double omega0[MAXL + 1], sigma2[MAXL + 1], x[MAXL + 2];
+  omega0[0] = 1 - *lam_io;                                        // :166-168
+  for (int l = 0; l < nslab; ++l) omega0[1 + l] = *lam_io * omegas_io[l];
+  sigma2[0] = 1e-16;                                              // :169-171
+  for (int l = 0; l < nslab; ++l) sigma2[1 + l] = sigmas[l];
+  for (int l = 0; l < L; ++l) x[l] = omega0[l];                   // :173-178
+  x[L] = std::isnan(*gam_io) ? 1.0 : *gam_io;
+  MleFn f{c, gam1s, a, L, sigma2, omega0, 0.0, SGV_OK};
+  CHK(sgv_mle_exp_max(c, gam1s, L, sigma2, &f.exp_max));           // :152, once per update
+  const int ier = sgv_fsolve(L + 1, mle_lagrangian, &f, x, nullptr, nullptr);   // :179
+  if (f.rc != SGV_OK) return f.rc;
+  if (ier != 1) {                                                 // :181-184
+    *status_out = SGV_MLE_NOT_CONVERGED;
+    return SGV_OK;
+  }
+  for (int l = 0; l < L; ++l)
+    if (x[l] <= 0) {                                              // :185-188
+      *status_out = SGV_MLE_NEGATIVE;
+      return SGV_OK;
+    }
+  double sw = 0.0;                                                // :190 x[:-1] /= sum(x[:-1])
+  for (int l = 0; l < L; ++l) sw += x[l];
+  for (int l = 0; l < L; ++l) x[l] = x[l] / sw;
+  *lam_io = 1 - x[0];                                             // :191
+  double ss = 0.0;                                                // :192 w / sum(x[1:-1])
+  for (int l = 1; l < L; ++l) ss += x[l];
+  for (int l = 0; l < nslab; ++l) omegas_io[l] = x[1 + l] / ss;
+  *gam_io = x[L];                                                 // :193
+  *status_out = 0;
   return SGV_OK;
 }
 
@@ -2711,6 +2788,9 @@ static int step_impl(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
   c->pref_src = probes;
   if (flags & SGV_STEP_EM) {   // :250-257
     CHK(sgv_em(c, gam1s, a, nslab, sigmas, em_maxit, lam_io, omegas_io, &ires[0], &res[0]));
+  } else if (flags & SGV_STEP_MLE) {   // :244-247
+    CHK(sgv_mle_update(c, gam1s, a, nslab, sigmas, lam_io, omegas_io, &c->mle_gam, &ires[0]));
+    res[0] = c->mle_gam;
   }
   if (nslab < 1 || nslab > MAXL) return fail(c, SGV_ERR_ARG, "sgv_step: nslab=%d", nslab);
   // denoiser (:270-291); the output copies and metrics (:281-283, 379-387) are

@@ -208,6 +208,24 @@ class Engine:
                                hb.dptr(hb.f64(omega)), float(exp_max), hb.dptr(out))
         return out
 
+    def set_mle_gam(self, gam):
+        """The Lagrange multiplier SGV_STEP_MLE steps start from (None = the reference's)."""
+        self.ctx.sgv_set_mle_gam(float("nan") if gam is None else float(gam))
+
+    def mle_update(self, gam1s, a, sigmas, lam, omegas, gam):
+        """The whole MLE prior update in the library (sgv_mle_update,
+        src/sgvamp.py:162-194): returns (status, lam, omegas, gam); status 0 =
+        updated, hb.MLE_NOT_CONVERGED / hb.MLE_NEGATIVE = the reference's "No prior
+        update!" cases (inputs returned unchanged).  gam None = the reference's."""
+        sg = hb.f64(sigmas)
+        lam_io = np.array([lam], dtype=np.float64)
+        om = np.array(omegas, dtype=np.float64).copy()
+        g = np.array([np.nan if gam is None else gam], dtype=np.float64)
+        st = np.zeros(1, dtype=np.int32)
+        self.ctx.sgv_mle_update(hb.dptr(hb.f64(gam1s)), hb.dptr(hb.f64(a)), len(sg), hb.dptr(sg),
+                                hb.dptr(lam_io), hb.dptr(om), hb.dptr(g), hb.iptr(st))
+        return int(st[0]), float(lam_io[0]), om, (None if np.isnan(g[0]) else float(g[0]))
+
     def lmmse(self, it, gamw, gam2, alpha1, alpha2_prev, probes_local, cg_maxit, lmmse_damp, rho,
               learn_gamw, rtol=1e-5):
         K = self.K
@@ -254,7 +272,9 @@ class Engine:
         self.ctx.sgv_step_end()
         K = self.K
         return dict(lam=float(h["lam"][0]), omegas=h["om"], em_steps=int(h["ires"][0]),
-                    em_err=float(h["res"][0]), alpha1=h["res"][1:1 + K].tolist(),
+                    em_err=float(h["res"][0]), mle_status=int(h["ires"][0]),
+                    mle_gam=(None if np.isnan(h["res"][0]) else float(h["res"][0])),
+                    alpha1=h["res"][1:1 + K].tolist(),
                     gam2=h["res"][1 + K:1 + 2 * K].tolist(), metrics=h["res"][1 + 2 * K:],
                     out=h["out"], cg=h["cg"], passes=int(h["ires"][1]))
 

@@ -17,7 +17,8 @@ VEC_R, VEC_R1, VEC_XHAT1, VEC_XHAT2, VEC_SIG2U, VEC_X0 = range(6)
 LMMSE_NOUT = 8
 O_TRSIGMA2, O_ALPHA2, O_GAM1, O_Z, O_TRRSIGMA2, O_GAMW, O_XR, O_XRX = range(8)
 STEP_EM, STEP_DENOISE_DAMP, STEP_ALPHA1_DAMP, STEP_LMMSE_DAMP, STEP_LEARN_GAMW, STEP_METRICS, \
-    STEP_CHAIN = 1, 2, 4, 8, 16, 32, 64
+    STEP_CHAIN, STEP_MLE = 1, 2, 4, 8, 16, 32, 64, 128
+MLE_NOT_CONVERGED, MLE_NEGATIVE = 1, 2
 OUT_SLOTS = 3
 MAX_COHORTS = 1024
 MAX_SLABS = 8
@@ -47,6 +48,10 @@ _SIGS = {
     "sgv_mle_exp_max": [_vp, _c_dbl_p, ctypes.c_int, _c_dbl_p, _c_dbl_p],
     "sgv_mle_terms": [_vp, _c_dbl_p, _c_dbl_p, ctypes.c_int, _c_dbl_p, _c_dbl_p, ctypes.c_double,
                       _c_dbl_p],
+    "sgv_mle_update": [_vp, _c_dbl_p, _c_dbl_p, ctypes.c_int, _c_dbl_p, _c_dbl_p, _c_dbl_p,
+                       _c_dbl_p, _c_int_p],
+    "sgv_fsolve": [ctypes.c_int, ctypes.c_void_p, _vp, _c_dbl_p, _c_dbl_p, _c_int_p],
+    "sgv_set_mle_gam": [_vp, ctypes.c_double],
     "sgv_set_ld_block": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, ctypes.c_int64],
     "sgv_get_ld_block": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, ctypes.c_int64],
     "sgv_set_ld_block_csr": [_vp, ctypes.c_int, ctypes.c_int, _c_i64_p, _c_i64_p, _c_dbl_p],
@@ -129,6 +134,36 @@ def load(path=LIB_PATH):
         fn.restype = _RESTYPES.get(name, ctypes.c_int)
     _lib = lib
     return lib
+
+
+FSOLVE_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.c_int, _c_dbl_p, _c_dbl_p)
+
+
+def fsolve(func, x0):
+    """sgv_fsolve (the library's scipy.optimize.fsolve, MINPACK hybrd with
+    fsolve's defaults) on a Python function: returns (x, info, nfev).  For the
+    tests; the product path calls it from C (sgv_mle_update)."""
+    lib = load()
+    x = np.array(x0, dtype=np.float64)
+    n = x.size
+    err = []
+
+    def cb(_user, nn, xp, fp):
+        try:
+            xv = np.ctypeslib.as_array(xp, shape=(nn,)).copy()
+            fp_arr = np.ctypeslib.as_array(fp, shape=(nn,))
+            fp_arr[:] = np.asarray(func(xv), dtype=np.float64)
+            return 0
+        except Exception as e:  # noqa: BLE001 -- reported after the solver returns
+            err.append(e)
+            return -1
+
+    cfn = FSOLVE_FN(cb)
+    nfev = np.zeros(1, dtype=np.int32)
+    info = lib.sgv_fsolve(int(n), ctypes.cast(cfn, ctypes.c_void_p), None, dptr(x), None, iptr(nfev))
+    if err:
+        raise err[0]
+    return x, int(info), int(nfev[0])
 
 
 def dptr(a):

@@ -499,18 +499,14 @@ class VAMP:
         """Change the iteration horizon (see begin); call between steps."""
         self._n_iter = iterations
 
-    def _flags(self, it, gam1s, rec):
-        """sgv_step flags of iteration it; runs the MLE prior update (host fsolve on
-        device sums, src/sgvamp.py:244-247) when it is due."""
+    def _flags(self, it):
+        """sgv_step flags of iteration it (the prior update, EM or MLE, runs inside
+        the step: src/sgvamp.py:242-259)."""
         st = self._st
         flags = 0
         if it >= st["update_prior_from"]:                             # :242-259
             if st["prior_update"] == "mle":
-                if self.rank == 0:
-                    logging.info("...Updating prior parameters using MLE")
-                warn = self.prior_update_mle(gam1s)
-                if warn:
-                    rec["mle_warning"] = warn
+                flags |= hb.STEP_MLE
             elif st["prior_update"] == "em":
                 flags |= hb.STEP_EM
         if it > 0:
@@ -557,7 +553,6 @@ class VAMP:
         st = self._st
         return (self._n_iter is not None and nxt < self._n_iter
                 and not (st["return_xhat"] and not self.write_files)
-                and not (st["prior_update"] == "mle" and nxt >= st["update_prior_from"])
                 and hb.ab_env("SGV_STEP") != "nochain")
 
     def _begin_step(self, it, flags, u, chain):
@@ -600,7 +595,9 @@ class VAMP:
             h, flags = q["h"], q["flags"]
             rec.update(q["rec"])
         else:
-            flags = self._flags(it, gam1s, rec)
+            flags = self._flags(it)
+            if flags & hb.STEP_MLE:
+                eng.set_mle_gam(self.gam)   # the step chain carries it on from here
             u = self._take_probes(rec)
             if self.write_files:
                 self._flush_until(it - hb.OUT_SLOTS, rec)
@@ -610,7 +607,7 @@ class VAMP:
         self._submit_csv()            # previous iterations' rows
         if self._can_chain(it + 1):
             rec1 = {}
-            flags1 = self._flags(it + 1, None, rec1)
+            flags1 = self._flags(it + 1)
             u1 = self._take_probes(rec1)
             if self.write_files:
                 self._flush_until(it + 1 - hb.OUT_SLOTS, rec1)
@@ -638,6 +635,12 @@ class VAMP:
                 logging.info("...Updating prior parameters using EM")
                 logging.info("... prior-learning EM algorithm performed %s steps "
                              "and had final relative error = %0.9f", r["em_steps"], r["em_err"])
+        elif flags & hb.STEP_MLE:                                     # :244-247
+            if rank == 0:
+                logging.info("...Updating prior parameters using MLE")
+            warn = self._mle_result(r["mle_status"], r["lam"], r["omegas"], r["mle_gam"])
+            if warn:
+                rec["mle_warning"] = warn
         if rank == 0:
             logging.debug("lam=%s", self.lam)
             logging.debug("omegas=%s", self.omegas)
@@ -812,50 +815,24 @@ class VAMP:
         self.history.append(rec)
         return rec
 
-    def Lagrangian_der(self, x, omega0, sigma2, gam1s, exp_max):
-        """src/sgvamp.py:139-160.  The K x M x L marker sums run on the device over
-        the current r1 vectors (sgv_mle_terms); the rest is the reference's host
-        arithmetic.  exp_max (:152) depends only on r1, gam1s and sigma2 and is
-        computed once per update."""
-        L = self.L
-        y = np.zeros(L + 1)
-        omega = x[:L]
-        gam = x[L]
-        S = self.engine.mle_terms(self.a, gam1s, sigma2, omega, exp_max)
-        y[:L] = S + (omega0 - 1) / omega + gam
-        y[L] = sum(omega) - 1.0
-        return y
+    MLE_WARNINGS = {hb.MLE_NOT_CONVERGED: "WARNING: fsolve not converged. No prior update!",
+                    hb.MLE_NEGATIVE: "WARNING: Negative values in MLE. No prior update!"}
+
+    def _mle_result(self, status, lam, omegas, gam):
+        """Take an MLE prior update's outcome (src/sgvamp.py:180-194): the new
+        lam/omegas/gam, or the reference's warning and no update."""
+        if status:
+            msg = self.MLE_WARNINGS[status]
+            if self.rank == 0:
+                logging.info(msg)
+            return msg
+        self.lam, self.omegas, self.gam = lam, np.array(omegas), gam
+        return None
 
     def prior_update_mle(self, gam1s):
-        """src/sgvamp.py:162-194: scipy's fsolve (MINPACK hybrd) on the host, as
-        the reference calls it, on the device-side Lagrangian."""
-        from scipy import optimize
-
-        omega0 = np.zeros(self.L)
-        omega0[0] = 1 - self.lam
-        omega0[1:] = self.lam * self.omegas
-        sigma2 = np.zeros(self.L)
-        sigma2[0] = 1e-16
-        sigma2[1:] = self.sigmas
-        x0 = np.zeros(self.L + 1)
-        x0[:-1] = omega0
-        if self.gam is None:
-            x0[-1] = 1
-        else:
-            x0[-1] = self.gam
-        exp_max = self.engine.mle_exp_max(gam1s, sigma2)
-        x, _, ier, _ = optimize.fsolve(func=self.Lagrangian_der, x0=x0,
-                                       args=(omega0, sigma2, gam1s, exp_max), full_output=True)
-        if ier != 1:
-            if self.rank == 0:
-                logging.info("WARNING: fsolve not converged. No prior update!")
-            return "WARNING: fsolve not converged. No prior update!"
-        elif any(s <= 0 for s in x[:-1]):
-            if self.rank == 0:
-                logging.info("WARNING: Negative values in MLE. No prior update!")
-            return "WARNING: Negative values in MLE. No prior update!"
-        x[:-1] /= sum(x[:-1])
-        self.lam = 1 - x[0]
-        self.omegas = np.array([w / sum(x[1:-1]) for w in x[1:-1]])
-        self.gam = x[self.L]
-        return None
+        """src/sgvamp.py:162-194 in one library call (sgv_mle_update): scipy's
+        fsolve (MINPACK hybrd, restated in csrc/hybrd.cpp) on Lagrangian_der
+        (:139-160), whose K x M x L marker sums run on the device."""
+        status, lam, omegas, gam = self.engine.mle_update(gam1s, self.a, self.sigmas, self.lam,
+                                                          self.omegas, self.gam)
+        return self._mle_result(status, lam, omegas, gam)

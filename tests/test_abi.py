@@ -55,8 +55,11 @@ def test_binding_constants_match_header():
         pairs["SGV_VEC_" + n] = getattr(hb, "VEC_" + n)
     for n in ("TRSIGMA2", "ALPHA2", "GAM1", "Z", "TRRSIGMA2", "GAMW", "XR", "XRX"):
         pairs["SGV_O_" + n] = getattr(hb, "O_" + n)
-    for n in ("EM", "DENOISE_DAMP", "ALPHA1_DAMP", "LMMSE_DAMP", "LEARN_GAMW", "METRICS", "CHAIN"):
+    for n in ("EM", "DENOISE_DAMP", "ALPHA1_DAMP", "LMMSE_DAMP", "LEARN_GAMW", "METRICS", "CHAIN",
+              "MLE"):
         pairs["SGV_STEP_" + n] = getattr(hb, "STEP_" + n)
+    for n in ("NOT_CONVERGED", "NEGATIVE"):
+        pairs["SGV_MLE_" + n] = getattr(hb, "MLE_" + n)
     for name, value in pairs.items():
         assert defs[name] == value, (name, defs[name], value)
 

@@ -429,12 +429,13 @@ def test_cg_exact_columns_vs_lookahead(name, tmp_path, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["k1_defaults", "k1_L3", "k2_shared", "k4_shared_s_damp",
-                                  "k2_mle_L3", "k1_blocks_csr_s_damp"])
+                                  "k1_mle", "k2_mle_L3", "k1_blocks_csr_s_damp"])
 def test_step_driver_matches_phases(name, tmp_path, monkeypatch):
     """VAMP.step through sgv_step on the library's worker thread -- chained (the
     next step queued behind the running one, its scalars taken from it on the
-    device side) and unchained -- against one host call per phase
-    (SGV_STEP=phases): every output file byte-identical, same CG/EM counts."""
+    device side; MLE prior updates too, inside the step: SGV_STEP_MLE) and
+    unchained -- against one host call per phase (SGV_STEP=phases): every output
+    file byte-identical, same CG/EM counts and MLE outcomes."""
     c = Case(name)
     res = {}
     monkeypatch.setenv("SGV_AB", "1")
@@ -445,7 +446,8 @@ def test_step_driver_matches_phases(name, tmp_path, monkeypatch):
         v, xh = run_vamp_case(c, d)
         files = sorted(p.name for p in d.iterdir())
         res[mode] = ({f: (d / f).read_bytes() for f in files},
-                     [(h["cg_iters"], h["cg_info"], h.get("em_steps")) for h in v.history],
+                     [(h["cg_iters"], h["cg_info"], h.get("em_steps"), h.get("mle_warning"))
+                      for h in v.history],
                      [np.asarray(x) for x in xh])
         v.engine.close()
     ref = res["phases"]
@@ -907,10 +909,57 @@ def test_c5_shape_divergence_matches_oracle(tmp_path):
     eng.close()
 
 
+@pytest.mark.parametrize("K,nslab,gam", [(1, 1, None), (3, 2, 0.7), (12, 3, None), (40, 2, 1.3)])
+def test_mle_update_matches_scipy_on_device_sums(K, nslab, gam):
+    """sgv_mle_update (the whole MLE prior update in the library) against
+    scipy.optimize.fsolve driven from Python on the same device sums
+    (sgv_mle_exp_max / sgv_mle_terms), as the reference drives it
+    (src/sgvamp.py:162-194): bitwise the same prior, the same outcome."""
+    from scipy import optimize
+
+    sizes = [700, 300]
+    M = sum(sizes)
+    rs = np.random.RandomState(K * 7 + nslab)
+    eng = Engine(sizes, K=K)
+    lam = 0.2
+    for k in range(K):
+        z = rs.rand(M) < lam
+        eng.set_vector(hb.VEC_R1, k, np.where(z, rs.normal(0, 1.5, M), 0.0) + rs.normal(0, .4, M))
+    gam1s = rs.uniform(3.0, 8.0, K)
+    a = np.full(K, 1.0 / K)
+    sig = np.sort(rs.uniform(0.5, 3.0, nslab))
+    omegas = rs.dirichlet(np.ones(nslab))
+    L = nslab + 1
+    omega0 = np.concatenate([[1 - lam], lam * omegas])
+    sigma2 = np.concatenate([[1e-16], sig])
+    exp_max = eng.mle_exp_max(gam1s, sigma2)
+
+    def lagrangian(x):                                  # src/sgvamp.py:139-160
+        y = np.zeros(L + 1)
+        y[:L] = eng.mle_terms(a, gam1s, sigma2, x[:L], exp_max) + (omega0 - 1) / x[:L] + x[L]
+        y[L] = sum(x[:L]) - 1.0
+        return y
+
+    x0 = np.concatenate([omega0, [1.0 if gam is None else gam]])
+    x, _, ier, _ = optimize.fsolve(lagrangian, x0, full_output=True)
+    status, lam2, om2, gam2 = eng.mle_update(gam1s, a, sig, lam, omegas, gam)
+    if ier != 1:
+        assert status == hb.MLE_NOT_CONVERGED
+    elif any(v <= 0 for v in x[:-1]):
+        assert status == hb.MLE_NEGATIVE
+    else:
+        assert status == 0
+        x[:-1] /= sum(x[:-1])                           # :190-193
+        assert lam2 == 1 - x[0]
+        np.testing.assert_array_equal(om2, [w / sum(x[1:-1]) for w in x[1:-1]])
+        assert gam2 == x[L]
+    eng.close()
+
+
 def test_mle_prior_many_cohorts_vs_oracle(tmp_path):
     """--prior-update mle (src/sgvamp.py:139-194) with K = 10 cohorts (more than
-    one LMMSE group; the MLE sums over all cohorts on the device, fsolve on the
-    host) against the oracle on the same device-generated inputs."""
+    one LMMSE group; the MLE sums over all cohorts on the device, fsolve in the
+    library) against the oracle on the same device-generated inputs."""
     sizes = [600, 500]
     nsamp, K = 700, 10
     M = sum(sizes)
