@@ -27,9 +27,13 @@ def main():
     ap.add_argument("--ncols", default="4,8")
     ap.add_argument("--nsamp", type=int, default=2000)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--lib", default=None, help="A/B of builds: load this libsgvamp_hip.so")
     ap.add_argument("--rhs", default="normal", choices=["normal", "zero", "ones"],
                     help="right-hand sides (zero/ones: the pass's data-dependent power, not its products)")
     a = ap.parse_args()
+    if a.lib:
+        import hip_backend
+        hip_backend.load(a.lib)
     for shape in a.shapes.split(","):
         nb, n = (int(x) for x in shape.split("x"))
         sizes = [n] * nb
