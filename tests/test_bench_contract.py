@@ -39,7 +39,8 @@ def test_traffic_none_for_unprofiled_workload():
     assert bench.read_traffic("k_sym_pass", 2.0e11, 1, 200000) == (None, None)
     assert bench.read_traffic("k_no_such_kernel", 20210140245.0, 1, 200000) == (None, None)
     # C5 and the north star store the same LD (bytes within 0.2 %): K tells them apart
-    assert bench.read_traffic("k_sym_mfma", 63779430912.0, 8, 1000000)[1] == "pmc_sym_mfma_r01s6_c5.json"
+    src = bench.read_traffic("k_sym_mfma", 63779430912.0, 8, 1000000)[1]
+    assert src.startswith("pmc_sym_mfma_") and src.endswith("_c5.json"), src
     src = bench.read_traffic("k_sym_mfma", 63651430912.0, 4, 1000000)[1]
     assert src.startswith("pmc_sym_mfma_") and src.endswith("_northstar.json"), src
 
