@@ -116,8 +116,9 @@ def ab_env(name):
     return v
 
 
-def load(path=LIB_PATH):
-    """Load and type the library (cached).  Raises if it is absent."""
+def load(path=LIB_PATH, strict=True):
+    """Load and type the library (cached).  Raises if it is absent.  strict=False
+    (A/B tools loading an older build): symbols the build lacks are left untyped."""
     global _lib
     if _lib is not None:
         return _lib
@@ -127,6 +128,8 @@ def load(path=LIB_PATH):
     lib = ctypes.CDLL(path)
     for name, args in _SIGS.items():
         if not hasattr(lib, name):
+            if not strict:
+                continue
             raise HipError("%s does not export %s: stale build -- rebuild with "
                            "`make -C sgvamp-py_amd/csrc`" % (path, name))
         fn = getattr(lib, name)

@@ -33,7 +33,7 @@ def main():
     a = ap.parse_args()
     if a.lib:
         import hip_backend
-        hip_backend.load(a.lib)
+        hip_backend.load(a.lib, strict=False)
     for shape in a.shapes.split(","):
         nb, n = (int(x) for x in shape.split("x"))
         sizes = [n] * nb
