@@ -162,14 +162,16 @@ def test_sharded_bench_equals_one_rank(name, flags, tmp_path):
 @pytest.mark.skipif(os.environ.get("SGV_FULL_GATE") != "1",
                     reason="~10 min of host oracle: run with SGV_FULL_GATE=1 "
                            "(profiles/r03/northstar_50it_gate.log)")
-def test_north_star_50_iterations_vs_oracle(tmp_path):
+@pytest.mark.parametrize("K", [4, 1])
+def test_north_star_50_iterations_vs_oracle(K, tmp_path):
     """The north star's own gate at its own size: M = 1e6 in 64 blocks of 15,625,
-    K = 4 cohorts sharing one LD (the f64 MFMA pass), the bench's problem and
-    flags, 50 outer iterations of the HIP path against the CPU oracle on the same
-    inputs read back from the device.  Bar (BASELINE.json north_star): xhat within
-    1e-5 relative after 50 iterations; asserted at every iteration, with the CG
-    iteration counts and EM steps compared per iteration."""
-    K, its = 4, 50
+    K = 4 cohorts sharing one LD (the f64 MFMA pass; K = 1: C4, the VALU pass),
+    the bench's problem and flags, 50 outer iterations of the HIP path against
+    the CPU oracle on the same inputs read back from the device.  Bar
+    (BASELINE.json north_star): xhat within 1e-5 relative after 50 iterations;
+    asserted at every iteration, with the CG iteration counts and EM steps
+    compared per iteration."""
+    its = 50
     sizes = [15625] * 64
     eng = Engine(sizes, K=K, ld_of=[0] * K)
     args = argparse.Namespace(seed=SEED, nsamp=NSAMP)
@@ -189,7 +191,7 @@ def test_north_star_50_iterations_vs_oracle(tmp_path):
     xh = v.infer(None, None, its, x0=x0, **run)
     hist = [(h["cg_iters"], h.get("em_steps")) for h in v.history]
     eng.close()
-    _log("north star: GPU 50 iterations done")
+    _log("K=%d: GPU 50 iterations done" % K)
     t = vo.infer([L], [0] * K, r_list, [N] * K, its, rho=0.5, gamw=5.0, gam1=1e-6, x0=x0,
                  seed=SEED, reducer=vo.Reducer("blocked", bounds=L.bounds), rs_recurrence=True,
                  batched=True, **prior, **run)
@@ -202,8 +204,8 @@ def test_north_star_50_iterations_vs_oracle(tmp_path):
     same_cg = sum(list(map(list, h[0])) == list(map(list, x))
                   for h, x in zip(hist, t["cg_iters"]))
     same_em = sum(a == b for a, b in zip([h[1] for h in hist][1:], t["em_steps"]))
-    _log("north star 50 it: max rel xhat err per iteration", ["%.2e" % e for e in errs])
-    _log("north star 50 it: CG counts equal in %d/%d iterations, EM steps in %d/%d"
-         % (same_cg, its, same_em, its - 1))
-    _log("north star 50 it: CG counts", [h[0] for h in hist])
+    _log("K=%d 50 it: max rel xhat err per iteration" % K, ["%.2e" % e for e in errs])
+    _log("K=%d 50 it: CG counts equal in %d/%d iterations, EM steps in %d/%d"
+         % (K, same_cg, its, same_em, its - 1))
+    _log("K=%d 50 it: CG counts" % K, [h[0] for h in hist])
     assert max(errs) < 1e-5, max(errs)
