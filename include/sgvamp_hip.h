@@ -112,8 +112,8 @@ int sgv_set_ld_block(sgv_ctx* ctx, int ld, int blk_local, const double* rowmajor
  * summed).  Replaces the sparse loaders src/main.py:199-200 (.npz CSR of any
  * sparsity) and :251-257 (PLINK .ld pairs assembled into CSR): a block whose
  * entries lie within j - i <= bw is stored as a packed BAND -- panel g (rows
- * 256g ..) keeps columns 256g .. 256g + round_up(256 + bw, 512) - 1 -- so
- * windowed LD over a whole chromosome needs n * (bw + 256..767) doubles instead
+ * 256g ..) keeps columns 256g .. 256g + round_up(256 + bw, 256) - 1 -- so
+ * windowed LD over a whole chromosome needs n * (bw + 256..511) doubles instead
  * of n^2 / 2.  Blocks whose band is as wide as the triangle are stored as the
  * packed triangle.  Never allocates n x n on the host. */
 int sgv_set_ld_block_csr(sgv_ctx* ctx, int ld, int blk_local, const int64_t* indptr /* n+1 */,

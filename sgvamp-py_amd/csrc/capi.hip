@@ -62,6 +62,7 @@ struct LdPlan {
   SymItem* d_sitems = nullptr;
   SymPanel* d_spanels = nullptr;
   int nstrips = 0;
+  bool ragged = false;         // some strip item is narrower than its strip (band blocks)
   double stored_bytes = 0.0, dense_bytes = 0.0;
 };
 
@@ -669,16 +670,16 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
       for (int64_t c0 = (int64_t)SYM_H * p; c0 < n; c0 += 2 * SYM_H) {
         const int G = (int)(c0 / SYM_H);
         const int sb = (int)strips.size();
-        // a band block's panel g reaches c0 iff c0 - 256 g < ext (ext a multiple
-        // of 512: the panels G - ext/256 + 2, ..., G of this parity)
+        // a band block's panel g reaches c0 iff c0 - 256 g < ext (ext = e
+        // panels: the panels G - 2 floor((e - 1) / 2), ..., G of this parity)
         const int64_t ext = c->ldb[ld][b].ext;
-        const int glo = ext > 0 ? std::max(p, G - (int)(ext / SYM_H) + 2) : p;
+        const int glo = ext > 0 ? std::max(p, G - 2 * (((int)(ext / SYM_H) - 1) / 2)) : p;
         for (int g0 = glo; g0 <= G; g0 += 2 * S) {
           SymStrip st;
           st.it0 = (int)sitems.size();
           st.npan = 0;
           st.slot = (int)strips.size();
-          st.pad_ = 0;
+          st.ncmax = 0;
           for (int g = g0; g <= G && g < g0 + 2 * S; g += 2) {
             const SymPanel& pn = panels[bp0 + g];
             const int idx = pn.item_begin + (int)((c0 - (int64_t)SYM_H * g) / (2 * SYM_H));
@@ -686,6 +687,7 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
               return fail(c, SGV_ERR_STATE, "strip plan: item (%d, %lld) missing", g,
                           (long long)c0);
             sitems.push_back(items[idx]);
+            st.ncmax = std::max(st.ncmax, items[idx].nc);
             ++st.npan;
           }
           strips.push_back(st);
@@ -710,6 +712,9 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
       return wa > wb;
     });
   pl->nstrips = (int)strips.size();
+  pl->ragged = false;
+  for (const SymStrip& st : strips)
+    for (int i = 0; i < st.npan; ++i) pl->ragged |= sitems[st.it0 + i].nc < st.ncmax;
   CHK(upload_table(c, strips, &pl->d_strips));
   CHK(upload_table(c, sitems, &pl->d_sitems));
   CHK(upload_table(c, sp, &pl->d_spanels));
@@ -839,7 +844,7 @@ static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa) {
     const int cls = mf ? 1 : sym_class(nc);
     if (mf) {
       HIPCHK(launch_sym_mfma(nc, pl.d_strips, pl.nstrips, pl.d_sitems, pa, c->Mpad, c->d_pk,
-                             c->d_rowpart, c->d_colpart, c->st));
+                             c->d_rowpart, c->d_colpart, pl.ragged, c->st));
       HIPCHK(launch_sym_finalize_strip(nc, pl.d_spanels, pl.npanels, pa, c->d_rowpart,
                                        c->d_colpart, c->d_part, c->st));
       c->aux_bytes += 2.0 * 8.0 * nc * ((double)pl.nitems[cls] * SYM_H + (double)pl.nstrips * 512);

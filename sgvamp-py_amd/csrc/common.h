@@ -73,10 +73,11 @@ struct RowGroup {
 
 // ---- packed symmetric LD blocks (sym_pass.hip) ----------------------------
 constexpr int SYM_H = 256;   // rows per panel
-// packed band blocks: a panel's stored column extent is a multiple of BAND_Q, so
-// every item of an MFMA strip (512-column chunk) covers the same columns and the
-// earlier panels covering a panel's rows are a contiguous range
-constexpr int BAND_Q = 512;
+// packed band blocks: a panel's stored column extent is a multiple of BAND_Q (a
+// whole number of panels), so the earlier panels covering a panel's rows are a
+// contiguous range; an MFMA strip's items may stop 256 columns short of the
+// strip's widest (SymStrip::ncmax: the kernels read zeros there)
+constexpr int BAND_Q = 256;
 // one (panel, column chunk) work item of k_sym_pass
 struct SymItem {
   const double* P;   // panel base: element (r0, r0)
@@ -106,9 +107,10 @@ struct SymPanel {
 // MFMA pass work item: one 512-column chunk (block-relative c0, shared by all
 // its panels) over npan panels of one parity, g0, g0 + 2, ... (increasing);
 // their (panel, chunk) items are sitems[it0 .. it0 + npan), column sums go to
-// colpart slot `slot`
+// colpart slot `slot`; ncmax = the widest item's columns (a band's first item
+// can be narrower than the others)
 struct SymStrip {
-  int32_t it0, npan, slot, pad_;
+  int32_t it0, npan, slot, ncmax;
 };
 
 // element (i, j) of a packed block is stored iff j >= 256 * floor(i / 256)
@@ -302,7 +304,7 @@ hipError_t launch_sym_pass(int nc, int cls, const SymItem* d_items, int nitems,
                            const PassArgs& pa, double* rowpart, double* colpart, hipStream_t st);
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                            const PassArgs& pa, int64_t mpad, double* d_pk, double* rowpart,
-                           double* colpart, hipStream_t st);
+                           double* colpart, bool ragged, hipStream_t st);
 hipError_t launch_sym_finalize_strip(int nc, const SymPanel* d_panels, int npanels,
                                      const PassArgs& pa, const double* rowpart,
                                      const double* colpart, double* partials, hipStream_t st);

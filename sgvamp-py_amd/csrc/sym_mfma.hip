@@ -87,7 +87,7 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // per panel when the item's row partials are written -- the same additions as
 // the per-row-group exchange through red[] (PW = false), with one barrier pair
 // per panel instead of a barrier per 16-row group.
-template <int NG, int NW, int PD, bool PW, bool SKIP>
+template <int NG, int NW, int PD, bool PW, bool SKIP, bool RAG = false>
 __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
                                                          const SymItem* __restrict__ sitems,
                                                          const double* __restrict__ pk, int ncol,
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   const int lo = lane & 15, hi = lane >> 4, bq = (lane >> 2) & 3, n4 = lane & 3;
   const int pc = hi + 4 * bq;                          // this lane's column pair in a fragment
   SymItem cur = sitems[sp.it0];
-  const int c0 = cur.c0, ncc = cur.nc;                 // the strip's chunk
+  const int c0 = cur.c0, ncc = sp.ncmax;               // the strip's chunk, widest item
   const int PKS = pks;             // Pk row stride (k_pack): 4 NG, or 16 (A/B)
   const double* pkb = pk + (int64_t)cur.voff * PKS;   // Pk of this block (block-relative index)
   const int cw0 = wid * WC;                            // first chunk column of this wave
@@ -162,14 +162,14 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   // row group the caller passes the cache-resident Pk with stride 0 (a dummy
   // fetch: the load count is the same on every path, so the compiler never
   // drains vmcnt(0) at a branch join or the row-group loop head).
-  auto load_cf = [&](uint64_t b0, int64_t ws, int H, int g, int t, d2* cf) {
+  auto load_cf = [&](uint64_t b0, int64_t ws, int H, int nci, int g, int t, d2* cf) {
     asm volatile("" : "+s"(b0));
     const int xc = cw0 + 32 * t + 2 * lo;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int rB = 16 * g + 4 * a + hi;
       const double* row = (const double*)b0 + (int64_t)(rB < H ? rB : H - 1) * ws;
-      cf[a] = ldg_nt((const d2*)(row + (xc < ncc ? xc : 0)));
+      cf[a] = ldg_nt((const d2*)(row + (xc < (RAG ? nci : ncc) ? xc : 0)));
     }
   };
   // column-part B operands of row group g of a panel (first row r0): P at its
@@ -186,13 +186,23 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
     }
   };
   auto pbase = [&](const SymItem& x) { return (uint64_t)(x.P + (x.c0 - x.r0)); };
+  // a band panel's item narrower than the strip: its columns past nci (never
+  // loaded: the loads above took column 0) read as zero
+  auto band_zero = [&](int nci, int t, d2* cf) {
+    const int xc = cw0 + 32 * t + 2 * lo;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      cf[a].x = xc < nci ? cf[a].x : 0.0;
+      cf[a].y = xc + 1 < nci ? cf[a].y : 0.0;
+    }
+  };
 
   uint64_t curb = pbase(cur);
   // ring of PD steps in flight per wave
   d2 cfq[PD][4];
   double bcn[4][NG];
 #pragma unroll
-  for (int p = 0; p < PD; ++p) load_cf(curb, cur.w, cur.H, 0, p, cfq[p]);
+  for (int p = 0; p < PD; ++p) load_cf(curb, cur.w, cur.H, cur.nc, 0, p, cfq[p]);
   load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
 
   int gg = 0;                                          // row groups done (LDS buffer parity)
@@ -209,6 +219,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
       const uint64_t gb = same ? curb : nxb;
       const int64_t gw = same ? cur.w : (more ? nx.w : 0);
       const int gH = same ? cur.H : (more ? nx.H : 1);
+      const int gnc = same ? cur.nc : nx.nc;
       const int gn = same ? g + 1 : 0;
       const int gr0 = same ? cur.r0 : nx.r0;
       const bool gz = dhalf && gr0 == c0;
@@ -231,12 +242,13 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
         for (int a = 0; a < 4; ++a) cf[a] = cfq[slot][a];
         // step + PD goes out here, ahead of this step's LDS and MFMA work
         if (t + PD < NT) {
-          load_cf(curb, cur.w, cur.H, g, t + PD, cfq[slot]);
+          load_cf(curb, cur.w, cur.H, cur.nc, g, t + PD, cfq[slot]);
         } else {
-          load_cf(gb, gw, gH, gn, t + PD - NT, cfq[slot]);
+          load_cf(gb, gw, gH, gnc, gn, t + PD - NT, cfq[slot]);
           if (t + PD == NT) load_bcol(gr0, gH, gz, gn, bcn);
         }
         if (t >= nta) continue;                        // wave-uniform: past the chunk
+        if (RAG && cur.nc < ncc) band_zero(cur.nc, t, cf);   // uniform: a band item's stored end
         lds_order();                                   // previous step's tile reads issued
 #pragma unroll
         for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[a];
@@ -373,7 +385,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int MF_WC = MF_CW / 4;
 constexpr int MF_NT = MF_WC / 32;
 
-template <bool SKIP>
+template <bool SKIP, bool RAG = false>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -389,7 +401,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   const int lo = lane & 15, hi = lane >> 4;
   SymItem cur = sitems[sp.it0];
-  const int c0 = cur.c0, ncc = cur.nc;
+  const int c0 = cur.c0, ncc = sp.ncmax;
   const double* pkb = pk + (int64_t)cur.voff * 16;    // Pk of this block (block-relative index)
   const int cw0 = wid * MF_WC;                         // first chunk column of this wave
   const bool dhalf = cw0 < SYM_H;
@@ -412,14 +424,22 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
 #pragma unroll
   for (int t = 0; t < MF_NT; ++t) dcol[t][0] = dcol[t][1] = d4{0.0, 0.0, 0.0, 0.0};
 
-  auto load_cf = [&](uint64_t b0, int64_t ws, int H, int g, int t, d2* cf) {
+  auto load_cf = [&](uint64_t b0, int64_t ws, int H, int nci, int g, int t, d2* cf) {
     asm volatile("" : "+s"(b0));
     const int xc = cw0 + 32 * t + 2 * lo;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int rB = 16 * g + 4 * a + hi;
       const double* row = (const double*)b0 + (int64_t)(rB < H ? rB : H - 1) * ws;
-      cf[a] = ldg_nt((const d2*)(row + (xc < ncc ? xc : 0)));
+      cf[a] = ldg_nt((const d2*)(row + (xc < (RAG ? nci : ncc) ? xc : 0)));
+    }
+  };
+  auto band_zero = [&](int nci, int t, d2* cf) {   // as k_sym_mfma
+    const int xc = cw0 + 32 * t + 2 * lo;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      cf[a].x = xc < nci ? cf[a].x : 0.0;
+      cf[a].y = xc + 1 < nci ? cf[a].y : 0.0;
     }
   };
   auto load_bcol = [&](int r0, int H, bool zero, int g, double* bc) {
@@ -435,7 +455,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
   uint64_t curb = pbase(cur);
   d2 cfn[4];
   double bcn[4];
-  load_cf(curb, cur.w, cur.H, 0, 0, cfn);
+  load_cf(curb, cur.w, cur.H, cur.nc, 0, 0, cfn);
   load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
 
   int gg = 0;
@@ -452,6 +472,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
       const int64_t gw = same ? cur.w : (more ? nx.w : 0);
       const int gH = same ? cur.H : (more ? nx.H : 1);
       const int gn = same ? g + 1 : 0;
+      const int gnc = same ? cur.nc : nx.nc;
       const int gr0 = same ? cur.r0 : nx.r0;
       const bool gz = dhalf && gr0 == c0;
       double bcol[4];
@@ -466,12 +487,13 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
         for (int a = 0; a < 4; ++a) cf[a] = cfn[a];
         // next step's loads are issued here, ahead of this step's LDS and MFMA work
         if (t + 1 < MF_NT) {
-          load_cf(curb, cur.w, cur.H, g, t + 1, cfn);
+          load_cf(curb, cur.w, cur.H, cur.nc, g, t + 1, cfn);
         } else {
-          load_cf(gb, gw, gH, gn, 0, cfn);
+          load_cf(gb, gw, gH, gnc, gn, 0, cfn);
           load_bcol(gr0, gH, gz, gn, bcn);
         }
         if (t >= nta) continue;
+        if (RAG && cur.nc < ncc) band_zero(cur.nc, t, cf);
         lds_order();                                   // previous step's tile reads done
 #pragma unroll
         for (int a = 0; a < 4; ++a) *(d2*)(sb + (4 * a + hi) * LDP + 2 * lo) = cf[a];
@@ -594,11 +616,16 @@ static bool mf_skip() {
   return v;
 }
 
+// ragged: some strip item stops short of its strip's widest (band blocks): the
+// RAG kernels (default variant only: the A/B switches do not apply there)
 template <int NG, int NW, int PD>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
-                      const int* run, int pks, hipStream_t st) {
-  if (mf_pw() && mf_skip())
+                      const int* run, int pks, bool ragged, hipStream_t st) {
+  if (ragged)
+    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, true>), dim3(nstrips), dim3(NW * 64), 0,
+                       st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (mf_pw() && mf_skip())
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true>), dim3(nstrips), dim3(NW * 64), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else if (mf_pw())
@@ -611,7 +638,7 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
 
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                            const PassArgs& pa, int64_t mpad, double* d_pk, double* rowpart,
-                           double* colpart, hipStream_t st) {
+                           double* colpart, bool ragged, hipStream_t st) {
   if (nc < 1 || nc > 16) return hipErrorInvalidValue;
   // SGV_PK16=1 (A/B, SGV_AB=1): the round-2 16-column Pk rows for every NC
   static const bool pk16 = [] {
@@ -632,10 +659,13 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
   // not come from cache): measured in DESIGN.md
   switch ((nc + 3) / 4) {
     // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
-    case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, st); break;
-    case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, st); break;
+    case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, st); break;
+    case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, st); break;
     default:
-      if (mf_skip())
+      if (ragged)
+        hipLaunchKernelGGL((k_sym_mfma16<true, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
+                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
+      else if (mf_skip())
         hipLaunchKernelGGL(k_sym_mfma16<true>, dim3(nstrips), dim3(256), 0, st, d_strips, d_sitems,
                            d_pk, nc, rowpart, colpart, pa.run);
       else

@@ -767,7 +767,7 @@ def test_ld_matvec_band_vs_scipy(parts, ncol, s, kern):
     if all(bw is None or bw >= 5 for _, bw in parts):   # one detected block per part
         assert L.block_sizes == [n for n, _ in parts]
         for b, (n, bw) in enumerate(parts):
-            band = bw is not None and -(-(256 + bw) // 512) * 512 < n
+            band = bw is not None and -(-(256 + bw) // 256) * 256 < n
             assert eng.ld_block_format(0, b) == (2 if band else 1), (b, n, bw)
     else:   # R = I splits into 1-marker blocks, merged into >= 128-marker blocks
         assert min(L.block_sizes[:-2]) >= 128 and L.block_sizes[-1] == 2050

@@ -3,12 +3,13 @@
 (sgv_set_ld_block_csr): one band of M markers and bandwidth bw built on the host
 (oracle.vamp_oracle.banded_ld, a few taps so it is cheap at any size), uploaded as
 CSR, then kernel time per pass (HIP events) for 1..16 right-hand sides.  The
-stored bytes are the band's panels (round_up(256 + bw, 512) columns per 256-row
+stored bytes are the band's panels (round_up(256 + bw, 256) columns per 256-row
 panel); the "csr_equiv" rate counts the 12 B per stored nonzero (8-B value +
 4-B index) a CSR mat-vec would stream instead.
 
   python tools/ldpass_band.py --M 200000 --bw 2000 --ncols 1,2,8,16"""
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -28,7 +29,12 @@ def main():
     ap.add_argument("--taps", type=int, default=12)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--ncols", default="1,2,8,16")
+    ap.add_argument("--lib", default=None, help="A/B of builds: load this libsgvamp_hip.so")
+    ap.add_argument("--tag", default="")
     a = ap.parse_args()
+    if a.lib:
+        import hip_backend
+        hip_backend.load(a.lib, strict=False)
     from engine import Engine
     from oracle import vamp_oracle as vo
     from sgvamp import BlockLD
@@ -45,17 +51,18 @@ def main():
     rs = np.random.RandomState(0)
     for nc in [int(x) for x in a.ncols.split(",")]:
         V = rs.normal(size=(nc, a.M))
-        eng.ld_matvec(0, V)
+        Y = eng.ld_matvec(0, V)
         eng.timers(reset=True)
         for _ in range(a.reps):
             eng.ld_matvec(0, V)
         t = eng.timers()
         ms = t["ld_ms"] / t["ld_launches"]
-        print(json.dumps(dict(M=a.M, bw=a.bw, ncol=nc, ms_per_pass=ms,
+        print(json.dumps(dict(tag=a.tag, M=a.M, bw=a.bw, ncol=nc, ms_per_pass=ms,
                               stored_GB=t["ld_bytes"] / t["ld_launches"] / 1e9,
                               stored_GBs=t["ld_bytes"] / t["ld_launches"] / ms / 1e6,
                               frac_of_8TBs=t["ld_bytes"] / t["ld_launches"] / ms / 1e6 / 8000.0,
-                              csr_equiv_GBs=12.0 * A.nnz / ms / 1e6)), flush=True)
+                              csr_equiv_GBs=12.0 * A.nnz / ms / 1e6,
+                              sha=hashlib.sha256(Y.tobytes()).hexdigest()[:16])), flush=True)
     eng.close()
 
 
