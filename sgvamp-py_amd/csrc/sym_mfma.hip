@@ -7,7 +7,8 @@
 // f64 of R and ONE f64 of P per lane and lets the matrix core do the register
 // blocking.  Of the two f64 shapes, v_mfma_f64_4x4x4f64 (4 blocks of 4x4x4)
 // costs 17 cycles for 256 MACs (~71 TF) and v_mfma_f64_16x16x4f64 140 cycles
-// for 1024 (~47 TF) (tools/mfma_probe.hip); the 4x4x4 form also needs only
+// for 1024 (~47 TF) (tools/mfma_probe.hip; one accumulator chain: 44 / 184
+// cycles per MFMA, 4 chains 18 / 144); the 4x4x4 form also needs only
 // ceil(NC/4) column groups instead of padding to 16.  Per 16x32 sub-tile
 // (4 KiB of R) the pass issues 16 * ceil(NC/4) of them (~270 cycles per group),
 // under the ~1300-1500 cycles the same bytes take to arrive from HBM.
@@ -87,7 +88,11 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // per panel when the item's row partials are written -- the same additions as
 // the per-row-group exchange through red[] (PW = false), with one barrier pair
 // per panel instead of a barrier per 16-row group.
-template <int NG, int NW, int PD, bool PW, bool SKIP, bool RAG = false>
+// DEF: a step's row MFMAs are deferred into the next step and interleaved with
+// its column MFMAs, so consecutive MFMAs of one accumulator chain sit 8 issues
+// apart instead of 4 (2 at NG = 1); every chain accumulates in the same order
+// (bitwise the same sums), the row fragments are double-buffered in registers.
+template <int NG, int NW, int PD, bool PW, bool SKIP, bool RAG = false, bool DEF = false>
 __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
                                                          const SymItem* __restrict__ sitems,
                                                          const double* __restrict__ pk, int ncol,
@@ -234,9 +239,11 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
 #pragma unroll
         for (int q = 0; q < NG; ++q) drow[r][q] = 0.0;
       const bool colz = SKIP && dhalf && cur.r0 == c0;   // this panel's column B operands are 0
+      d2 rfb[DEF ? 2 : 1][4];                            // row fragments (DEF: this and the previous step)
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        d2 cf[4], rf[4];
+        d2 cf[4];
+        d2* rf = rfb[DEF ? (t & 1) : 0];
         const int slot = t % PD;                       // compile-time after unrolling
 #pragma unroll
         for (int a = 0; a < 4; ++a) cf[a] = cfq[slot][a];
@@ -262,25 +269,54 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
         // (NC = 4/8 0.7-1.5 % faster per pass on two boxes; NC = 16 1 % slower,
         // not used there -- profiles/r02s10_prio_ab.txt)
         __builtin_amdgcn_s_setprio(1);
-        if (!colz) {
+        // x halves of all 4*NG row chains, then the y halves: a chain's two MFMAs
+        // are 4*NG issues apart instead of back to back (same per-chain order)
+        auto row_mfma = [&](const d2* f, int tt) {
 #pragma unroll
-          for (int a = 0; a < 4; ++a)
+          for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int q = 0; q < NG; ++q) {
-              dcol[t][0][q] = MFMA4(cf[a].x, bcol[a][q], dcol[t][0][q]);
-              dcol[t][1][q] = MFMA4(cf[a].y, bcol[a][q], dcol[t][1][q]);
+            for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(f[r].x, brow[tt][0][q], drow[r][q]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(f[r].y, brow[tt][1][q], drow[r][q]);
+        };
+        if constexpr (DEF) {
+          // column level a of this step, then a quarter of the previous step's
+          // row MFMAs (x halves of rows 2(a&1), +1 for a < 2, then the y halves)
+          const d2* rp = rfb[(t + 1) & 1];
+#pragma unroll
+          for (int a = 0; a < 4; ++a) {
+            if (!colz) {
+#pragma unroll
+              for (int q = 0; q < NG; ++q) {
+                dcol[t][0][q] = MFMA4(cf[a].x, bcol[a][q], dcol[t][0][q]);
+                dcol[t][1][q] = MFMA4(cf[a].y, bcol[a][q], dcol[t][1][q]);
+              }
             }
+            if (t > 0) {
+              const int tp = t > 0 ? t - 1 : 0;
+#pragma unroll
+              for (int r = 2 * (a & 1); r < 2 * (a & 1) + 2; ++r)
+#pragma unroll
+                for (int q = 0; q < NG; ++q)
+                  drow[r][q] = MFMA4(a < 2 ? rp[r].x : rp[r].y, brow[tp][a < 2 ? 0 : 1][q], drow[r][q]);
+            }
+          }
+          // the row group's last active step: its own row MFMAs now
+          if (t == NT - 1 || t + 1 == nta) row_mfma(rf, t);
+        } else {
+          if (!colz) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+              for (int q = 0; q < NG; ++q) {
+                dcol[t][0][q] = MFMA4(cf[a].x, bcol[a][q], dcol[t][0][q]);
+                dcol[t][1][q] = MFMA4(cf[a].y, bcol[a][q], dcol[t][1][q]);
+              }
+          }
+          row_mfma(rf, t);
         }
-        // x halves of all 4*NG chains, then the y halves: a chain's two MFMAs are
-        // 4*NG issues apart instead of back to back (same per-chain order)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(rf[r].x, brow[t][0][q], drow[r][q]);
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(rf[r].y, brow[t][1][q], drow[r][q]);
         __builtin_amdgcn_s_setprio(0);
       }
       // row sums: the 4 blocks (lanes differing in bits 2,3), then the waves in order
@@ -385,7 +421,7 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int MF_WC = MF_CW / 4;
 constexpr int MF_NT = MF_WC / 32;
 
-template <bool SKIP, bool RAG = false>
+template <int PD, bool SKIP, bool RAG = false>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -452,10 +488,12 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
   };
   auto pbase = [&](const SymItem& x) { return (uint64_t)(x.P + (x.c0 - x.r0)); };
 
+  static_assert(PD >= 1 && PD <= MF_NT && MF_NT % PD == 0, "prefetch depth divides the steps");
   uint64_t curb = pbase(cur);
-  d2 cfn[4];
+  d2 cfq[PD][4];                                       // ring of PD steps in flight per wave
   double bcn[4];
-  load_cf(curb, cur.w, cur.H, cur.nc, 0, 0, cfn);
+#pragma unroll
+  for (int p = 0; p < PD; ++p) load_cf(curb, cur.w, cur.H, cur.nc, 0, p, cfq[p]);
   load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
 
   int gg = 0;
@@ -483,14 +521,15 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
 #pragma unroll
       for (int t = 0; t < MF_NT; ++t) {
         d2 cf[4], rf[4];
+        const int slot = t % PD;                       // compile-time after unrolling
 #pragma unroll
-        for (int a = 0; a < 4; ++a) cf[a] = cfn[a];
-        // next step's loads are issued here, ahead of this step's LDS and MFMA work
-        if (t + 1 < MF_NT) {
-          load_cf(curb, cur.w, cur.H, cur.nc, g, t + 1, cfn);
+        for (int a = 0; a < 4; ++a) cf[a] = cfq[slot][a];
+        // step + PD goes out here, ahead of this step's LDS and MFMA work
+        if (t + PD < MF_NT) {
+          load_cf(curb, cur.w, cur.H, cur.nc, g, t + PD, cfq[slot]);
         } else {
-          load_cf(gb, gw, gH, gnc, gn, 0, cfn);
-          load_bcol(gr0, gH, gz, gn, bcn);
+          load_cf(gb, gw, gH, gnc, gn, t + PD - MF_NT, cfq[slot]);
+          if (t + PD == MF_NT) load_bcol(gr0, gH, gz, gn, bcn);
         }
         if (t >= nta) continue;
         if (RAG && cur.nc < ncc) band_zero(cur.nc, t, cf);
@@ -616,6 +655,29 @@ static bool mf_skip() {
   return v;
 }
 
+// SGV_MF_DEFER (A/B, with SGV_AB=1): default 1 = row MFMAs deferred into the
+// next step (k_sym_mfma<.., DEF>: bitwise the same products; NC = 4 passes
+// 1-2 % faster, NC = 8 within noise -- profiles/r03/s4/mf_defer_ab.jsonl);
+// 0 = a step's row MFMAs right behind its column MFMAs
+static bool mf_defer() {
+  static const bool v = [] {
+    const char* e = ab_env("SGV_MF_DEFER");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+// SGV_MF16_PD (A/B, with SGV_AB=1): prefetch depth of k_sym_mfma16, default 2
+// (bitwise the same products; C5's pass -1.3 %, the 8-block share -2.5 %, M = 1e6
+// at 16 columns within noise -- profiles/r03/s4/mf16_pd_ab.jsonl), 1 = one step
+static int mf16_pd() {
+  static const int v = [] {
+    const char* e = ab_env("SGV_MF16_PD");
+    return (e && e[0] == '1') ? 1 : 2;
+  }();
+  return v;
+}
+
 // ragged: some strip item stops short of its strip's widest (band blocks): the
 // RAG kernels (default variant only: the A/B switches do not apply there)
 template <int NG, int NW, int PD>
@@ -625,6 +687,9 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
   if (ragged)
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, true>), dim3(nstrips), dim3(NW * 64), 0,
                        st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (mf_pw() && mf_skip() && mf_defer())
+    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, false, true>), dim3(nstrips),
+                       dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else if (mf_pw() && mf_skip())
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true>), dim3(nstrips), dim3(NW * 64), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
@@ -655,22 +720,26 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
   else
     hipLaunchKernelGGL(k_pack<16>, pg, dim3(256), 0, st, pa, nc, mpad, d_pk);
   // 9..16 columns: one 16x16x4 group beats three/four 4x4x4 groups (register
-  // pressure) and splitting the groups over two wave sets (the repeat R reads do
-  // not come from cache): measured in DESIGN.md
+  // pressure) and two 8-column wave sets of the 4x4x4 kernel in one 8-wave
+  // workgroup re-reading the same R with the default cache policy (+33 %,
+  // profiles/r03/s4/mf_sets_ab.jsonl): measured in DESIGN.md
   switch ((nc + 3) / 4) {
     // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
     case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, st); break;
     case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, st); break;
     default:
       if (ragged)
-        hipLaunchKernelGGL((k_sym_mfma16<true, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
+        hipLaunchKernelGGL((k_sym_mfma16<1, true, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
+                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
+      else if (mf16_pd() == 2)
+        hipLaunchKernelGGL((k_sym_mfma16<2, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
                            d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       else if (mf_skip())
-        hipLaunchKernelGGL(k_sym_mfma16<true>, dim3(nstrips), dim3(256), 0, st, d_strips, d_sitems,
-                           d_pk, nc, rowpart, colpart, pa.run);
+        hipLaunchKernelGGL((k_sym_mfma16<1, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
+                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       else
-        hipLaunchKernelGGL(k_sym_mfma16<false>, dim3(nstrips), dim3(256), 0, st, d_strips, d_sitems,
-                           d_pk, nc, rowpart, colpart, pa.run);
+        hipLaunchKernelGGL((k_sym_mfma16<1, false>), dim3(nstrips), dim3(256), 0, st, d_strips,
+                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       break;
   }
   return hipGetLastError();

@@ -3,6 +3,7 @@
 # the B setting, then the LD-pass microbenchmark (tools/ldpass_ab.py, bitwise
 # hashes) and the north-star bench, alternating A and B processes.
 #   bash tools/gpu_ab_env.sh <out-prefix> <VAR> <A> <B> [bench args...]
+# AB_NCOLS / AB_SHAPES override the microbenchmark's column counts / block shapes.
 set -o pipefail
 out=$1; var=$2; va=$3; vb=$4
 shift 4
@@ -13,7 +14,7 @@ env "$var=$vb" timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x
 tail -1 ${out}_parity.log
 for v in $va $vb $va $vb; do
   env "$var=$v" timeout -k 10 300 python -u tools/ldpass_ab.py --tag "$var=$v" \
-      --shapes 64x15625,8x25000,8x15625 --ncols 4,8 >> ${out}_ab.jsonl 2>> ${out}_ab.err || exit 1
+      --shapes ${AB_SHAPES:-64x15625,8x25000,8x15625} --ncols ${AB_NCOLS:-4,8} >> ${out}_ab.jsonl 2>> ${out}_ab.err || exit 1
 done
 for v in $va $vb $va $vb; do
   env "$var=$v" timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --cpu-baseline off \

@@ -173,6 +173,24 @@ int main() {
     printf("v_fma_f64 waves/SIMD=%d: %.3f ms  %.1f TF  cycles/fma(clock64)=%.2f\n", wps, ms,
            flops / ms / 1e9, (double)cyc / (iters * 16.0));
   }
+  // dependent-accumulator latency: one wave per SIMD, NACC independent chains
+  // (cycles per MFMA at NACC = 1 is the dependent issue-to-issue latency)
+  auto chains = [&](auto kern, const char* name, int nacc) {
+    const int nblk = 256;
+    kern<<<nblk, 256>>>(dout, iters, dcyc);
+    CK(hipDeviceSynchronize());
+    long long cyc;
+    CK(hipMemcpy(&cyc, dcyc, 8, hipMemcpyDeviceToHost));
+    printf("%s chains=%d: cycles/mfma(clock64)=%.1f\n", name, nacc, (double)cyc / (iters * (double)nacc));
+  };
+  chains(k_mfma4_rate<1>, "mfma_f64_4x4x4", 1);
+  chains(k_mfma4_rate<2>, "mfma_f64_4x4x4", 2);
+  chains(k_mfma4_rate<4>, "mfma_f64_4x4x4", 4);
+  chains(k_mfma4_rate<8>, "mfma_f64_4x4x4", 8);
+  chains(k_mfma_rate<1>, "mfma_f64_16x16x4", 1);
+  chains(k_mfma_rate<2>, "mfma_f64_16x16x4", 2);
+  chains(k_mfma_rate<4>, "mfma_f64_16x16x4", 4);
+  chains(k_mfma_rate<8>, "mfma_f64_16x16x4", 8);
   printf("done\n");
   return 0;
 }
