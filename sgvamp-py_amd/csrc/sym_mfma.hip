@@ -722,7 +722,9 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
   // 9..16 columns: one 16x16x4 group beats three/four 4x4x4 groups (register
   // pressure) and two 8-column wave sets of the 4x4x4 kernel in one 8-wave
   // workgroup re-reading the same R with the default cache policy (+33 %,
-  // profiles/r03/s4/mf_sets_ab.jsonl): measured in DESIGN.md
+  // profiles/r03/s4/mf_sets_ab.jsonl) and three / four 4x4x4 groups at one wave
+  // per SIMD with the deferred row MFMAs (+13 % / +28 %, ng4_ab.jsonl):
+  // measured in DESIGN.md
   switch ((nc + 3) / 4) {
     // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
     case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, st); break;
