@@ -7,6 +7,7 @@
 // reference expressions (src/sgvamp.py cited per line); all vector arithmetic
 // runs in the HIP kernels of ld_pass.hip / vec.hip / synth.hip.
 #include "common.h"
+#include "hybrd.h"
 #include "../../include/sgvamp_hip.h"
 
 #include <rccl/rccl.h>
@@ -1316,7 +1317,8 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   CREATE_HIP(hipMemcpy(c->d_counts, &nblk, sizeof(int), hipMemcpyHostToDevice));
   CREATE_HIP(hipMalloc(&c->d_tot, sizeof(double) * 64));
   CREATE_HIP(hipMalloc(&c->d_pq, sizeof(double) * 2 * MAXC));
-  CREATE_HIP(hipHostMalloc(&c->h_tot, sizeof(double) * std::max(64, K), hipHostMallocCoherent));
+  // >= (MAXL + 1) * (MAXL + 1): the MLE Jacobian's batched sums (mle_jacobian)
+  CREATE_HIP(hipHostMalloc(&c->h_tot, sizeof(double) * std::max(128, K), hipHostMallocCoherent));
   CREATE_HIP(hipMalloc(&c->d_cgs, sizeof(CgState)));
   CREATE_HIP(hipMalloc(&c->d_rhonew, sizeof(double) * MAXC));
   CREATE_HIP(hipHostMalloc(&c->h_cgm, sizeof(CgState) * CG_RING, hipHostMallocCoherent));
@@ -2206,21 +2208,90 @@ struct MleFn {
   const double* omega0;
   double exp_max;
   int rc;
+  // the sums of the last evaluation and the omega they were taken at: the
+  // Jacobian's gam column (x[L] perturbed) has the same omega, so its sums are
+  // these, bitwise (the device sums are deterministic)
+  double S[MAXL + 1], Sx[MAXL + 1];
+  bool have_s;
 };
 
-static int mle_lagrangian(void* user, int n, const double* x, double* y) {
-  MleFn& f = *(MleFn*)user;
+// Lagrangian_der (:159-160) from the sums S at omega = x[:L]
+static void mle_residual(const MleFn& f, const double* x, const double* S, double* y) {
   const int L = f.L;
-  double S[MAXL + 1];
-  f.rc = sgv_mle_terms(f.c, f.a, f.gam1s, L, f.sigma2, x, f.exp_max, S);   // omega = x[:L]
-  if (f.rc != SGV_OK) return -1;
   const double gam = x[L];
   for (int l = 0; l < L; ++l) y[l] = (S[l] + (f.omega0[l] - 1.0) / x[l]) + gam;   // :159
   double sw = 0.0;                                                                   // :160
   for (int l = 0; l < L; ++l) sw += x[l];
   y[L] = sw - 1.0;
+}
+
+static int mle_lagrangian(void* user, int n, const double* x, double* y) {
+  MleFn& f = *(MleFn*)user;
+  const int L = f.L;
+  f.rc = sgv_mle_terms(f.c, f.a, f.gam1s, L, f.sigma2, x, f.exp_max, f.S);   // omega = x[:L]
+  if (f.rc != SGV_OK) return -1;
+  std::memcpy(f.Sx, x, sizeof(double) * L);
+  f.have_s = true;
+  mle_residual(f, x, f.S, y);
   (void)n;
   return 0;
+}
+
+// the forward-difference Jacobian's n = L + 1 points (hybrd's fdjac1): the L
+// omega columns' device sums enqueued back to back with one host wait instead
+// of one per point, the gam column from the base point's sums.  One cohort
+// group, one rank (the host exchange waits per reduction anyway); otherwise
+// point by point.  Each point's sums are the same launches as mle_lagrangian's,
+// so the Jacobian is bitwise the per-point one.
+static int mle_jacobian(void* user, int n, const double* x, const double* h, double* F) {
+  MleFn& f = *(MleFn*)user;
+  sgv_ctx* c = f.c;
+  const int L = f.L;
+  double xj[MAXL + 2];
+  const bool base = f.have_s && std::memcmp(f.Sx, x, sizeof(double) * L) == 0;
+  if (c->K > MAXK || c->comm || c->host_ag) {
+    for (int j = 0; j < n; ++j) {
+      std::memcpy(xj, x, sizeof(double) * n);
+      xj[j] = x[j] + h[j];
+      if (mle_lagrangian(user, n, xj, F + (size_t)j * n) < 0) return -1;
+    }
+    return 0;
+  }
+  f.rc = [&]() -> int {
+    ENTER(c);
+    MleArgs m;
+    CHK(mle_args(c, f.gam1s, L, f.sigma2, 0, &m));
+    for (int k = 0; k < m.K; ++k) m.a[k] = f.a[k];
+    m.exp_max = f.exp_max;
+    for (int j = 0; j < L; ++j) {
+      for (int l = 0; l < L; ++l) m.omega[l] = l == j ? x[l] + h[l] : x[l];
+      HIPCHK(launch_mle_terms(c->d_ch, c->nch, m, c->d_part, c->st));
+      CHK(reduce_dev(c, MAXL + 1, c->d_ch_begin, identity_map(), c->h_tot + j * (MAXL + 1)));
+    }
+    CHK(stream_wait(c));
+    resolve_timers(c);
+    return SGV_OK;
+  }();
+  if (f.rc != SGV_OK) return -1;
+  double base_s[MAXL + 1];
+  if (base) std::memcpy(base_s, f.S, sizeof(double) * L);
+  for (int j = 0; j < L; ++j) {
+    std::memcpy(xj, x, sizeof(double) * n);
+    xj[j] = x[j] + h[j];
+    std::memcpy(f.S, c->h_tot + j * (MAXL + 1), sizeof(double) * L);
+    std::memcpy(f.Sx, xj, sizeof(double) * L);
+    mle_residual(f, xj, f.S, F + (size_t)j * n);
+  }
+  // the gam column: omega = x[:L], the base point's sums
+  std::memcpy(xj, x, sizeof(double) * n);
+  xj[L] = x[L] + h[L];
+  if (base) {
+    std::memcpy(f.S, base_s, sizeof(double) * L);
+    std::memcpy(f.Sx, x, sizeof(double) * L);
+    mle_residual(f, xj, f.S, F + (size_t)L * n);
+    return 0;
+  }
+  return mle_lagrangian(user, n, xj, F + (size_t)L * n);
 }
 
 extern "C" int sgv_mle_update(sgv_ctx* c, const double* gam1s, const double* a, int nslab,
@@ -2238,9 +2309,15 @@ extern "C" int sgv_mle_update(sgv_ctx* c, const double* gam1s, const double* a, 
   for (int l = 0; l < nslab; ++l) sigma2[1 + l] = sigmas[l];
   for (int l = 0; l < L; ++l) x[l] = omega0[l];                   // :173-178
   x[L] = std::isnan(*gam_io) ? 1.0 : *gam_io;
-  MleFn f{c, gam1s, a, L, sigma2, omega0, 0.0, SGV_OK};
+  MleFn f{c, gam1s, a, L, sigma2, omega0, 0.0, SGV_OK, {}, {}, false};
   CHK(sgv_mle_exp_max(c, gam1s, L, sigma2, &f.exp_max));           // :152, once per update
-  const int ier = sgv_fsolve(L + 1, mle_lagrangian, &f, x, nullptr, nullptr);   // :179
+  // :179; SGV_MLE_JAC=0 (with SGV_AB=1): the Jacobian point by point
+  static const bool jb = [] {
+    const char* e = ab_env("SGV_MLE_JAC");
+    return !(e && e[0] == '0');
+  }();
+  const int ier = sgv_fsolve_jac(L + 1, mle_lagrangian, jb ? mle_jacobian : nullptr, &f, x,
+                                 nullptr, nullptr);
   if (f.rc != SGV_OK) return f.rc;
   if (ier != 1) {                                                 // :181-184
     *status_out = SGV_MLE_NOT_CONVERGED;

@@ -15,7 +15,7 @@
 #include <cstring>
 #include <vector>
 
-#include "sgvamp_hip.h"
+#include "hybrd.h"
 
 namespace {
 
@@ -310,15 +310,19 @@ void r1mpyq(int m, int n, double* a, int lda, const double* v, const double* w) 
 // 1.49012e-08, maxfev 200 (n + 1), epsfcn = machine eps, factor 100, mode 1.
 // Returns MINPACK's info (1 = converged; 2 maxfev; 3 xtol too small; 4/5 no
 // progress; < 0 the callback's negative status); x_io holds the last iterate.
-extern "C" int sgv_fsolve(int n, sgv_fsolve_fn fcn, void* user, double* x_io, double* fvec_out,
-                          int* nfev_out) {
+// jac (may be null): the forward-difference Jacobian's n evaluations in one
+// call, F row j = fcn(x + h_j e_j) -- the same points, so the same iterates as
+// n calls of fcn; a caller whose evaluations are device passes enqueues them
+// back to back and waits once (sgv_mle_update)
+int sgv_fsolve_jac(int n, sgv_fsolve_fn fcn, sgv_fsolve_jac_fn jac, void* user, double* x_io,
+                   double* fvec_out, int* nfev_out) {
   if (n <= 0 || !fcn || !x_io) return 0;
   const double xtol = 1.49012e-08, factor = 100.0;
   const double epsfcn = EPSMCH;
   const int maxfev = 200 * (n + 1);
   const double p1 = 0.1, p5 = 0.5, p001 = 1e-3, p0001 = 1e-4;
   std::vector<double> fvec(n), diag(n), fjac((size_t)n * n), r((size_t)n * (n + 1) / 2), qtf(n),
-      wa1(n), wa2(n), wa3(n), wa4(n);
+      wa1(n), wa2(n), wa3(n), wa4(n), hj(jac ? n : 0), fj(jac ? (size_t)n * n : 0);
   double* x = x_io;
   Mat J{fjac.data(), n};
   int info = 0, nfev = 0;
@@ -333,15 +337,26 @@ extern "C" int sgv_fsolve(int n, sgv_fsolve_fn fcn, void* user, double* x_io, do
     const double eps = std::sqrt(std::fmax(epsfcn, EPSMCH));
     for (;;) {   // outer loop: a fresh forward-difference Jacobian
       bool jeval = true;
-      for (int j = 0; j < n && rc >= 0; ++j) {   // fdjac1, dense
-        const double temp = x[j];
-        double h = eps * std::fabs(temp);
-        if (h == 0.0) h = eps;
-        x[j] = temp + h;
-        rc = fcn(user, n, x, wa1.data());
-        if (rc < 0) break;
-        x[j] = temp;
-        for (int i = 0; i < n; ++i) J(i, j) = (wa1[i] - fvec[i]) / h;
+      if (jac) {   // fdjac1, the n points in one call
+        for (int j = 0; j < n; ++j) {
+          hj[j] = eps * std::fabs(x[j]);
+          if (hj[j] == 0.0) hj[j] = eps;
+        }
+        rc = jac(user, n, x, hj.data(), fj.data());
+        if (rc >= 0)
+          for (int j = 0; j < n; ++j)
+            for (int i = 0; i < n; ++i) J(i, j) = (fj[(size_t)j * n + i] - fvec[i]) / hj[j];
+      } else {
+        for (int j = 0; j < n && rc >= 0; ++j) {   // fdjac1, dense
+          const double temp = x[j];
+          double h = eps * std::fabs(temp);
+          if (h == 0.0) h = eps;
+          x[j] = temp + h;
+          rc = fcn(user, n, x, wa1.data());
+          if (rc < 0) break;
+          x[j] = temp;
+          for (int i = 0; i < n; ++i) J(i, j) = (wa1[i] - fvec[i]) / h;
+        }
       }
       nfev += n;
       if (rc < 0) {
@@ -471,4 +486,9 @@ extern "C" int sgv_fsolve(int n, sgv_fsolve_fn fcn, void* user, double* x_io, do
   }
   if (nfev_out) *nfev_out = nfev;
   return info;
+}
+
+extern "C" int sgv_fsolve(int n, sgv_fsolve_fn fcn, void* user, double* x_io, double* fvec_out,
+                          int* nfev_out) {
+  return sgv_fsolve_jac(n, fcn, nullptr, user, x_io, fvec_out, nfev_out);
 }
