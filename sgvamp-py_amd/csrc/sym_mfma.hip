@@ -758,6 +758,8 @@ extern "C" int sgv_diag_mf_trace(unsigned long long* out, int n) {
 hipError_t launch_sym_finalize_strip(int nc, const SymPanel* d_panels, int npanels,
                                      const PassArgs& pa, const double* rowpart,
                                      const double* colpart, double* partials, hipStream_t st) {
+  // the partials with the default cache policy: nontemporal loads measured
+  // 0.5-3 % slower (profiles/r03/s4/fin_nt_ab.jsonl; they were just written)
 #define FIN_CASE(N)                                                                        \
   case N:                                                                                  \
     hipLaunchKernelGGL(k_sym_finalize_strip<N>, dim3(npanels), dim3(256 * FIN_Q), 0, st, d_panels, \
