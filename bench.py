@@ -375,6 +375,7 @@ def main():
         log("[bench] warmup it=%d cg=%s passes=%d %.1f ms" % (it, rec["cg_iters"], rec["ld_passes"],
                                                               rec["wall_s"] * 1e3))
     eng.timers(reset=True)
+    eng.exchange_stats(reset=True)
     eng.sync()
     v.set_iterations(args.warmup + args.steps)
     comm.barrier()
@@ -388,6 +389,8 @@ def main():
     comm.barrier()
     dt = max(comm.allgather(t1 - t0))
     tm = eng.timers()
+    xs = eng.exchange_stats()
+    xs_all = comm.allgather(xs) if world > 1 else [xs]
     # this box's own streaming-read rate (after the timed region; context only:
     # the roofline peak stays the guide's 8 TB/s); the slowest rank's
     box_bw = None
@@ -483,6 +486,23 @@ def main():
             "traffic_source": traffic_src,
             "box_stream_GBs": box_bw,
             "frac_of_box_stream": (achieved / box_bw) if (achieved and box_bw) else None,
+        },
+        "exchange": {
+            # cross-rank all-gathers of the timed steps (sgv_exchange_stats): the
+            # ordered CG/EM reductions and r1 gathers that replace the reference's
+            # bcast all-gather (src/sgvamp.py:228-233); ms = HIP events around each
+            # ncclAllGather (the wait for the slowest peer included) or the host
+            # callback's wall time; the slowest rank's
+            "transport": xs["transport"],
+            "allgathers_per_step": xs["allgathers"] / steps,
+            "ms_per_step": max(x["ms"] for x in xs_all) / steps,
+            "frac_of_step": (max(x["ms"] for x in xs_all) / steps) / (dt / steps * 1e3),
+            "bytes_per_step_per_rank": xs["bytes"] / steps,
+            "em_mode": xs["em_mode"],
+            "em_rep_max_km": xs["em_rep_max_km"],
+            "em_rep_max_km_source": "env SGV_EM_REP_MAX_KM" if os.environ.get("SGV_EM_REP_MAX_KM")
+                                    else "default (tunable; not measured on xGMI)",
+            "K_times_M": K * eng.M,
         },
         "ld_passes_per_step": passes / steps,
         "effective_ld_gbps_end_to_end": passes * ld_bytes_total / dt / 1e9,

@@ -155,6 +155,10 @@ int sgv_set_cg_exact(sgv_ctx* ctx, int mode);
 int sgv_set_ld_packing(sgv_ctx* ctx, int mode);
 /* fmt_out: 0 dense, 1 packed symmetric (triangle), 2 packed band, -1 not set. */
 int sgv_ld_block_format(sgv_ctx* ctx, int ld, int blk_local, int* fmt_out);
+/* Bytes one pass over LD matrix ld reads from this rank's blocks that are set
+ * (dense n^2*8, packed triangle / band: the stored panels).  Python's Engine
+ * sums it over ranks to pick the run's CG column-set mode (sgv_set_cg_exact). */
+int sgv_ld_stored_bytes(sgv_ctx* ctx, int ld, double* bytes_out);
 /* Download one LD block (row-major n x n into a host array of row stride ld_host). */
 int sgv_get_ld_block(sgv_ctx* ctx, int ld, int blk_local, double* rowmajor, int64_t ld_host);
 /* Start a new VAMP.infer on this context (src/sgvamp.py:198-217 restarts from
@@ -356,6 +360,17 @@ int sgv_cg_solve(sgv_ctx* ctx, int ld, int ncol, const double* c1, const double*
  * (2 * ncol * M_local * 8), t[4] = dense-equivalent LD bytes (n^2*8),
  * t[5] = packed-pass partial-buffer bytes (written + read).  reset != 0 zeroes. */
 int sgv_timers(sgv_ctx* ctx, double* t6, int reset);
+/* Cross-rank exchange counters since the last reset (the bcast/all-gather of
+ * src/sgvamp.py:228-233 and the CG/EM scalar reductions that replace it):
+ * out[0] = all-gathers issued, out[1] = ms spent in them (RCCL: HIP events
+ * around each ncclAllGather on the ctx stream, the wait for the slowest peer
+ * included; host exchange: wall time of the callback), out[2] = bytes this rank
+ * contributed, out[3] = EM prior loop mode (1 replicated: r1 all-gathered once
+ * per loop; 0 one exchange per EM step; -1 no communicator), out[4] = the
+ * replicated-EM threshold in cohort-markers (env SGV_EM_REP_MAX_KM, read when
+ * the communicator is set up; default 2^20), out[5] = 1 RCCL, 2 host exchange,
+ * 0 none.  reset != 0 zeroes out[0..2]. */
+int sgv_exchange_stats(sgv_ctx* ctx, double* out6, int reset);
 
 /* Synchronise the ctx stream. */
 int sgv_sync(sgv_ctx* ctx);

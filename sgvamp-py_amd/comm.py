@@ -337,7 +337,12 @@ def launch_from_env(environ=None):
     job = None
     if _int(env, "WORLD_SIZE") is not None:
         source = "env"
-        rank, size = _int(env, "RANK") or 0, _int(env, "WORLD_SIZE")
+        rank, size = _int(env, "RANK"), _int(env, "WORLD_SIZE")
+        if rank is None:
+            if size > 1:   # every process would take rank 0 and bind the rendezvous port
+                raise RuntimeError("WORLD_SIZE=%d but RANK is not set: a launcher of %d ranks "
+                                   "must give each its RANK" % (size, size))
+            rank = 0
         local_rank = _int(env, "LOCAL_RANK")
         local_size = _int(env, "LOCAL_WORLD_SIZE")
     elif _int(env, "OMPI_COMM_WORLD_SIZE") is not None:
@@ -368,7 +373,13 @@ def launch_from_env(environ=None):
     if rank is None or size is None or not 0 <= rank < size:
         raise RuntimeError("launcher environment (%s): rank %r of world size %r" % (source, rank, size))
     if local_rank is None:
-        local_rank = rank if (local_size == size or size == 1 or source == "env") else None
+        # the global rank is the node-local one only on a one-node world: the
+        # launcher says so (node-local size = world size), or -- RANK/WORLD_SIZE
+        # launches that set no LOCAL_WORLD_SIZE -- the ranks meet on this host
+        one_node = (local_size == size or size == 1 or
+                    (source == "env" and local_size is None and
+                     env.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost", "::1")))
+        local_rank = rank if one_node else None
     if local_rank is None:
         raise RuntimeError("launcher environment (%s) gives no node-local rank: set LOCAL_RANK "
                            "(it selects this rank's GPU)" % source)

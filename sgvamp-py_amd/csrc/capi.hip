@@ -296,6 +296,12 @@ struct sgv_ctx {
   // timers
   std::vector<hipEvent_t> evpool;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+  // cross-rank exchange counters (sgv_exchange_stats): all-gathers issued, the
+  // bytes each rank contributed, and their time -- HIP events around every
+  // ncclAllGather on the ctx stream (the wait for the slowest peer included),
+  // wall time of the host callback for the host exchange
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> xpending;
+  double xchg_n = 0.0, xchg_ms = 0.0, xchg_bytes = 0.0;
   double ld_ms = 0.0, ld_launches = 0.0, rhs_bytes = 0.0, ld_bytes = 0.0, dense_bytes = 0.0,
          aux_bytes = 0.0;
   std::string err;
@@ -376,6 +382,49 @@ static void resolve_timers(sgv_ctx* c) {
     c->evpool.push_back(pr.second);
   }
   c->pending.clear();
+  for (auto& pr : c->xpending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) c->xchg_ms += ms;
+    c->evpool.push_back(pr.first);
+    c->evpool.push_back(pr.second);
+  }
+  c->xpending.clear();
+}
+
+static int event_pair(sgv_ctx* c, hipEvent_t* e0, hipEvent_t* e1) {
+  if (c->evpool.size() < 2) {
+    HIPCHK(hipEventCreate(e0));
+    HIPCHK(hipEventCreate(e1));
+  } else {
+    *e0 = c->evpool.back();
+    c->evpool.pop_back();
+    *e1 = c->evpool.back();
+    c->evpool.pop_back();
+  }
+  return SGV_OK;
+}
+
+// every cross-rank all-gather of cnt doubles per rank goes through here: RCCL
+// on the ctx stream (timed by events), or the host callback on staged copies
+// (timed by the wall clock; the caller's copies are its own)
+static int allgather_timed(sgv_ctx* c, const double* d_send, double* d_recv, size_t cnt,
+                           const double* h_send, double* h_recv) {
+  c->xchg_n += 1.0;
+  c->xchg_bytes += 8.0 * (double)cnt;
+  if (c->comm) {
+    hipEvent_t e0, e1;
+    CHK(event_pair(c, &e0, &e1));
+    HIPCHK(hipEventRecord(e0, c->st));
+    NCCLCHK(ncclAllGather(d_send, d_recv, cnt, ncclDouble, c->comm, c->st));
+    HIPCHK(hipEventRecord(e1, c->st));
+    c->xpending.emplace_back(e0, e1);
+    return SGV_OK;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = c->host_ag(c->host_ag_user, h_send, h_recv, (int64_t)cnt);
+  c->xchg_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (rc != 0) return fail(c, SGV_ERR_RCCL, "host all-gather callback failed");
+  return SGV_OK;
 }
 
 // partials [nparts][nv] -> d_dst[map.d[v]] (global, ordered); stays on device
@@ -389,15 +438,13 @@ static int reduce_dev(sgv_ctx* c, int nv, const int* d_begin, const Map16& map, 
   const double* src = c->d_bsum;
   int nr = 1, nbm = c->nblk;
   if (c->comm) {
-    NCCLCHK(ncclAllGather(c->d_bsum, c->d_bsum_all, (size_t)c->nbmax * nv, ncclDouble, c->comm,
-                          c->st));
+    CHK(allgather_timed(c, c->d_bsum, c->d_bsum_all, (size_t)c->nbmax * nv, nullptr, nullptr));
   } else if (c->host_ag) {
     const size_t cnt = (size_t)c->nbmax * nv;
     HIPCHK(hipMemcpyAsync(c->h_bsum, c->d_bsum, sizeof(double) * cnt, hipMemcpyDeviceToHost,
                           c->st));
     CHK(stream_wait(c));
-    if (c->host_ag(c->host_ag_user, c->h_bsum, c->h_bsum_all, (int64_t)cnt) != 0)
-      return fail(c, SGV_ERR_RCCL, "host all-gather callback failed");
+    CHK(allgather_timed(c, nullptr, nullptr, cnt, c->h_bsum, c->h_bsum_all));
     HIPCHK(hipMemcpyAsync(c->d_bsum_all, c->h_bsum_all, sizeof(double) * cnt * c->nranks,
                           hipMemcpyHostToDevice, c->st));
   }
@@ -1487,14 +1534,10 @@ static int comm_args(sgv_ctx* c, int nranks, int rank, const int* nblk_per_rank)
 // all-gather of cnt doubles per rank (device buffers), RCCL or the host callback
 static int gather_f64(sgv_ctx* c, const double* d_send, double* d_recv, size_t cnt,
                       double* h_send, double* h_recv) {
-  if (c->comm) {
-    NCCLCHK(ncclAllGather(d_send, d_recv, cnt, ncclDouble, c->comm, c->st));
-    return SGV_OK;
-  }
+  if (c->comm) return allgather_timed(c, d_send, d_recv, cnt, nullptr, nullptr);
   HIPCHK(hipMemcpyAsync(h_send, d_send, sizeof(double) * cnt, hipMemcpyDeviceToHost, c->st));
   CHK(stream_wait(c));
-  if (c->host_ag(c->host_ag_user, h_send, h_recv, (int64_t)cnt) != 0)
-    return fail(c, SGV_ERR_RCCL, "host all-gather callback failed");
+  CHK(allgather_timed(c, nullptr, nullptr, cnt, h_send, h_recv));
   HIPCHK(hipMemcpyAsync(d_recv, h_recv, sizeof(double) * cnt * c->nranks, hipMemcpyHostToDevice,
                         c->st));
   return SGV_OK;
@@ -1512,12 +1555,24 @@ static int gather_f64(sgv_ctx* c, const double* d_send, double* d_recv, size_t c
 // over xGMI, so the replicated loop pays only below about a million
 // cohort-markers (C2: K M = 2e5 -> replicated; north star: 4e6 -> per step).
 // SGV_EM_REP=0/1 (with SGV_AB=1) forces either.
-constexpr double EM_REP_MAX_KM = 1048576.0;
+// The threshold is a tunable, not a measurement of this machine's xGMI:
+// SGV_EM_REP_MAX_KM overrides the default (read when the communicator is set
+// up), and sgv_exchange_stats reports the value in force and the mode chosen.
+constexpr double EM_REP_MAX_KM_DEFAULT = 1048576.0;
+static double em_rep_max_km() {
+  const char* e = std::getenv("SGV_EM_REP_MAX_KM");
+  if (e && *e) {
+    char* end = nullptr;
+    const double v = std::strtod(e, &end);
+    if (end != e && v >= 0.0) return v;
+  }
+  return EM_REP_MAX_KM_DEFAULT;
+}
 static bool em_rep_choice(const sgv_ctx* c) {
   if (c->K > MAXK) return false;   // the replicated loop runs one cohort group
   const char* e = ab_env("SGV_EM_REP");
   if (e) return e[0] != '0';
-  return (double)c->K * (double)c->Mtot <= EM_REP_MAX_KM;
+  return (double)c->K * (double)c->Mtot <= em_rep_max_km();
 }
 
 // replicated EM tables: every rank's block sizes (gathered), the global chunk
@@ -1817,6 +1872,16 @@ extern "C" int sgv_ld_block_format(sgv_ctx* c, int ld, int b, int* fmt_out) {
     return fail(c, SGV_ERR_ARG, "sgv_ld_block_format: bad arguments");
   const LdBlock& lb = c->ldb[ld][b];
   *fmt_out = lb.ptr ? (lb.fmt == 1 && lb.ext > 0 ? 2 : lb.fmt) : -1;
+  return SGV_OK;
+}
+
+extern "C" int sgv_ld_stored_bytes(sgv_ctx* c, int ld, double* out) {
+  ENTER(c);
+  if (ld < 0 || ld >= c->nld || !out) return fail(c, SGV_ERR_ARG, "sgv_ld_stored_bytes: bad arguments");
+  double s = 0.0;
+  for (int b = 0; b < c->nblk; ++b)
+    if (c->ldb[ld][b].ptr) s += c->ldb[ld][b].stored_bytes;
+  *out = s;
   return SGV_OK;
 }
 
@@ -2802,6 +2867,21 @@ extern "C" int sgv_timers(sgv_ctx* c, double* t6, int reset) {
   if (reset) {
     c->ld_ms = c->ld_launches = c->rhs_bytes = c->ld_bytes = c->dense_bytes = c->aux_bytes = 0.0;
   }
+  return SGV_OK;
+}
+
+extern "C" int sgv_exchange_stats(sgv_ctx* c, double* out, int reset) {
+  ENTER(c);
+  if (!out) return fail(c, SGV_ERR_ARG, "sgv_exchange_stats: out is null");
+  CHK(stream_wait(c));
+  resolve_timers(c);
+  out[0] = c->xchg_n;
+  out[1] = c->xchg_ms;
+  out[2] = c->xchg_bytes;
+  out[3] = (c->comm || c->host_ag) ? (c->em_rep ? 1.0 : 0.0) : -1.0;
+  out[4] = em_rep_max_km();
+  out[5] = c->comm ? 1.0 : c->host_ag ? 2.0 : 0.0;
+  if (reset) c->xchg_n = c->xchg_ms = c->xchg_bytes = 0.0;
   return SGV_OK;
 }
 

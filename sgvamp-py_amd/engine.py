@@ -21,9 +21,20 @@ def cg_exact_mode(block_sizes):
     """The run's CG column-set mode (sgv_set_cg_exact) from the GLOBAL LD: exact
     sets when a pass streams >= 24 GB of packed triangle, else look-ahead.  A
     function of the global block sizes only, so every rank of a run and every
-    rank count make the same choice (the modes can round differently)."""
+    rank count make the same choice (the modes can round differently).  The
+    estimate before any LD is stored; Engine.update_cg_exact refines it from the
+    bytes actually stored (band blocks store far less than the triangle)."""
     tri = sum(float(n) * (n + SYM_H) / 2.0 * 8.0 for n in block_sizes)
     return 1 if tri >= CG_EXACT_MIN_BYTES else 0
+
+
+def cg_exact_from_stored(global_bytes_per_ld, ld_of):
+    """The same choice from the global stored bytes of each LD matrix: exact when
+    a matrix shared by >= 2 cohorts (>= 4 CG columns: the MFMA pass, where a
+    narrower column set is cheaper) streams >= 24 GB per pass."""
+    shared = [l for l in set(ld_of) if list(ld_of).count(l) >= 2]
+    big = max((global_bytes_per_ld[l] for l in shared), default=0.0)
+    return 1 if big >= CG_EXACT_MIN_BYTES else 0
 
 
 class Engine:
@@ -105,6 +116,28 @@ class Engine:
         data = np.ascontiguousarray(upper.data, dtype=np.float64)
         self.ctx.sgv_set_ld_block_csr(ld, b_global - self.b0, indptr.ctypes.data_as(hb._c_i64_p),
                                       indices.ctypes.data_as(hb._c_i64_p), hb.dptr(data))
+
+    def stored_bytes(self, ld):
+        """Bytes one pass over LD matrix ld reads on this rank (blocks set so far)."""
+        out = np.zeros(1)
+        self.ctx.sgv_ld_stored_bytes(int(ld), hb.dptr(out))
+        return float(out[0])
+
+    def update_cg_exact(self):
+        """Once every rank's LD blocks are stored: the run's CG column-set mode
+        from the GLOBAL stored bytes (summed over ranks in rank order, so every
+        rank makes the same choice for any rank count).  Collective."""
+        local = np.array([self.stored_bytes(l) for l in range(self.nld)], dtype=np.float64)
+        if self.nranks > 1:
+            parts = self.comm.allgather(local)
+            tot = np.zeros(self.nld)
+            for p in parts:
+                tot = tot + np.asarray(p, dtype=np.float64)
+        else:
+            tot = local
+        self.cg_exact = cg_exact_from_stored(list(tot), self.ld_of)
+        self.ctx.sgv_set_cg_exact(self.cg_exact)    # an SGV_CG_EXACT A/B override wins
+        return self.cg_exact
 
     def get_ld_block(self, ld, b_global):
         n = self.block_sizes[b_global]
@@ -314,6 +347,16 @@ class Engine:
         self.ctx.sgv_timers(hb.dptr(t), int(bool(reset)))
         return dict(ld_ms=t[0], ld_launches=int(t[1]), ld_bytes=t[2], rhs_bytes=t[3],
                     dense_bytes=t[4], aux_bytes=t[5])
+
+    def exchange_stats(self, reset=False):
+        """Cross-rank exchange counters (sgv_exchange_stats): all-gathers issued,
+        ms in them, bytes contributed, the EM loop mode and its threshold."""
+        t = np.zeros(6)
+        self.ctx.sgv_exchange_stats(hb.dptr(t), int(bool(reset)))
+        return dict(allgathers=int(t[0]), ms=float(t[1]), bytes=float(t[2]),
+                    em_mode={1: "replicated", 0: "per-step", -1: None}[int(t[3])],
+                    em_rep_max_km=float(t[4]),
+                    transport={1: "rccl", 2: "host", 0: None}[int(t[5])])
 
     def set_ld_packing(self, packed):
         """True: symmetric blocks set/generated from now on are stored packed."""

@@ -57,6 +57,7 @@ _SIGS = {
     "sgv_set_ld_block_csr": [_vp, ctypes.c_int, ctypes.c_int, _c_i64_p, _c_i64_p, _c_dbl_p],
     "sgv_set_ld_packing": [_vp, ctypes.c_int],
     "sgv_ld_block_format": [_vp, ctypes.c_int, ctypes.c_int, _c_int_p],
+    "sgv_ld_stored_bytes": [_vp, ctypes.c_int, _c_dbl_p],
     "sgv_set_ridge": [_vp, ctypes.c_double],
     "sgv_set_cohort_n": [_vp, ctypes.c_int, ctypes.c_double],
     "sgv_set_vector": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p],
@@ -78,6 +79,7 @@ _SIGS = {
     "sgv_cg_solve": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, _c_dbl_p, _c_dbl_p, _c_dbl_p,
                      ctypes.c_int, ctypes.c_double, _c_int_p, _c_int_p],
     "sgv_timers": [_vp, _c_dbl_p, ctypes.c_int],
+    "sgv_exchange_stats": [_vp, _c_dbl_p, ctypes.c_int],
     "sgv_step": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dbl_p, _c_dbl_p,
                  _c_dbl_p, _c_dbl_p, _c_dbl_p, ctypes.c_double, _c_dbl_p, _c_dbl_p, _c_dbl_p,
                  _c_i8_p, ctypes.c_int, ctypes.c_double, ctypes.c_int, _c_dbl_p, _c_int_p,

@@ -45,13 +45,44 @@ def rank_envs(n, base=None, port=None, token=None):
     return out
 
 
+class _Signalled(BaseException):
+    def __init__(self, signum):
+        super().__init__(signum)
+        self.signum = signum
+
+
+def _pdeathsig():
+    """Child side, between fork and exec (nothing has touched a GPU): the kernel
+    sends the rank SIGTERM if the parent dies without stopping it (SIGKILL)."""
+    try:
+        import ctypes
+
+        libc = ctypes.CDLL(None, use_errno=True)
+        libc.prctl(1, signal.SIGTERM, 0, 0, 0)      # PR_SET_PDEATHSIG
+    except Exception:  # noqa: BLE001 -- best effort (non-Linux)
+        pass
+
+
 def spawn(n, argv, base=None, poll_s=0.05):
     """Run argv as n local ranks; returns the exit status (0 when all succeed,
-    else the first failing rank's)."""
+    else the first failing rank's).  A SIGTERM / SIGHUP / SIGINT to this parent
+    (a scheduler or timeout signalling only its PID) stops every rank before the
+    parent exits with 128 + the signal; a parent killed outright takes the ranks
+    with it (PR_SET_PDEATHSIG)."""
     procs = []
+    old = {}
+
+    def on_signal(signum, _frame):
+        raise _Signalled(signum)
+
+    for sig in (signal.SIGTERM, signal.SIGHUP):
+        try:
+            old[sig] = signal.signal(sig, on_signal)
+        except ValueError:   # not the main thread: leave the handlers alone
+            pass
     try:
         for r, env in enumerate(rank_envs(n, base)):
-            procs.append(subprocess.Popen(argv, env=env,
+            procs.append(subprocess.Popen(argv, env=env, preexec_fn=_pdeathsig,
                                           stdout=None if r == 0 else sys.stderr.fileno()))
         while True:
             codes = [p.poll() for p in procs]
@@ -62,9 +93,15 @@ def spawn(n, argv, base=None, poll_s=0.05):
             if all(c == 0 for c in codes):
                 return 0
             time.sleep(poll_s)
+    except _Signalled as e:
+        _stop(procs)
+        return 128 + int(e.signum)
     except BaseException:
         _stop(procs)
         raise
+    finally:
+        for sig, h in old.items():
+            signal.signal(sig, h)
 
 
 def _stop(procs, grace=10.0):

@@ -292,6 +292,7 @@ class VAMP:
         for l, L in enumerate(uniq):
             for b in range(eng.b0, eng.b1):
                 L.upload(eng, l, b, packed=self.ld_packing)
+        eng.update_cg_exact()   # the run's CG column sets from the bytes stored (collective)
         rr = np.asarray(r, dtype=np.float64)
         rr = rr.reshape(K, -1) if rr.size == K * self.M else rr
         for k in range(K):
@@ -315,6 +316,7 @@ class VAMP:
         (e.g. generated there); sets r1 = r (src/sgvamp.py:204) and N_k."""
         self.engine = engine
         self._begun = False
+        engine.update_cg_exact()   # collective: every rank attaches its engine
         for k in range(self.K):
             engine.set_vector(hb.VEC_R1, k, engine.get_vector(hb.VEC_R, k))
             engine.set_cohort_n(k, self.N_list[k])
@@ -353,6 +355,11 @@ class VAMP:
         elif getattr(self, "_begun", False):
             self._restart(R, r, x0)
         self._begun = True
+        # MLE steps chained behind a non-MLE one start fsolve from the context's
+        # gam: make it this object's (a rebuilt engine starts with none, and a
+        # drained step may have moved it), as the reference's self.gam carries
+        # over between infer() calls (src/sgvamp.py:170-176)
+        self.engine.set_mle_gam(self.gam)
         K = self.K
         self._st = dict(gam1=[self.gam1] * K, gamw=[self.gamw] * K, alpha1=[0] * K,
                         alpha2=[0] * K, gamws=[[] for _ in range(K)], xhat1s=[],
@@ -474,6 +481,8 @@ class VAMP:
         if getattr(self, "_queued", None) is not None:   # a step queued past the last call
             self.engine.step_end(self._queued["h"])
             self._queued = None
+            # its MLE update (if any) is thrown away: the context's gam follows Python's
+            self.engine.set_mle_gam(self.gam)
         self._submit_csv()
         self.flush()
         xl = getattr(self, "_xhat_loc", None)
@@ -835,4 +844,6 @@ class VAMP:
         (:139-160), whose K x M x L marker sums run on the device."""
         status, lam, omegas, gam = self.engine.mle_update(gam1s, self.a, self.sigmas, self.lam,
                                                           self.omegas, self.gam)
-        return self._mle_result(status, lam, omegas, gam)
+        warn = self._mle_result(status, lam, omegas, gam)
+        self.engine.set_mle_gam(self.gam)   # a later chained MLE step starts from it
+        return warn

@@ -147,6 +147,13 @@ def test_sharded_bench_equals_one_rank(name, flags, tmp_path):
     assert eight["config"]["share_device"] and eight["config"]["K"] == one["config"]["K"]
     assert eight["cg_iters_per_step"] == one["cg_iters_per_step"]
     assert one["config"]["cg_column_sets"] == eight["config"]["cg_column_sets"]
+    # the 8-rank line says where its exchange went: collectives per
+    # step, their time, the EM loop's exchange mode; one rank has no communicator
+    x1, x8 = one["exchange"], eight["exchange"]
+    assert x1["transport"] is None and x1["allgathers_per_step"] == 0 and x1["em_mode"] is None
+    assert x8["transport"] == "host" and x8["allgathers_per_step"] > 0 and x8["ms_per_step"] > 0
+    assert x8["em_mode"] == ("replicated" if x8["K_times_M"] <= x8["em_rep_max_km"] else "per-step")
+    _log(name, "eight-rank exchange", x8)
     files = sorted(f for f in os.listdir(tmp_path / "one") if f.endswith(".bin"))
     K = one["config"]["K"]
     assert len(files) == 3 * (K + 1)          # warmup + 2 steps: xhat and r1 per cohort
@@ -156,6 +163,67 @@ def test_sharded_bench_equals_one_rank(name, flags, tmp_path):
         assert len(a) == 8 * 1000000 and a == b, f
     for f in sorted(f for f in os.listdir(tmp_path / "one") if f.endswith(".csv")):
         assert (tmp_path / "one" / f).read_bytes() == (tmp_path / "eight" / f).read_bytes(), f
+
+
+def _gate_50(nblk, size, K, tmp_path, its=50):
+    """50 outer iterations of the HIP path against the CPU oracle on the same
+    inputs read back from the device (the bench's problem, prior and flags);
+    returns the per-iteration max relative xhat errors, the CG counts (GPU,
+    oracle) and EM steps (GPU, oracle)."""
+    sizes = [size] * nblk
+    eng = Engine(sizes, K=K, ld_of=[0] * K)
+    args = argparse.Namespace(seed=SEED, nsamp=NSAMP)
+    beta, _ = bench.make_problem(eng, eng.comm, args)
+    M, N = eng.M, NSAMP
+    cm = int(M * 0.5)
+    prior = dict(prior_vars=[0.0, 0.8 / cm * N / (N * K)], prior_probs=[0.5, 0.5])
+    x0 = beta * np.sqrt(N)
+    r_list = [eng.get_vector(hb.VEC_R, k) for k in range(K)]
+    L = _host_ld(eng, (nblk, size), nblk)
+    L.s = 0.0
+    v = VAMP(N=[N] * K, Nt=N * K, M=M, K=K, rho=0.5, gamw=5.0, gam1=1e-6, a=[1.0 / K] * K,
+             out_dir=str(tmp_path), out_name="gate50", seed=SEED, write_files=False, **prior)
+    v.attach_engine(eng, x0=x0)
+    run = dict(cg_maxit=500, em_prior_maxit=100, learn_gamw=True, lmmse_damp=False,
+               prior_update="em", update_prior_from=1)
+    xh = v.infer(None, None, its, x0=x0, **run)
+    hist = [(h["cg_iters"], h.get("em_steps")) for h in v.history]
+    eng.close()
+    _log("%dx%d K=%d: GPU %d iterations done" % (nblk, size, K, its))
+    t = vo.infer([L], [0] * K, r_list, [N] * K, its, rho=0.5, gamw=5.0, gam1=1e-6, x0=x0,
+                 seed=SEED, reducer=vo.Reducer("blocked", bounds=L.bounds), rs_recurrence=True,
+                 batched=True, **prior, **run)
+    errs = []
+    for it in range(its):
+        got = xh[it].ravel() / np.sqrt(N * K)
+        ref = np.asarray(t["xhat"][it])
+        assert np.isfinite(ref).all()
+        errs.append(maxrel(got, ref))
+    cg = ([list(map(list, h[0])) for h in hist], [list(map(list, x)) for x in t["cg_iters"]])
+    em = ([h[1] for h in hist][1:], list(t["em_steps"]))
+    same_cg = sum(a == b for a, b in zip(*cg))
+    same_em = sum(a == b for a, b in zip(*em))
+    _log("%dx%d K=%d %d it: max rel xhat err per iteration" % (nblk, size, K, its),
+         ["%.2e" % e for e in errs])
+    _log("%dx%d K=%d %d it: CG counts equal in %d/%d iterations, EM steps in %d/%d"
+         % (nblk, size, K, its, same_cg, its, same_em, its - 1))
+    _log("CG counts", cg[0])
+    return errs, cg, em
+
+
+@pytest.mark.timeout(900)
+def test_50_iterations_mid_size_vs_oracle(tmp_path):
+    """The north star's 50-iteration gate in the driver's suite, above toy size
+    (VERDICT round 3): 4 LD blocks of 12,500 markers (M = 50,000, each block
+    wider than the MFMA pass's strips of 8 panels), K = 4 cohorts sharing the LD
+    (8 CG columns: the f64 MFMA pass), rho 0.5, the bench's generator and prior.
+    Bar (BASELINE.json north_star): xhat within 1e-5 relative of the oracle,
+    asserted at every one of the 50 iterations; CG iteration counts and EM steps
+    equal at every iteration."""
+    errs, cg, em = _gate_50(4, 12500, 4, tmp_path)
+    assert max(errs) < 1e-5, max(errs)
+    assert cg[0] == cg[1]
+    assert em[0] == em[1]
 
 
 @pytest.mark.timeout(2400)
@@ -171,41 +239,5 @@ def test_north_star_50_iterations_vs_oracle(K, tmp_path):
     (BASELINE.json north_star): xhat within 1e-5 relative after 50 iterations;
     asserted at every iteration, with the CG iteration counts and EM steps
     compared per iteration."""
-    its = 50
-    sizes = [15625] * 64
-    eng = Engine(sizes, K=K, ld_of=[0] * K)
-    args = argparse.Namespace(seed=SEED, nsamp=NSAMP)
-    beta, _ = bench.make_problem(eng, eng.comm, args)
-    M, N = eng.M, NSAMP
-    cm = int(M * 0.5)
-    prior = dict(prior_vars=[0.0, 0.8 / cm * N / (N * K)], prior_probs=[0.5, 0.5])
-    x0 = beta * np.sqrt(N)
-    r_list = [eng.get_vector(hb.VEC_R, k) for k in range(K)]
-    L = _host_ld(eng, (64, 15625), 64)
-    L.s = 0.0
-    v = VAMP(N=[N] * K, Nt=N * K, M=M, K=K, rho=0.5, gamw=5.0, gam1=1e-6, a=[1.0 / K] * K,
-             out_dir=str(tmp_path), out_name="ns50", seed=SEED, write_files=False, **prior)
-    v.attach_engine(eng, x0=x0)
-    run = dict(cg_maxit=500, em_prior_maxit=100, learn_gamw=True, lmmse_damp=False,
-               prior_update="em", update_prior_from=1)
-    xh = v.infer(None, None, its, x0=x0, **run)
-    hist = [(h["cg_iters"], h.get("em_steps")) for h in v.history]
-    eng.close()
-    _log("K=%d: GPU 50 iterations done" % K)
-    t = vo.infer([L], [0] * K, r_list, [N] * K, its, rho=0.5, gamw=5.0, gam1=1e-6, x0=x0,
-                 seed=SEED, reducer=vo.Reducer("blocked", bounds=L.bounds), rs_recurrence=True,
-                 batched=True, **prior, **run)
-    errs = []
-    for it in range(its):
-        got = xh[it].ravel() / np.sqrt(N * K)
-        ref = np.asarray(t["xhat"][it])
-        assert np.isfinite(ref).all()
-        errs.append(maxrel(got, ref))
-    same_cg = sum(list(map(list, h[0])) == list(map(list, x))
-                  for h, x in zip(hist, t["cg_iters"]))
-    same_em = sum(a == b for a, b in zip([h[1] for h in hist][1:], t["em_steps"]))
-    _log("K=%d 50 it: max rel xhat err per iteration" % K, ["%.2e" % e for e in errs])
-    _log("K=%d 50 it: CG counts equal in %d/%d iterations, EM steps in %d/%d"
-         % (K, same_cg, its, same_em, its - 1))
-    _log("K=%d 50 it: CG counts" % K, [h[0] for h in hist])
+    errs, _, _ = _gate_50(64, 15625, K, tmp_path)
     assert max(errs) < 1e-5, max(errs)

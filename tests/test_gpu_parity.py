@@ -461,6 +461,41 @@ def test_step_driver_matches_phases(name, tmp_path, monkeypatch):
             np.testing.assert_array_equal(a_, b_)
 
 
+def test_mle_gam_carries_over_infer_calls(tmp_path, monkeypatch):
+    """Two infer() calls on one VAMP object, the second with a different R (a new
+    engine), MLE prior from iteration 1: the MLE step chained behind iteration 0
+    starts fsolve from the gam the first call left on the object, as the
+    reference's self.gam does (src/sgvamp.py:175-178,194) -- chained, unchained
+    and per-phase runs write byte-identical files and take the same MLE
+    outcomes (the chained step started from x0[-1] = 1)."""
+    c = Case("k1_mle")
+    f = c.flags
+    monkeypatch.setenv("SGV_AB", "1")
+    res = {}
+    for mode in ("phases", "nochain", ""):
+        monkeypatch.setenv("SGV_STEP", mode)
+        d = tmp_path / (mode or "chain")
+        d.mkdir()
+        v, _ = run_vamp_case(c, d)
+        gam_first = v.gam
+        # the same LD as a new object: _restart builds a new engine
+        R2 = BlockLD(c.ld_blocks[0], s=f["s"])
+        v.setup_io(str(d), c.name + "_2")
+        v.infer(R2, c.r, f["iterations"], x0=c.x0, cg_maxit=f["cg_maxit"],
+                em_prior_maxit=f["em_prior_maxit"], learn_gamw=f["learn_gamw"],
+                lmmse_damp=f["lmmse_damp"], prior_update="mle", update_prior_from=1)
+        files = sorted(p.name for p in d.iterdir())
+        res[mode] = ({p: (d / p).read_bytes() for p in files}, gam_first, v.gam,
+                     [(h.get("mle_warning"), h["cg_iters"]) for h in v.history])
+        v.engine.close()
+    assert res["phases"][1] is not None, "the first run's MLE must converge for this test"
+    for mode in ("nochain", ""):
+        assert res[mode][0].keys() == res["phases"][0].keys()
+        for p, b in res["phases"][0].items():
+            assert res[mode][0][p] == b, (mode, p)
+        assert res[mode][1:] == res["phases"][1:], mode
+
+
 def test_vamp_is_deterministic(tmp_path):
     c = Case("k2_shared")
     (tmp_path / "a").mkdir()

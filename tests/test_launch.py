@@ -163,6 +163,53 @@ def test_spawn_propagates_failure():
     assert time.monotonic() - t < 30                   # rank 0 was stopped, not waited for
 
 
+def test_rank_dying_in_a_collective_ends_the_job(tmp_path):
+    """A rank that dies mid-run while its peer waits in a collective: the parent
+    exits non-zero within a bounded time and leaves no rank blocked (the
+    waiting rank is stopped, not waited for)."""
+    code = ("import os, sys, time\n"
+            "sys.path.insert(0, %r)\n"
+            "from comm import world_from_env\n"
+            "c = world_from_env()\n"
+            "c.barrier()\n"
+            "open(os.path.join(%r, 'pid%%d' %% c.Get_rank()), 'w').write(str(os.getpid()))\n"
+            "if c.Get_rank() == 1:\n"
+            "    os._exit(7)\n"
+            "time.sleep(0.5)\n"
+            "c.allgather(b'x')\n"
+            "time.sleep(600)\n") % (os.path.join(ROOT, "sgvamp-py_amd"), str(tmp_path))
+    t = time.monotonic()
+    rc = launch.spawn(2, [sys.executable, "-c", code], base=_clean_env())
+    assert rc == 7
+    assert time.monotonic() - t < 60
+    for r in range(2):
+        pid = int((tmp_path / ("pid%d" % r)).read_text())
+        with pytest.raises(ProcessLookupError):
+            os.kill(pid, 0)
+
+
+def test_sigterm_to_parent_stops_every_rank(tmp_path):
+    """a SIGTERM to the self-launching parent alone (a scheduler
+    or `timeout` signalling its PID) stops the N ranks before the parent exits
+    (128 + 15), instead of leaving them holding their GPUs and the port."""
+    child = ("import os, time; open(os.path.join(%r, 'pid' + os.environ['RANK']), 'w')"
+             ".write(str(os.getpid())); time.sleep(600)") % str(tmp_path)
+    parent = ("import sys; sys.path.insert(0, %r); import launch; "
+              "sys.exit(launch.spawn(2, [sys.executable, '-c', %r]))") % (
+                  os.path.join(ROOT, "sgvamp-py_amd"), child)
+    p = subprocess.Popen([sys.executable, "-c", parent], env=_clean_env())
+    deadline = time.monotonic() + 60
+    while time.monotonic() < deadline and not all(
+            (tmp_path / ("pid%d" % r)).exists() for r in range(2)):
+        time.sleep(0.1)
+    pids = [int((tmp_path / ("pid%d" % r)).read_text()) for r in range(2)]
+    p.send_signal(15)
+    assert p.wait(timeout=60) == 128 + 15
+    for pid in pids:
+        with pytest.raises(ProcessLookupError):
+            os.kill(pid, 0)
+
+
 # ---- host communicator hardening ----------------------------------------------------------
 
 def test_codec_roundtrip_and_refusals():
@@ -211,3 +258,22 @@ def test_rendezvous_drops_stray_and_unauthenticated_peers():
     stray.close()
     impostor.close()
     assert out[0] == [0, 10] and out[1] == [0, 10], out
+
+
+def test_env_launch_requires_rank_and_local_rank():
+    """a RANK/WORLD_SIZE launch without RANK is refused (every
+    process would be rank 0); LOCAL_RANK falls back to the global rank only on a
+    one-node world (LOCAL_WORLD_SIZE == WORLD_SIZE, or no LOCAL_WORLD_SIZE and
+    the ranks meeting on this host)."""
+    import comm as cm
+
+    with pytest.raises(RuntimeError, match="RANK is not set"):
+        cm.launch_from_env(dict(WORLD_SIZE="2", LOCAL_RANK="0"))
+    assert cm.launch_from_env(dict(WORLD_SIZE="1"))["rank"] == 0
+    one = cm.launch_from_env(dict(RANK="1", WORLD_SIZE="2", LOCAL_WORLD_SIZE="2"))
+    assert one["local_rank"] == 1
+    assert cm.launch_from_env(dict(RANK="1", WORLD_SIZE="2", MASTER_ADDR="127.0.0.1"))["local_rank"] == 1
+    with pytest.raises(RuntimeError, match="LOCAL_RANK"):     # two nodes of 4 GPUs
+        cm.launch_from_env(dict(RANK="5", WORLD_SIZE="8", LOCAL_WORLD_SIZE="4", MASTER_ADDR="10.0.0.5"))
+    with pytest.raises(RuntimeError, match="LOCAL_RANK"):     # remote rendezvous, node size unknown
+        cm.launch_from_env(dict(RANK="5", WORLD_SIZE="8", MASTER_ADDR="10.0.0.5"))

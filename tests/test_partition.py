@@ -94,3 +94,18 @@ def test_coarsen_blocks_merges_tiny_blocks():
     assert coarsen_blocks([60, 70, 5]) == [135]
     assert coarsen_blocks([5] * 10) == [50]
     assert coarsen_blocks([]) == []
+
+
+def test_cg_exact_mode_from_stored_bytes():
+    """The run's CG column-set mode (engine.cg_exact_from_stored):
+    decided by the bytes the shared LD actually stores, so a banded LD whose
+    block sizes alone would suggest >= 24 GB keeps the look-ahead; a matrix used
+    by one cohort (2 columns: the VALU pass) never narrows."""
+    from engine import cg_exact_from_stored, cg_exact_mode
+
+    assert cg_exact_mode([15625] * 64) == 1                      # north star: 63.5 GB triangle
+    assert cg_exact_mode([1_000_000]) == 1                       # one 1e6 block by size ...
+    assert cg_exact_from_stored([10.2e9], [0, 0, 0, 0]) == 0     # ... but a bw=1000 band stores 10 GB
+    assert cg_exact_from_stored([63.5e9], [0, 0, 0, 0]) == 1
+    assert cg_exact_from_stored([63.5e9, 1e9], [0, 1]) == 0      # distinct LD: 2 columns per matrix
+    assert cg_exact_from_stored([1e9, 30e9], [0, 0, 1, 1]) == 1
