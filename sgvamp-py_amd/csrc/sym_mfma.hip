@@ -71,6 +71,77 @@ __device__ __forceinline__ void lds_order() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// The row fragment is the column fragment with lane bits (5,4) and (1,0)
+// exchanged, register for register: rf[r] at lane 16 h + 4 b + n = cf[r] at lane
+// 16 n + 4 b + h.  Besides the LDS tile (XP = 0) two register-only forms
+// (A/B, SGV_MF_XPOSE):
+// XP = 1: permlane32/16_swap exchange lane bits 5 / 4 with the register bits of
+//   r (1 / 0), quad DPP moves + selects exchange lane bits 1 / 0 with them, and
+//   a second permlane pass puts r back: (L54 r)(L10 r)(L54 r) = (L54 L10);
+//   16 + 32 + 16 swaps / selects (+ 32 DPP moves) per 4-KiB step, no LDS.
+// XP = 2: ds_bpermute_b32 (the LDS crossbar, no LDS storage), 16 per step.
+__device__ __forceinline__ void xp_p32(unsigned& x, unsigned& y) {
+  const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+  x = r[0];
+  y = r[1];
+}
+__device__ __forceinline__ void xp_p16(unsigned& x, unsigned& y) {
+  const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+  x = r[0];
+  y = r[1];
+}
+// lane bit `B` (0 or 1) <-> the register bit distinguishing x (0) from y (1)
+template <int B>
+__device__ __forceinline__ void xp_quad(unsigned& x, unsigned& y, bool sel) {
+  constexpr int CTRL = B == 0 ? 0xB1 : 0x4E;   // quad_perm [1,0,3,2] / [2,3,0,1]
+  const unsigned dx = (unsigned)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, true);
+  const unsigned dy = (unsigned)__builtin_amdgcn_mov_dpp((int)y, CTRL, 0xF, 0xF, true);
+  const unsigned nx = sel ? dy : x;
+  y = sel ? y : dx;
+  x = nx;
+}
+__device__ __forceinline__ void xp_rows(unsigned (&v)[4]) {   // (L5 r1)(L4 r0)
+  xp_p32(v[0], v[2]);
+  xp_p32(v[1], v[3]);
+  xp_p16(v[0], v[1]);
+  xp_p16(v[2], v[3]);
+}
+__device__ __forceinline__ void xpose_perm(const d2* cf, d2* rf, bool l1, bool l0) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {   // the 4 dwords of a d2, each over the 4 registers
+    unsigned v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const unsigned long long u = __builtin_bit_cast(unsigned long long, cf[r][e >> 1]);
+      v[r] = (unsigned)(e & 1 ? u >> 32 : u);
+    }
+    xp_rows(v);
+    xp_quad<1>(v[0], v[2], l1);
+    xp_quad<1>(v[1], v[3], l1);
+    xp_quad<0>(v[0], v[1], l0);
+    xp_quad<0>(v[2], v[3], l0);
+    xp_rows(v);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      unsigned long long u = __builtin_bit_cast(unsigned long long, rf[r][e >> 1]);
+      u = e & 1 ? ((u & 0xFFFFFFFFull) | ((unsigned long long)v[r] << 32))
+                : ((u & 0xFFFFFFFF00000000ull) | v[r]);
+      rf[r][e >> 1] = __builtin_bit_cast(double, u);
+    }
+  }
+}
+__device__ __forceinline__ void xpose_bperm(const d2* cf, d2* rf, int src4) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const unsigned long long u = __builtin_bit_cast(unsigned long long, cf[r][e]);
+      const unsigned lo32 = (unsigned)__builtin_amdgcn_ds_bpermute(src4, (int)(unsigned)u);
+      const unsigned hi32 = (unsigned)__builtin_amdgcn_ds_bpermute(src4, (int)(unsigned)(u >> 32));
+      rf[r][e] = __builtin_bit_cast(double, (unsigned long long)lo32 | ((unsigned long long)hi32 << 32));
+    }
+}
+
 constexpr int MF_CW = 512;   // chunk width (class 1 items)
 constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conflict-free both ways
 
@@ -92,7 +163,7 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // its column MFMAs, so consecutive MFMAs of one accumulator chain sit 8 issues
 // apart instead of 4 (2 at NG = 1); every chain accumulates in the same order
 // (bitwise the same sums), the row fragments are double-buffered in registers.
-template <int NG, int NW, int PD, bool PW, bool SKIP, bool RAG = false, bool DEF = false>
+template <int NG, int NW, int PD, bool PW, bool SKIP, bool RAG = false, bool DEF = false, int XP = 0>
 __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
                                                          const SymItem* __restrict__ sitems,
                                                          const double* __restrict__ pk, int ncol,
@@ -114,7 +185,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   // sums and the tiles fit two workgroups per CU) and conflict-free both ways:
   // a write's 16-lane quarter covers one row, a row-fragment read's quarter
   // (rows 4q + (l & 3), pairs 4((l >> 2) & 3) + (l >> 4)) 16 distinct slots mod 16
-  __shared__ __attribute__((aligned(16))) double stg[NW][16 * 32];
+  __shared__ __attribute__((aligned(16))) double stg[XP == 0 ? NW : 1][16 * 32];
   double* rbuf = rowbuf + 2 * NW * 256;
   const SymStrip sp = strips[blockIdx.x];
   if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
@@ -136,7 +207,9 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   // diagonal-block waves of a diagonal panel (B = 0 there).  The loads stay, so
   // the load count is the same on every path.
   const int nta = SKIP ? min(NT, max(0, (ncc - cw0 + 31) / 32)) : NT;
-  double* sb = stg[wid];
+  double* sb = stg[XP == 0 ? wid : 0];
+  const bool xl1 = (lane & 2) != 0, xl0 = (lane & 1) != 0;   // XP = 1: quad lane bits
+  const int xsrc4 = 4 * (16 * n4 + 4 * bq + hi);               // XP = 2: source lane x 4
 
   // row-part B operands: P at this wave's columns, reused by every row group
   double brow[NT][2][NG];
@@ -256,14 +329,20 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
         }
         if (t >= nta) continue;                        // wave-uniform: past the chunk
         if (RAG && cur.nc < ncc) band_zero(cur.nc, t, cf);   // uniform: a band item's stored end
-        lds_order();                                   // previous step's tile reads issued
+        if constexpr (XP == 1) {
+          xpose_perm(cf, rf, xl1, xl0);
+        } else if constexpr (XP == 2) {
+          xpose_bperm(cf, rf, xsrc4);
+        } else {
+          lds_order();                                 // previous step's tile reads issued
 #pragma unroll
-        for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[a];
-        lds_order();                                   // tile written
-        // the row fragment reads go out right behind the writes (a wave's DS
-        // operations execute in order); the column MFMAs cover their latency
+          for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[a];
+          lds_order();                                 // tile written
+          // the row fragment reads go out right behind the writes (a wave's DS
+          // operations execute in order); the column MFMAs cover their latency
 #pragma unroll
-        for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
+          for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
+        }
         // the MFMA burst at raised wave priority: the SIMD's other wave, whose
         // loads are in flight, takes the issue slots back when this one drains
         // (NC = 4/8 0.7-1.5 % faster per pass on two boxes; NC = 16 1 % slower,
@@ -678,6 +757,16 @@ static int mf16_pd() {
   return v;
 }
 
+// SGV_MF_XPOSE (A/B, with SGV_AB=1): the row fragment's transpose -- default 0
+// through the per-wave LDS tile, 1 permlane swaps + quad DPP, 2 ds_bpermute
+static int mf_xpose() {
+  static const int v = [] {
+    const char* e = ab_env("SGV_MF_XPOSE");
+    return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
+  }();
+  return v;
+}
+
 // ragged: some strip item stops short of its strip's widest (band blocks): the
 // RAG kernels (default variant only: the A/B switches do not apply there)
 template <int NG, int NW, int PD>
@@ -687,6 +776,12 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
   if (ragged)
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, true>), dim3(nstrips), dim3(NW * 64), 0,
                        st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (mf_pw() && mf_skip() && mf_defer() && mf_xpose() == 1)
+    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, false, true, 1>), dim3(nstrips),
+                       dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (mf_pw() && mf_skip() && mf_defer() && mf_xpose() == 2)
+    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, false, true, 2>), dim3(nstrips),
+                       dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else if (mf_pw() && mf_skip() && mf_defer())
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, false, true>), dim3(nstrips),
                        dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);

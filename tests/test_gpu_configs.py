@@ -212,15 +212,17 @@ def _gate_50(nblk, size, K, tmp_path, its=50):
 
 
 @pytest.mark.timeout(900)
-def test_50_iterations_mid_size_vs_oracle(tmp_path):
+@pytest.mark.parametrize("nblk,size", [(4, 12500), (8, 25000)])
+def test_50_iterations_mid_size_vs_oracle(nblk, size, tmp_path):
     """The north star's 50-iteration gate in the driver's suite, above toy size
     (VERDICT round 3): 4 LD blocks of 12,500 markers (M = 50,000, each block
-    wider than the MFMA pass's strips of 8 panels), K = 4 cohorts sharing the LD
-    (8 CG columns: the f64 MFMA pass), rho 0.5, the bench's generator and prior.
+    wider than the MFMA pass's strips of 8 panels) and C3's full problem (8 x
+    25,000, M = 200,000), K = 4 cohorts sharing the LD (8 CG columns: the f64
+    MFMA pass), rho 0.5, the bench's generator and prior.
     Bar (BASELINE.json north_star): xhat within 1e-5 relative of the oracle,
     asserted at every one of the 50 iterations; CG iteration counts and EM steps
     equal at every iteration."""
-    errs, cg, em = _gate_50(4, 12500, 4, tmp_path)
+    errs, cg, em = _gate_50(nblk, size, 4, tmp_path)
     assert max(errs) < 1e-5, max(errs)
     assert cg[0] == cg[1]
     assert em[0] == em[1]
