@@ -64,6 +64,7 @@ struct LdPlan {
   SymPanel* d_spanels = nullptr;
   int nstrips = 0;
   bool ragged = false;         // some strip item is narrower than its strip (band blocks)
+  bool pair = false;           // NC <= 8 passes run k_sym_mfma_pair (build_strips)
   double stored_bytes = 0.0, dense_bytes = 0.0;
 };
 
@@ -696,6 +697,53 @@ static int mfma_strip_len() {
   return std::max(1, std::min(64, v));
 }
 
+// Longest-processing-time makespan of `cost` on `slots` identical slots, as a
+// fraction of the perfect split (the dispatcher hands the strips out in this
+// order, most panels first, to whichever slot frees first)
+static double lpt_efficiency(std::vector<double> cost, int slots) {
+  std::sort(cost.begin(), cost.end(), std::greater<double>());
+  std::vector<double> load((size_t)slots, 0.0);
+  double tot = 0.0;
+  for (double x : cost) {
+    auto it = std::min_element(load.begin(), load.end());
+    *it += x;
+    tot += x;
+  }
+  const double mk = *std::max_element(load.begin(), load.end());
+  return mk > 0.0 ? tot / slots / mk : 1.0;
+}
+
+// NC <= 8 MFMA passes: the 4-wave kernel (two 4-wave workgroups per CU, 512
+// slots) or the wave-pair kernel (one 8-wave workgroup per CU, a strip in half
+// the time: 256 slots at half the cost) -- bitwise the same products, so the
+// choice is free per plan.  Auto: the pair kernel when its launch drains with
+// at least SGV_MF_PAIR_GAIN (default 3 %) less tail by the strips' model cost
+// (a few strips per slot: an 8-block share of the north star); SGV_MF_PAIR=0/1
+// (with SGV_AB=1) forces either.
+static bool mfma_pair_choice(const std::vector<SymStrip>& strips,
+                             const std::vector<SymItem>& sitems) {
+  const char* e = ab_env("SGV_MF_PAIR");
+  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+      ncu = prop.multiProcessorCount;
+  }
+  std::vector<double> cost;
+  cost.reserve(strips.size());
+  for (const SymStrip& st : strips) {
+    double x = 0.0;
+    for (int i = 0; i < st.npan; ++i) x += (double)sitems[st.it0 + i].H / SYM_H;
+    cost.push_back(x * (double)st.ncmax / 512.0);
+  }
+  const double quad = lpt_efficiency(cost, 2 * ncu);
+  const double pair = lpt_efficiency(cost, ncu);   // per slot: twice the speed, same ratio
+  const char* g = std::getenv("SGV_MF_PAIR_GAIN");
+  const double gain = g && *g ? std::atof(g) : 0.03;
+  return pair >= quad + gain;
+}
+
 // MFMA strips of one LD matrix from the class-1 (512-column) tables.  Chunk
 // (parity p, c0 = 256 p + 512 k) of a block holds the items (g, c0) of panels
 // g = p, p + 2, ..., G = c0 / 256 (the diagonal panel); they are cut into strips
@@ -767,6 +815,7 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
   pl->ragged = false;
   for (const SymStrip& st : strips)
     for (int i = 0; i < st.npan; ++i) pl->ragged |= sitems[st.it0 + i].nc < st.ncmax;
+  pl->pair = !pl->ragged && mfma_pair_choice(strips, sitems);
   CHK(upload_table(c, strips, &pl->d_strips));
   CHK(upload_table(c, sitems, &pl->d_sitems));
   CHK(upload_table(c, sp, &pl->d_spanels));
@@ -896,7 +945,7 @@ static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa) {
     const int cls = mf ? 1 : sym_class(nc);
     if (mf) {
       HIPCHK(launch_sym_mfma(nc, pl.d_strips, pl.nstrips, pl.d_sitems, pa, c->Mpad, c->d_pk,
-                             c->d_rowpart, c->d_colpart, pl.ragged, c->st));
+                             c->d_rowpart, c->d_colpart, pl.ragged, pl.pair, c->st));
       HIPCHK(launch_sym_finalize_strip(nc, pl.d_spanels, pl.npanels, pa, c->d_rowpart,
                                        c->d_colpart, c->d_part, c->st));
       c->aux_bytes += 2.0 * 8.0 * nc * ((double)pl.nitems[cls] * SYM_H + (double)pl.nstrips * 512);

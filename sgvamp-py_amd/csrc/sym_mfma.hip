@@ -142,6 +142,12 @@ __device__ __forceinline__ void xpose_bperm(const d2* cf, d2* rf, int src4) {
     }
 }
 
+// SGV_BAND_SKIP=0 (A/B, with SGV_AB=1; read by the host at launch and passed
+// in the strip flags would cost a register -- a device constant is enough):
+// band strips' all-zero steps run their MFMAs as before
+__constant__ int c_band_rag_skip = 1;
+__device__ __forceinline__ bool band_rag_skip() { return c_band_rag_skip != 0; }
+
 constexpr int MF_CW = 512;   // chunk width (class 1 items)
 constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conflict-free both ways
 
@@ -328,6 +334,10 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
           if (t + PD == NT) load_bcol(gr0, gH, gz, gn, bcn);
         }
         if (t >= nta) continue;                        // wave-uniform: past the chunk
+        // a band item narrower than its strip (its panel's last 256 columns):
+        // a step wholly past its stored end adds only zeros -- skipped like the
+        // steps past the chunk (band_rag_skip, default on)
+        if (RAG && cw0 + 32 * t >= cur.nc && band_rag_skip()) continue;
         if (RAG && cur.nc < ncc) band_zero(cur.nc, t, cf);   // uniform: a band item's stored end
         if constexpr (XP == 1) {
           xpose_perm(cf, rf, xl1, xl0);
@@ -489,6 +499,258 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   MF_TRACE_END
 }
 
+// Wave-pair form of k_sym_mfma (PW, SKIP; no band items): one 8-wave workgroup
+// per strip, TWO waves per 128-column segment, each owning 64 columns (two
+// 32-column steps).  Every sum is the 4-wave kernel's, bit for bit:
+//  * a column's sum is one MFMA chain over the strip's rows in one wave, as
+//    there (its wave only changed);
+//  * a row's sum over a segment is the chain x0 y0 x1 y1 x2 y2 x3 y3 over the
+//    segment's four steps: the first wave of the pair runs steps 0-1 from zero
+//    and hands its accumulators (4 NG doubles per lane) through LDS to the
+//    second, which continues with steps 2-3 -- the same MFMAs in the same order
+//    -- then reduces the 4 blocks (DPP) and keeps the segment's panel row sums
+//    (wrow), added over the 4 segments in order per panel as there.
+// So a strip takes half the time on a workgroup holding a whole CU (8 waves, 1
+// per CU: the same 2 waves per SIMD): a launch whose strips are few per slot
+// (an 8-block share: ~2 strips of up to 8 panels per slot of the 4-wave form)
+// drains with half the tail, with products identical to the 4-wave kernel's --
+// the form can be chosen per partition.  One barrier per 16-row group: the
+// hand-off (first wave: accumulators out before it; second wave: in after it,
+// double-buffered by row-group parity).
+// MAP 0: waves 2s, 2s + 1 hold segment s (the pair on two SIMDs); MAP 1: waves
+// s, s + 4 (waves are dealt to SIMDs round-robin: the pair shares one SIMD, each
+// SIMD runs one first and one second half)
+template <int NG, int PD, int XP, int MAP = 0>
+__global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __restrict__ strips,
+                                                          const SymItem* __restrict__ sitems,
+                                                          const double* __restrict__ pk, int ncol,
+                                                          double* __restrict__ rowpart,
+                                                          double* __restrict__ colpart,
+                                                          const int* __restrict__ run, int pks) {
+  constexpr int NW = 8;
+  constexpr int WC = 64;           // columns per wave
+  constexpr int NT = WC / 32;      // 32-column steps per wave
+  static_assert(PD >= 1 && PD <= NT && NT % PD == 0, "prefetch depth divides the steps");
+  constexpr int RW = 4 * NG;
+  __shared__ __attribute__((aligned(16))) double wrow[4 * SYM_H * RW];   // [segment][row][4 NG]
+  __shared__ __attribute__((aligned(16))) double hand[2][4][4 * NG][WAVE];   // [gg & 1][segment][r, q][lane]
+  __shared__ __attribute__((aligned(16))) double stg[XP == 0 ? NW : 1][16 * 32];
+  const SymStrip sp = strips[blockIdx.x];
+  if (run && !ldg(run)) return;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+  const int seg = MAP ? (wid & 3) : (wid >> 1);        // 128-column segment
+  const int h = MAP ? (wid >> 2) : (wid & 1);            // half
+  const int lo = lane & 15, hi = lane >> 4, bq = (lane >> 2) & 3, n4 = lane & 3;
+  const int pc = hi + 4 * bq;
+  SymItem cur = sitems[sp.it0];
+  const int c0 = cur.c0, ncc = sp.ncmax;
+  const int PKS = pks;
+  const double* pkb = pk + (int64_t)cur.voff * PKS;
+  const int cw0 = seg * 128 + h * WC;                    // first chunk column of this wave
+  const bool dhalf = seg * 128 < SYM_H;                  // the 4-wave kernel's wave `seg`
+  // the segment's active 32-column steps (the 4-wave kernel's nta), this wave's share
+  const int nta_seg = min(4, max(0, (ncc - seg * 128 + 31) / 32));
+  const int nta = min(NT, max(0, nta_seg - NT * h));
+  double* sb = stg[XP == 0 ? wid : 0];
+  const bool xl1 = (lane & 2) != 0, xl0 = (lane & 1) != 0;
+  const int xsrc4 = 4 * (16 * n4 + 4 * bq + hi);
+
+  double brow[NT][2][NG];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int col = cw0 + 32 * t + 2 * pc + e;
+#pragma unroll
+      for (int q = 0; q < NG; ++q) {
+        const double v = ldg(pkb + (int64_t)(c0 + (col < ncc ? col : 0)) * PKS + 4 * q + n4);
+        brow[t][e][q] = col < ncc ? v : 0.0;
+      }
+    }
+  double dcol[NT][2][NG];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int q = 0; q < NG; ++q) dcol[t][e][q] = 0.0;
+
+  auto load_cf = [&](uint64_t b0, int64_t ws, int H, int g, int t, d2* cf) {
+    asm volatile("" : "+s"(b0));
+    const int xc = cw0 + 32 * t + 2 * lo;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int rB = 16 * g + 4 * a + hi;
+      const double* row = (const double*)b0 + (int64_t)(rB < H ? rB : H - 1) * ws;
+      cf[a] = ldg_nt((const d2*)(row + (xc < ncc ? xc : 0)));
+    }
+  };
+  auto load_bcol = [&](int r0, int H, bool zero, int g, double (*bc)[NG]) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int rB = 16 * g + 4 * a + hi;
+#pragma unroll
+      for (int q = 0; q < NG; ++q) {
+        const double v = ldg(pkb + (int64_t)(r0 + (rB < H ? rB : 0)) * PKS + 4 * q + n4);
+        bc[a][q] = (rB < H && !zero) ? v : 0.0;
+      }
+    }
+  };
+  auto pbase = [&](const SymItem& x) { return (uint64_t)(x.P + (x.c0 - x.r0)); };
+
+  uint64_t curb = pbase(cur);
+  d2 cfq[PD][4];
+  double bcn[4][NG];
+#pragma unroll
+  for (int p = 0; p < PD; ++p) load_cf(curb, cur.w, cur.H, 0, p, cfq[p]);
+  load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
+
+  int gg = 0;
+#pragma unroll 1
+  for (int s = 0; s < sp.npan; ++s) {
+    const bool more = s + 1 < sp.npan;
+    const SymItem nx = sitems[sp.it0 + (more ? s + 1 : s)];
+    const uint64_t nxb = more ? pbase(nx) : (uint64_t)pkb;
+    const int ng = (cur.H + 15) / 16;
+#pragma unroll 1
+    for (int g = 0; g < ng; ++g, ++gg) {
+      const bool same = g + 1 < ng;
+      const uint64_t gb = same ? curb : nxb;
+      const int64_t gw = same ? cur.w : (more ? nx.w : 0);
+      const int gH = same ? cur.H : (more ? nx.H : 1);
+      const int gn = same ? g + 1 : 0;
+      const int gr0 = same ? cur.r0 : nx.r0;
+      const bool gz = dhalf && gr0 == c0;
+      double bcol[4][NG];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int q = 0; q < NG; ++q) bcol[a][q] = bcn[a][q];
+      double drow[4][NG];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < NG; ++q) drow[r][q] = 0.0;
+      const bool colz = dhalf && cur.r0 == c0;
+      d2 rfs[NT][4];                                     // h = 1: row fragments, used after the hand-off
+      auto row_mfma = [&](const d2* f, int tt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(f[r].x, brow[tt][0][q], drow[r][q]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(f[r].y, brow[tt][1][q], drow[r][q]);
+      };
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        d2 cf[4];
+        const int slot = t % PD;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) cf[a] = cfq[slot][a];
+        if (t + PD < NT) {
+          load_cf(curb, cur.w, cur.H, g, t + PD, cfq[slot]);
+        } else {
+          load_cf(gb, gw, gH, gn, t + PD - NT, cfq[slot]);
+          if (t + PD == NT) load_bcol(gr0, gH, gz, gn, bcn);
+        }
+        if (t >= nta) continue;
+        d2* rf = rfs[t];
+        if constexpr (XP == 1) {
+          xpose_perm(cf, rf, xl1, xl0);
+        } else if constexpr (XP == 2) {
+          xpose_bperm(cf, rf, xsrc4);
+        } else {
+          lds_order();
+#pragma unroll
+          for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[a];
+          lds_order();
+#pragma unroll
+          for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
+        }
+        __builtin_amdgcn_s_setprio(1);
+        if (!colz) {
+#pragma unroll
+          for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int q = 0; q < NG; ++q) {
+              dcol[t][0][q] = MFMA4(cf[a].x, bcol[a][q], dcol[t][0][q]);
+              dcol[t][1][q] = MFMA4(cf[a].y, bcol[a][q], dcol[t][1][q]);
+            }
+        }
+        if (h == 0) row_mfma(rf, t);                     // the chain's first half
+        __builtin_amdgcn_s_setprio(0);
+      }
+      double* hs = &hand[gg & 1][seg][0][0];
+      if (h == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < NG; ++q) hs[(r * NG + q) * WAVE + lane] = drow[r][q];
+      }
+      __syncthreads();   // hand-off of row group gg (and the last group's reads of gg - 2)
+      if (h == 1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < NG; ++q) drow[r][q] = hs[(r * NG + q) * WAVE + lane];
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          if (t < nta) row_mfma(rfs[t], t);             // the chain's second half
+        __builtin_amdgcn_s_setprio(0);
+        double* wb = wrow + (seg * SYM_H + 16 * g) * RW;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < NG; ++q) {
+            double v = drow[r][q];
+            v = v + row_ror<12>(v);
+            v = v + row_ror<8>(v);
+            if (bq == 0) wb[(4 * r + hi) * RW + 4 * q + n4] = v;
+          }
+      }
+    }
+    {   // the item's H x ncol row sums: segments in order, contiguous in rowpart
+      __syncthreads();
+      const int n = cur.H * ncol;
+      double* dst = rowpart + (int64_t)cur.item * SYM_H * ncol;
+      for (int i = threadIdx.x; 2 * i < n; i += NW * 64) {
+        double v[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int k = 2 * i + e < n ? 2 * i + e : 2 * i;
+          const int row = k / ncol, cc = k - row * ncol;
+          const double* src = wrow + row * RW + cc;
+          double x = src[0];
+#pragma unroll
+          for (int w = 1; w < 4; ++w) x += src[w * SYM_H * RW];
+          v[e] = x;
+        }
+        if (2 * i + 1 < n)
+          *(d2*)(dst + 2 * i) = d2{v[0], v[1]};
+        else
+          dst[2 * i] = v[0];
+      }
+      __syncthreads();
+    }
+    cur = nx;
+    curb = nxb;
+  }
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    const int cc = 4 * q + n4;
+    if (cc < ncol) {
+      double* out = colpart + ((int64_t)sp.slot * ncol + cc) * MF_CW;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        *(d2*)(out + cw0 + 32 * t + 2 * pc) = d2{dcol[t][0][q], dcol[t][1][q]};
+    }
+  }
+}
+
 // 13..16 right-hand sides: v_mfma_f64_16x16x4f64 (one 16-column group, 140
 // cycles per 16x16x4) keeps fewer accumulators and B operands in registers
 // than four 4x4x4 groups, which spill at 4 waves.  Same strips as above:
@@ -611,6 +873,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
           if (t + PD == MF_NT) load_bcol(gr0, gH, gz, gn, bcn);
         }
         if (t >= nta) continue;
+        if (RAG && cw0 + 32 * t >= cur.nc && band_rag_skip()) continue;   // as k_sym_mfma
         if (RAG && cur.nc < ncc) band_zero(cur.nc, t, cf);
         lds_order();                                   // previous step's tile reads done
 #pragma unroll
@@ -767,15 +1030,30 @@ static int mf_xpose() {
   return v;
 }
 
+// SGV_MF_PAIR_MAP (A/B, with SGV_AB=1): k_sym_mfma_pair's wave map, default 0
+static int mf_pair_map() {
+  static const int v = [] {
+    const char* e = ab_env("SGV_MF_PAIR_MAP");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return v;
+}
+
 // ragged: some strip item stops short of its strip's widest (band blocks): the
 // RAG kernels (default variant only: the A/B switches do not apply there)
 template <int NG, int NW, int PD>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
-                      const int* run, int pks, bool ragged, hipStream_t st) {
+                      const int* run, int pks, bool ragged, bool pair, hipStream_t st) {
   if (ragged)
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, true>), dim3(nstrips), dim3(NW * 64), 0,
                        st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (pair && mf_pair_map() == 1)
+    hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0, 1>), dim3(nstrips), dim3(512), 0, st, d_strips,
+                       d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (pair)   // the plan's choice (capi.hip build_strips): bitwise the same products
+    hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0>), dim3(nstrips), dim3(512), 0, st, d_strips,
+                       d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else if (mf_pw() && mf_skip() && mf_defer() && mf_xpose() == 1)
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, false, true, 1>), dim3(nstrips),
                        dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
@@ -798,8 +1076,15 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
 
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                            const PassArgs& pa, int64_t mpad, double* d_pk, double* rowpart,
-                           double* colpart, bool ragged, hipStream_t st) {
+                           double* colpart, bool ragged, bool pair, hipStream_t st) {
   if (nc < 1 || nc > 16) return hipErrorInvalidValue;
+  static const hipError_t band_skip_set = [] {   // SGV_BAND_SKIP=0: the A/B's old band steps
+    const char* e = ab_env("SGV_BAND_SKIP");
+    if (!(e && e[0] == '0')) return hipSuccess;
+    const int zero = 0;
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_band_rag_skip), &zero, sizeof zero);
+  }();
+  if (band_skip_set != hipSuccess) return band_skip_set;
   // SGV_PK16=1 (A/B, SGV_AB=1): the round-2 16-column Pk rows for every NC
   static const bool pk16 = [] {
     const char* e = ab_env("SGV_PK16");
@@ -822,8 +1107,8 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
   // measured in DESIGN.md
   switch ((nc + 3) / 4) {
     // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
-    case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, st); break;
-    case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, st); break;
+    case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
+    case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
     default:
       if (ragged)
         hipLaunchKernelGGL((k_sym_mfma16<1, true, true>), dim3(nstrips), dim3(256), 0, st, d_strips,

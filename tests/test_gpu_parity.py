@@ -706,6 +706,36 @@ def test_mfma_strips_vs_numpy(strip, ncol, monkeypatch):
     eng.close()
 
 
+@pytest.mark.parametrize("strip", [3, 8])
+def test_mfma_pair_kernel_bitwise(strip, monkeypatch):
+    """The wave-pair MFMA kernel (k_sym_mfma_pair: two waves per 128-column
+    segment, the row chains handed from one to the other through LDS) gives
+    products bitwise identical to the 4-wave kernel's for 3-8 columns -- which
+    is what lets a plan pick either by its launch tail -- and both match numpy."""
+    monkeypatch.setenv("SGV_AB", "1")
+    monkeypatch.setenv("SGV_MFMA_STRIP", str(strip))
+    sizes = [5000, 513, 2600, 1, 4097]
+    blocks = rand_blocks(sizes, seed=strip, symmetric=True)
+    L = vo.BlockLD(blocks, s=0.1)
+    out = {}
+    for form in ("0", "1"):
+        monkeypatch.setenv("SGV_MF_PAIR", form)
+        eng = Engine(sizes, K=1)
+        for b, B in enumerate(blocks):
+            eng.set_ld_block(0, b, B)
+        eng.set_ridge(0.1)
+        out[form] = {}
+        for ncol in range(3, 9):
+            V = np.random.RandomState(ncol).normal(size=(ncol, sum(sizes)))
+            out[form][ncol] = eng.ld_matvec(0, V)
+        eng.close()
+    for ncol in range(3, 9):
+        np.testing.assert_array_equal(out["1"][ncol], out["0"][ncol])
+        V = np.random.RandomState(ncol).normal(size=(ncol, sum(sizes)))
+        for j in range(ncol):
+            assert maxrel(out["1"][ncol][j], L.matvec_Rs(V[j])) < 1e-12, (ncol, j)
+
+
 def _infer_again(v, c, out_dir):  # noqa: ARG001
     f = c.flags
     lds = [BlockLD(blocks, s=f["s"]) for blocks in c.ld_blocks]
