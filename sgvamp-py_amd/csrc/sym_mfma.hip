@@ -36,6 +36,7 @@
 // order).
 // Dcol accumulates over all rows of the strip in registers; every order is fixed.
 #include "common.h"
+#include "xpose.h"
 
 namespace sgv {
 
@@ -69,77 +70,6 @@ __device__ unsigned long long g_mf_trace[3 * MF_TRACE_MAX];
 __device__ __forceinline__ void lds_order() {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
-}
-
-// The row fragment is the column fragment with lane bits (5,4) and (1,0)
-// exchanged, register for register: rf[r] at lane 16 h + 4 b + n = cf[r] at lane
-// 16 n + 4 b + h.  Besides the LDS tile (XP = 0) two register-only forms
-// (A/B, SGV_MF_XPOSE):
-// XP = 1: permlane32/16_swap exchange lane bits 5 / 4 with the register bits of
-//   r (1 / 0), quad DPP moves + selects exchange lane bits 1 / 0 with them, and
-//   a second permlane pass puts r back: (L54 r)(L10 r)(L54 r) = (L54 L10);
-//   16 + 32 + 16 swaps / selects (+ 32 DPP moves) per 4-KiB step, no LDS.
-// XP = 2: ds_bpermute_b32 (the LDS crossbar, no LDS storage), 16 per step.
-__device__ __forceinline__ void xp_p32(unsigned& x, unsigned& y) {
-  const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
-  x = r[0];
-  y = r[1];
-}
-__device__ __forceinline__ void xp_p16(unsigned& x, unsigned& y) {
-  const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
-  x = r[0];
-  y = r[1];
-}
-// lane bit `B` (0 or 1) <-> the register bit distinguishing x (0) from y (1)
-template <int B>
-__device__ __forceinline__ void xp_quad(unsigned& x, unsigned& y, bool sel) {
-  constexpr int CTRL = B == 0 ? 0xB1 : 0x4E;   // quad_perm [1,0,3,2] / [2,3,0,1]
-  const unsigned dx = (unsigned)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xF, 0xF, true);
-  const unsigned dy = (unsigned)__builtin_amdgcn_mov_dpp((int)y, CTRL, 0xF, 0xF, true);
-  const unsigned nx = sel ? dy : x;
-  y = sel ? y : dx;
-  x = nx;
-}
-__device__ __forceinline__ void xp_rows(unsigned (&v)[4]) {   // (L5 r1)(L4 r0)
-  xp_p32(v[0], v[2]);
-  xp_p32(v[1], v[3]);
-  xp_p16(v[0], v[1]);
-  xp_p16(v[2], v[3]);
-}
-__device__ __forceinline__ void xpose_perm(const d2* cf, d2* rf, bool l1, bool l0) {
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {   // the 4 dwords of a d2, each over the 4 registers
-    unsigned v[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const unsigned long long u = __builtin_bit_cast(unsigned long long, cf[r][e >> 1]);
-      v[r] = (unsigned)(e & 1 ? u >> 32 : u);
-    }
-    xp_rows(v);
-    xp_quad<1>(v[0], v[2], l1);
-    xp_quad<1>(v[1], v[3], l1);
-    xp_quad<0>(v[0], v[1], l0);
-    xp_quad<0>(v[2], v[3], l0);
-    xp_rows(v);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      unsigned long long u = __builtin_bit_cast(unsigned long long, rf[r][e >> 1]);
-      u = e & 1 ? ((u & 0xFFFFFFFFull) | ((unsigned long long)v[r] << 32))
-                : ((u & 0xFFFFFFFF00000000ull) | v[r]);
-      rf[r][e >> 1] = __builtin_bit_cast(double, u);
-    }
-  }
-}
-__device__ __forceinline__ void xpose_bperm(const d2* cf, d2* rf, int src4) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const unsigned long long u = __builtin_bit_cast(unsigned long long, cf[r][e]);
-      const unsigned lo32 = (unsigned)__builtin_amdgcn_ds_bpermute(src4, (int)(unsigned)u);
-      const unsigned hi32 = (unsigned)__builtin_amdgcn_ds_bpermute(src4, (int)(unsigned)(u >> 32));
-      rf[r][e] = __builtin_bit_cast(double, (unsigned long long)lo32 | ((unsigned long long)hi32 << 32));
-    }
 }
 
 // SGV_BAND_SKIP=0 (A/B, with SGV_AB=1; read by the host at launch and passed
@@ -520,7 +450,10 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
 // MAP 0: waves 2s, 2s + 1 hold segment s (the pair on two SIMDs); MAP 1: waves
 // s, s + 4 (waves are dealt to SIMDs round-robin: the pair shares one SIMD, each
 // SIMD runs one first and one second half)
-template <int NG, int PD, int XP, int MAP = 0>
+// SYNC 0: one workgroup barrier per row group; SYNC 1: each pair syncs on its
+// own LDS counters (the first wave up to HS - 1 row groups ahead, a ring of HS
+// hand-off slots), barriers only at panel ends
+template <int NG, int PD, int XP, int MAP = 0, int SYNC = 0>
 __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __restrict__ strips,
                                                           const SymItem* __restrict__ sitems,
                                                           const double* __restrict__ pk, int ncol,
@@ -533,7 +466,9 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
   static_assert(PD >= 1 && PD <= NT && NT % PD == 0, "prefetch depth divides the steps");
   constexpr int RW = 4 * NG;
   __shared__ __attribute__((aligned(16))) double wrow[4 * SYM_H * RW];   // [segment][row][4 NG]
-  __shared__ __attribute__((aligned(16))) double hand[2][4][4 * NG][WAVE];   // [gg & 1][segment][r, q][lane]
+  constexpr int HS = SYNC ? 3 : 2;                                        // hand-off slots
+  __shared__ __attribute__((aligned(16))) double hand[HS][4][4 * NG][WAVE];   // [gg % HS][segment][r, q][lane]
+  __shared__ int hready[4], hdone[4];   // SYNC: row groups handed / taken per segment
   __shared__ __attribute__((aligned(16))) double stg[XP == 0 ? NW : 1][16 * 32];
   const SymStrip sp = strips[blockIdx.x];
   if (run && !ldg(run)) return;
@@ -605,6 +540,14 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
 #pragma unroll
   for (int p = 0; p < PD; ++p) load_cf(curb, cur.w, cur.H, 0, p, cfq[p]);
   load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
+  if (SYNC) {
+    if (threadIdx.x < 4) hready[threadIdx.x] = hdone[threadIdx.x] = 0;
+    __syncthreads();
+  }
+  auto lds_wait_ge = [&](int* ctr, int v) {
+    while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v)
+      __builtin_amdgcn_s_sleep(1);
+  };
 
   int gg = 0;
 #pragma unroll 1
@@ -683,19 +626,25 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
         if (h == 0) row_mfma(rf, t);                     // the chain's first half
         __builtin_amdgcn_s_setprio(0);
       }
-      double* hs = &hand[gg & 1][seg][0][0];
+      double* hs = &hand[gg % HS][seg][0][0];
       if (h == 0) {
+        if (SYNC) lds_wait_ge(&hdone[seg], gg - HS + 1);   // slot gg % HS taken back
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int q = 0; q < NG; ++q) hs[(r * NG + q) * WAVE + lane] = drow[r][q];
+        if (SYNC)
+          __hip_atomic_store(&hready[seg], gg + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-      __syncthreads();   // hand-off of row group gg (and the last group's reads of gg - 2)
+      if (!SYNC) __syncthreads();   // hand-off of row group gg (and the reads of gg - 2)
       if (h == 1) {
+        if (SYNC) lds_wait_ge(&hready[seg], gg + 1);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int q = 0; q < NG; ++q) drow[r][q] = hs[(r * NG + q) * WAVE + lane];
+        if (SYNC)
+          __hip_atomic_store(&hdone[seg], gg + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -1034,7 +983,7 @@ static int mf_xpose() {
 static int mf_pair_map() {
   static const int v = [] {
     const char* e = ab_env("SGV_MF_PAIR_MAP");
-    return (e && e[0] == '1') ? 1 : 0;
+    return (e && e[0] >= '1' && e[0] <= '3') ? e[0] - '0' : 0;
   }();
   return v;
 }
@@ -1048,6 +997,12 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
   if (ragged)
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, true>), dim3(nstrips), dim3(NW * 64), 0,
                        st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (pair && mf_pair_map() == 2)   // 2: MAP 0 + counters, 3: MAP 1 + counters
+    hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0, 0, 1>), dim3(nstrips), dim3(512), 0, st, d_strips,
+                       d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (pair && mf_pair_map() == 3)
+    hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0, 1, 1>), dim3(nstrips), dim3(512), 0, st, d_strips,
+                       d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else if (pair && mf_pair_map() == 1)
     hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0, 1>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);

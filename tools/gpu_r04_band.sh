@@ -8,6 +8,7 @@ out=$1
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q -k "band" \
     --timeout 200 --timeout-method thread > ${out}_parity.log 2>&1 || { echo "band parity FAILED"; tail -30 ${out}_parity.log; exit 1; }
 echo "band parity: $(tail -1 ${out}_parity.log)"
+if [ -z "$BAND_TRACE_ONLY" ]; then
 export SGV_AB=1
 for rep in 1 2; do
   for v in 0 1; do
@@ -19,8 +20,11 @@ python3 -c "
 import json
 for l in open('${out}_ab.jsonl'):
     d = json.loads(l); print(d['tag'], d['ncol'], '%.4f ms' % d['ms_per_pass'], '%.3f' % d['frac_of_8TBs'], d['sha'])"
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d ${out}_trace -o band -- \
-    python3 -u tools/ldpass_band.py --M 1000000 --bw 1000 --ncols 8,16 --reps 10 > ${out}_trace.log 2>&1 || exit 1
-find ${out}_trace -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} ${out}_kernel_stats.csv
+fi
+R=$PWD
+export TMPDIR=/tmp
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/${out}_trace -o band --output-format csv -- \
+    python3 -u $R/tools/ldpass_band.py --M 1000000 --bw 1000 --ncols 8,16 --reps 10) > ${out}_trace.log 2>&1 || exit 1
+f=$(find ${out}_trace -name "*kernel_stats.csv" | head -1)
+cp "$f" ${out}_kernel_stats.csv
 head -12 ${out}_kernel_stats.csv | cut -c1-200
