@@ -159,6 +159,17 @@ int sgv_ld_block_format(sgv_ctx* ctx, int ld, int blk_local, int* fmt_out);
  * (dense n^2*8, packed triangle / band: the stored panels).  Python's Engine
  * sums it over ranks to pick the run's CG column-set mode (sgv_set_cg_exact). */
 int sgv_ld_stored_bytes(sgv_ctx* ctx, int ld, double* bytes_out);
+/* Coupling between consecutive band pieces gb and gb + 1 (global block
+ * indices) of LD matrix ld: C = R[last nr rows of gb][first nc columns of gb+1],
+ * nr x nc row-major.  A band block too long for one GPU (one chromosome of
+ * windowed LD: src/main.py:199-200,251-257) is cut into pieces that ranks own
+ * like LD blocks; a pass then adds C p_{gb+1}[head] to gb's last rows and
+ * C^T p_gb[tail] to gb+1's first rows, in a fixed order on every rank (results
+ * bitwise independent of the rank count), the halo of a coupling that spans two
+ * ranks exchanged per pass.  Every rank calls this for EVERY coupling (C may be
+ * NULL where the rank owns neither piece): the exchange is collective.  Pieces
+ * must be stored packed (sgv_set_ld_block_csr). */
+int sgv_set_ld_coupling(sgv_ctx* ctx, int ld, int gb, int nr, int nc, const double* C);
 /* Download one LD block (row-major n x n into a host array of row stride ld_host). */
 int sgv_get_ld_block(sgv_ctx* ctx, int ld, int blk_local, double* rowmajor, int64_t ld_host);
 /* Start a new VAMP.infer on this context (src/sgvamp.py:198-217 restarts from

@@ -46,6 +46,16 @@ struct LdBlock {
   double stored_bytes = 0.0;   // bytes a pass reads: n^2*8 dense, sum H_g (n - r0_g)*8 packed
 };
 
+// coupling between consecutive band pieces gb and gb + 1 of one LD matrix (a
+// band block too long for one GPU, cut into pieces that ranks can own):
+// C = R[last nr rows of gb][first nc columns of gb + 1], kept by the ranks that
+// own either piece (sgv_set_ld_coupling)
+struct LdCoupling {
+  int gb = -1, nr = 0, nc = 0;
+  double* d_up = nullptr;   // C^T (nc x nr): side 0, on gb's rank
+  double* d_lo = nullptr;   // C (nr x nc): side 1, on gb + 1's rank
+};
+
 // launch tables of one LD matrix (rebuilt when a block's storage changes)
 struct LdPlan {
   bool valid = false;
@@ -66,6 +76,16 @@ struct LdPlan {
   bool ragged = false;         // some strip item is narrower than its strip (band blocks)
   bool pair = false;           // NC <= 8 passes run k_sym_mfma_pair (build_strips)
   double stored_bytes = 0.0, dense_bytes = 0.0;
+  // coupled band pieces: k_coupling tasks, panel slots of PassArgs::cpbuf, and
+  // the halo this rank sends (head of its first block, tail of its last) when a
+  // coupling spans two ranks -- the same decision on every rank (all ranks know
+  // every coupling and the block partition)
+  CouplingTask* d_ctasks = nullptr;
+  int nctasks = 0, ncp = 0;
+  bool halo = false;
+  int64_t hmax = 0, h_src0 = 0, h_src1 = 0;
+  int h_len0 = 0, h_len1 = 0;
+  double cpl_bytes = 0.0;      // coupling matrix bytes read per pass (this rank)
 };
 
 // A/B tuning switches: an environment override is honoured only with
@@ -170,6 +190,14 @@ struct sgv_ctx {
   std::vector<int64_t> lda;
   std::vector<BlkDesc*> d_blks;
   std::vector<LdPlan> plan;
+  std::vector<std::vector<LdCoupling>> cpl;   // [ld]: couplings of band pieces
+  std::vector<int> rank_blk0;    // first global block of each rank, then nblk_global
+  double* d_cpbuf = nullptr;     // coupling sums [slot][256][nc]
+  size_t cpbuf_cap = 0;
+  double* d_halo = nullptr;      // send [2][nc][hmax] then receive [nranks][2][nc][hmax]
+  size_t halo_cap = 0;
+  double* h_halo = nullptr;      // pinned staging of the host exchange (same layout)
+  size_t h_halo_cap = 0;
   int packing = 1;               // 1: packed symmetric storage for symmetric blocks
   double* d_rowpart = nullptr;   // k_sym_pass row partials
   double* d_colpart = nullptr;   // k_sym_pass column partials
@@ -583,6 +611,7 @@ static void free_plan(LdPlan& p) {
   if (p.d_strips) (void)hipFree(p.d_strips);
   if (p.d_sitems) (void)hipFree(p.d_sitems);
   if (p.d_spanels) (void)hipFree(p.d_spanels);
+  if (p.d_ctasks) (void)hipFree(p.d_ctasks);
   p = LdPlan();
 }
 
@@ -822,6 +851,107 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
   return SGV_OK;
 }
 
+// rank holding global block gb (rank_blk0 from the communicator; -1 outside)
+static int rank_of_block(const sgv_ctx* c, int gb) {
+  const int nr = (int)c->rank_blk0.size() - 1;
+  for (int r = 0; r < nr; ++r)
+    if (gb >= c->rank_blk0[r] && gb < c->rank_blk0[r + 1]) return r;
+  return -1;
+}
+
+// Coupling tasks of LD matrix ld and the panel slots they fill: for each
+// coupling (gb, gb + 1) side 0 = gb's last nr rows (if gb is local), side 1 =
+// gb + 1's first nc rows (if local), cut at panel boundaries; slot[(b, g)]
+// numbers the panels holding such rows.  Sources on another rank come from the
+// halo exchange (neighbouring ranks only: pieces are contiguous).
+static int plan_couplings(sgv_ctx* c, int ld, LdPlan& pl, std::vector<int>& slot_of,
+                          std::vector<int>& slot_base) {
+  const std::vector<LdCoupling>& cv = c->cpl[ld];
+  slot_base.assign(c->nblk + 1, 0);
+  for (int b = 0; b < c->nblk; ++b)
+    slot_base[b + 1] = slot_base[b] + (int)std::max<size_t>(1, c->ldb[ld][b].poff.size());
+  slot_of.assign(slot_base[c->nblk], -1);
+  if (cv.empty()) return SGV_OK;
+  const int me = c->rank;
+  std::vector<CouplingTask> tasks;
+  int ncp = 0;
+  auto slot = [&](int b, int g) {
+    int& sref = slot_of[slot_base[b] + g];
+    if (sref < 0) sref = ncp++;
+    return sref;
+  };
+  pl.hmax = 0;
+  for (const LdCoupling& q : cv) pl.hmax = std::max<int64_t>(pl.hmax, std::max(q.nr, q.nc));
+  pl.halo = false;
+  pl.h_len0 = pl.h_len1 = 0;
+  for (const LdCoupling& q : cv) {
+    const int ra = rank_of_block(c, q.gb), rb = rank_of_block(c, q.gb + 1);
+    if (ra < 0 || rb < 0)
+      return fail(c, SGV_ERR_STATE, "coupling (%d, %d): block outside the partition", q.gb, q.gb + 1);
+    if (ra != rb) pl.halo = true;   // the same decision on every rank
+    const int ba = q.gb - c->blk0, bb = q.gb + 1 - c->blk0;
+    const bool la = ba >= 0 && ba < c->nblk, lb = bb >= 0 && bb < c->nblk;
+    if (ra != rb && la) {           // gb is this rank's last block: send its tail
+      pl.h_src1 = c->bvoff[ba] + c->bn[ba] - q.nr;
+      pl.h_len1 = q.nr;
+    }
+    if (ra != rb && lb) {           // gb + 1 is this rank's first block: send its head
+      pl.h_src0 = c->bvoff[bb];
+      pl.h_len0 = q.nc;
+    }
+    if (la && c->ldb[ld][ba].fmt != 1)
+      return fail(c, SGV_ERR_ARG, "coupling (%d, %d): pieces must be stored packed", q.gb, q.gb + 1);
+    if (lb && c->ldb[ld][bb].fmt != 1)
+      return fail(c, SGV_ERR_ARG, "coupling (%d, %d): pieces must be stored packed", q.gb, q.gb + 1);
+    for (int side = 0; side < 2; ++side) {
+      if (side == 0 && !la) continue;
+      if (side == 1 && !lb) continue;
+      const int b = side == 0 ? ba : bb;
+      const int64_t rbeg = side == 0 ? c->bn[b] - q.nr : 0;   // block-relative output rows
+      const int64_t rend = side == 0 ? c->bn[b] : q.nc;
+      for (int64_t r = rbeg; r < rend;) {
+        const int g = (int)(r / SYM_H);
+        const int64_t pe = std::min<int64_t>(rend, (int64_t)(g + 1) * SYM_H);
+        CouplingTask t;
+        t.m = side == 0 ? q.d_up : q.d_lo;
+        t.ldm = side == 0 ? q.nr : q.nc;
+        t.inner = side == 0 ? q.nc : q.nr;
+        t.row0 = (int32_t)(r - rbeg);
+        t.nrows = (int32_t)(pe - r);
+        t.cp = slot(b, g);
+        t.prow0 = (int32_t)(r - (int64_t)g * SYM_H);
+        const bool local_src = side == 0 ? lb : la;
+        t.local = local_src ? 1 : 0;
+        if (local_src)
+          t.src = side == 0 ? c->bvoff[bb] : c->bvoff[ba] + c->bn[ba] - q.nr;
+        else   // halo [rank][slot]: the next rank's head (slot 0) or the previous one's tail (1)
+          t.src = side == 0 ? 2 * (int64_t)rb + 0 : 2 * (int64_t)ra + 1;
+        tasks.push_back(t);
+        r = pe;
+      }
+      pl.cpl_bytes += 8.0 * q.nr * q.nc;
+    }
+  }
+  (void)me;
+  pl.nctasks = (int)tasks.size();
+  pl.ncp = ncp;
+  CHK(upload_table(c, tasks, &pl.d_ctasks));
+  CHK(grow(c, &c->d_cpbuf, &c->cpbuf_cap, (size_t)std::max(ncp, 1) * 256 * MAXC));
+  if (pl.halo) {
+    const size_t per = 2 * (size_t)MAXC * pl.hmax;
+    CHK(grow(c, &c->d_halo, &c->halo_cap, per * (1 + (size_t)c->nranks)));
+    if (c->host_ag && c->h_halo_cap < per * (1 + (size_t)c->nranks)) {
+      if (c->h_halo) HIPCHK(hipHostFree(c->h_halo));
+      c->h_halo = nullptr;
+      HIPCHK(hipHostMalloc(&c->h_halo, sizeof(double) * per * (1 + (size_t)c->nranks)));
+      c->h_halo_cap = per * (1 + (size_t)c->nranks);
+    }
+    if (!c->comm && !c->host_ag)
+      return fail(c, SGV_ERR_STATE, "a coupling spans two ranks but no communicator is set");
+  }
+  return SGV_OK;
+}
+
 // launch tables of LD matrix ld: dense row groups, packed (panel, chunk) items
 // per chunk-width class, panels; unified partial slots in block order
 static int ensure_plan(sgv_ctx* c, int ld) {
@@ -849,6 +979,8 @@ static int ensure_plan(sgv_ctx* c, int ld) {
   pl.nrg = (int)rg.size();
   CHK(upload_table(c, rg, &pl.d_rg));
   CHK(upload_table(c, pbeg, &pl.d_pbeg));
+  std::vector<int> cp_slot, cp_base;   // coupled band pieces: panel -> cpbuf slot
+  CHK(plan_couplings(c, ld, pl, cp_slot, cp_base));
   size_t rowpart_need = 0, colpart_need = 0;
   for (int cls = 0; cls < 4; ++cls) {
     const int cw = 1024 >> cls;
@@ -889,6 +1021,7 @@ static int ensure_plan(sgv_ctx* c, int ld) {
         // first earlier panel whose stored columns cover this panel's rows
         pn.gmin = lb.ext > 0 ? std::max<int>(0, (int)g - (int)(lb.ext / SYM_H) + 1) : 0;
         pn.own_sb = pn.own_se = pn.oth_sb = pn.oth_se = 0;
+        pn.cp = cp_slot[cp_base[b] + (int)g];
         panels.push_back(pn);
       }
     }
@@ -924,10 +1057,36 @@ static int ensure_plan(sgv_ctx* c, int ld) {
 
 static const int* ld_parts(sgv_ctx* c, int ld) { return c->plan[ld].d_pbeg; }
 
-static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa) {
+static int gather_f64(sgv_ctx* c, const double* d_send, double* d_recv, size_t cnt,
+                      double* h_send, double* h_recv);
+
+// coupling sums of LD matrix ld's band pieces for this pass (before the
+// finalize that adds them): the halo of a coupling that spans two ranks is
+// all-gathered first (every rank takes part, whatever its own couplings)
+static int coupling_pass(sgv_ctx* c, const LdPlan& pl, int nc, const PassArgs& pa) {
+  const double* recv = nullptr;
+  if (pl.halo) {
+    const size_t per = 2 * (size_t)nc * pl.hmax;
+    double* send = c->d_halo;
+    double* drecv = c->d_halo + per;
+    HIPCHK(launch_halo_pack(pa, nc, pl.h_src0, pl.h_len0, pl.h_src1, pl.h_len1, pl.hmax, send,
+                            c->st));
+    CHK(gather_f64(c, send, drecv, per, c->h_halo, c->h_halo ? c->h_halo + per : nullptr));
+    recv = drecv;
+  }
+  if (pl.nctasks)
+    HIPCHK(launch_coupling(nc, pl.d_ctasks, pl.nctasks, pa, recv, pl.hmax, c->d_cpbuf, pl.ncp,
+                           c->st));
+  c->aux_bytes += pl.cpl_bytes + 2.0 * 8.0 * nc * 256.0 * pl.ncp;
+  return SGV_OK;
+}
+
+static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa_in) {
   if (nc <= 0) return SGV_OK;
   CHK(ensure_plan(c, ld));
   const LdPlan& pl = c->plan[ld];
+  PassArgs pa = pa_in;
+  pa.cpbuf = c->d_cpbuf;
   hipEvent_t e0, e1;
   if (c->evpool.size() < 2) {
     HIPCHK(hipEventCreate(&e0));
@@ -939,6 +1098,7 @@ static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa) {
     c->evpool.pop_back();
   }
   HIPCHK(hipEventRecord(e0, c->st));
+  if (pl.halo || pl.nctasks) CHK(coupling_pass(c, pl, nc, pa));
   if (pl.nrg) HIPCHK(launch_ld_pass(nc, c->d_blks[ld], pl.d_rg, pl.nrg, pa, c->d_part, c->st));
   if (pl.npanels) {
     const bool mf = c->mfma_min > 0 && nc >= c->mfma_min;
@@ -1368,6 +1528,8 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
   // LD descriptors
   c->ldb.assign(nld, std::vector<LdBlock>(nblk));
   c->plan.assign(nld, LdPlan());
+  c->cpl.assign(nld, std::vector<LdCoupling>());
+  c->rank_blk0 = {blk0, blk0 + nblk};   // one rank until a communicator says otherwise
   for (int l = 0; l < nld; ++l) {
     BlkDesc* d = nullptr;
     CREATE_HIP(hipMalloc(&d, sizeof(BlkDesc) * nblk));
@@ -1467,6 +1629,14 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   for (auto& v : c->ldb)
     for (LdBlock& lb : v) free_block(lb);
   for (LdPlan& pl : c->plan) free_plan(pl);
+  for (auto& v : c->cpl)
+    for (LdCoupling& q : v) {
+      if (q.d_up) (void)hipFree(q.d_up);
+      if (q.d_lo) (void)hipFree(q.d_lo);
+    }
+  if (c->d_cpbuf) (void)hipFree(c->d_cpbuf);
+  if (c->d_halo) (void)hipFree(c->d_halo);
+  if (c->h_halo) (void)hipHostFree(c->h_halo);
   if (c->d_rowpart) (void)hipFree(c->d_rowpart);
   if (c->d_colpart) (void)hipFree(c->d_colpart);
   if (c->d_pk) (void)hipFree(c->d_pk);
@@ -1557,6 +1727,9 @@ extern "C" int sgv_comm_unique_id(char* id_out) {
 static int comm_buffers(sgv_ctx* c, int nranks, int rank, const int* nblk_per_rank) {
   c->nranks = nranks;
   c->rank = rank;
+  c->rank_blk0.assign(nranks + 1, 0);
+  for (int r = 0; r < nranks; ++r) c->rank_blk0[r + 1] = c->rank_blk0[r] + nblk_per_rank[r];
+  for (auto& p : c->plan) p.valid = false;   // the halo decision depends on the partition
   c->nbmax = *std::max_element(nblk_per_rank, nblk_per_rank + nranks);
   const size_t per = (size_t)c->nbmax * MAXNV;
   HIPCHK(hipFree(c->d_bsum));
@@ -1921,6 +2094,45 @@ extern "C" int sgv_ld_block_format(sgv_ctx* c, int ld, int b, int* fmt_out) {
     return fail(c, SGV_ERR_ARG, "sgv_ld_block_format: bad arguments");
   const LdBlock& lb = c->ldb[ld][b];
   *fmt_out = lb.ptr ? (lb.fmt == 1 && lb.ext > 0 ? 2 : lb.fmt) : -1;
+  return SGV_OK;
+}
+
+extern "C" int sgv_set_ld_coupling(sgv_ctx* c, int ld, int gb, int nr, int nc, const double* C) {
+  ENTER(c);
+  if (ld < 0 || ld >= c->nld || gb < 0 || gb + 1 >= c->nblk_global || nr < 1 || nc < 1)
+    return fail(c, SGV_ERR_ARG, "sgv_set_ld_coupling: bad arguments (ld %d, gb %d, %d x %d)", ld,
+                gb, nr, nc);
+  const int ba = gb - c->blk0, bb = gb + 1 - c->blk0;
+  const bool la = ba >= 0 && ba < c->nblk, lb = bb >= 0 && bb < c->nblk;
+  if ((la && nr > c->bn[ba]) || (lb && nc > c->bn[bb]))
+    return fail(c, SGV_ERR_ARG, "sgv_set_ld_coupling: %d x %d exceeds the pieces", nr, nc);
+  if ((la || lb) && !C) return fail(c, SGV_ERR_ARG, "sgv_set_ld_coupling: C is null");
+  std::vector<LdCoupling>& cv = c->cpl[ld];
+  auto it = std::find_if(cv.begin(), cv.end(), [&](const LdCoupling& q) { return q.gb == gb; });
+  if (it == cv.end()) {
+    cv.push_back(LdCoupling());
+    it = cv.end() - 1;
+  }
+  if (it->d_up) HIPCHK(hipFree(it->d_up));
+  if (it->d_lo) HIPCHK(hipFree(it->d_lo));
+  it->d_up = it->d_lo = nullptr;
+  it->gb = gb;
+  it->nr = nr;
+  it->nc = nc;
+  const size_t n = (size_t)nr * nc;
+  if (la) {   // C^T, for gb's tail rows
+    std::vector<double> t(n);
+    for (int i = 0; i < nr; ++i)
+      for (int j = 0; j < nc; ++j) t[(size_t)j * nr + i] = C[(size_t)i * nc + j];
+    HIPCHK(hipMalloc(&it->d_up, sizeof(double) * n));
+    HIPCHK(hipMemcpy(it->d_up, t.data(), sizeof(double) * n, hipMemcpyHostToDevice));
+  }
+  if (lb) {   // C, for gb + 1's head rows
+    HIPCHK(hipMalloc(&it->d_lo, sizeof(double) * n));
+    HIPCHK(hipMemcpy(it->d_lo, C, sizeof(double) * n, hipMemcpyHostToDevice));
+  }
+  std::sort(cv.begin(), cv.end(), [](const LdCoupling& a, const LdCoupling& b) { return a.gb < b.gb; });
+  c->plan[ld].valid = false;
   return SGV_OK;
 }
 

@@ -103,6 +103,9 @@ struct SymPanel {
   // panels of this panel's parity, row offset 0) and the one starting at
   // r0 - 256 (the other parity, row offset 256); colpart slots [sb, se)
   int32_t own_sb, own_se, oth_sb, oth_se;
+  // coupled band pieces (sgv_set_ld_coupling): slot of this panel's rows in the
+  // coupling sums PassArgs::cpbuf [slot][256][NC], added last; -1 = none
+  int32_t cp;
 };
 // MFMA pass work item: one 512-column chunk (block-relative c0, shared by all
 // its panels) over npan panels of one parity, g0, g0 + 2, ... (increasing);
@@ -138,6 +141,25 @@ struct PassArgs {
   // enqueued ahead of the stop test becomes a no-op); every workgroup reads it
   // next to its first descriptor load
   const int* run;
+  // coupling sums of the panels next to a cut between coupled band pieces
+  // ([slot][256][ncol], SymPanel::cp), written by k_coupling before the finalize
+  const double* cpbuf;
+};
+
+// One task of k_coupling: up to 256 rows of one side of the coupling between
+// band pieces gb and gb + 1 (C = R[tail nr rows of gb][head nc columns of gb + 1]):
+//   side 0 (rows = gb's tail):   y[i] = sum_j C[i][j] p_{gb+1}[j]   (m = C^T, nc x nr)
+//   side 1 (rows = gb+1's head): y[j] = sum_i C[i][j] p_{gb}[n - nr + i] (m = C, nr x nc)
+// m is read as m[k * ldm + row] (coalesced over rows), k = 0 .. inner - 1 in
+// order.  The source p is pa.in[c] + src (local) or halo + src + c * hstride.
+struct CouplingTask {
+  const double* m;
+  int64_t src;       // source offset (see above)
+  int32_t ldm, inner;
+  int32_t row0, nrows;   // first output row (of the task's panel slot rows), count
+  int32_t cp;        // panel slot
+  int32_t prow0;     // the task's first output row within that panel
+  int32_t local;     // 1: the source is local (pa.in), 0: the gathered halo
 };
 
 // most values one ordered reduction carries
@@ -270,6 +292,7 @@ __device__ __forceinline__ void fin_epilogue(const SymPanel& pn, const PassArgs&
       double v = s_y[0][q][t];
 #pragma unroll
       for (int p = 1; p < FIN_Q; ++p) v += s_y[p][q][t];
+      if (pn.cp >= 0) v += pa.cpbuf[((int64_t)pn.cp * 256 + t) * NC + c];   // coupled pieces
       double acc = 0.0;
       if (row) {
         const double in = pre.in[b];
@@ -294,6 +317,12 @@ const char* ab_env(const char* name);
 hipError_t launch_read_probe(const double* buf, size_t bytes, double* out, hipStream_t st);
 
 // ---- launchers (defined in the .hip files) ------------------------------
+// coupling sums between band pieces (sym_pass.hip): cpbuf[slot][256][nc]
+hipError_t launch_coupling(int nc, const CouplingTask* d_tasks, int ntasks, const PassArgs& pa,
+                           const double* halo, int64_t hstride, double* cpbuf, int ncp_slots,
+                           hipStream_t st);
+hipError_t launch_halo_pack(const PassArgs& pa, int nc, int64_t src0, int len0, int64_t src1,
+                            int len1, int64_t hstride, double* send, hipStream_t st);
 // LD pass: one workgroup per row group; partials[rg.part * nc + c].
 hipError_t launch_ld_pass(int nc, const BlkDesc* d_blks, const RowGroup* d_rg, int nrg,
                           const PassArgs& pa, double* d_partials, hipStream_t st);

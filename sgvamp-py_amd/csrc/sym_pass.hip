@@ -245,6 +245,81 @@ hipError_t launch_sym_pass(int nc, int cls, const SymItem* d_items, int nitems,
   return hipErrorInvalidValue;
 }
 
+// ---- coupled band pieces --------------------------------------------------
+// One workgroup per CouplingTask, one thread per output row: y[c] = sum over
+// k (in order) of m[k][row] * p[k][c] -- a fixed order on every rank, so the
+// coupling sums are the same whichever rank holds the source rows.  Remote
+// sources sit in the gathered halo [rank][2][nc][hstride]: task.src = 2 rank +
+// slot.  Rows of a slot no task writes stay as cleared by the caller.
+template <int NC>
+__global__ __launch_bounds__(256) void k_coupling(const CouplingTask* __restrict__ tasks,
+                                                  PassArgs pa, const double* __restrict__ halo,
+                                                  int64_t hstride, double* __restrict__ cpbuf) {
+  const CouplingTask tk = tasks[blockIdx.x];
+  if (pa.run && !ldg(pa.run)) return;
+  const int r = threadIdx.x;
+  if (r >= tk.nrows) return;
+  const double* src[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c)
+    src[c] = tk.local ? pa.in[c] + tk.src : halo + (tk.src * NC + c) * hstride;
+  const double* m = tk.m + tk.row0 + r;
+  double y[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) y[c] = 0.0;
+#pragma unroll 4
+  for (int k = 0; k < tk.inner; ++k) {
+    const double a = m[(int64_t)k * tk.ldm];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) y[c] += a * ldg(src[c] + k);
+  }
+  double* out = cpbuf + ((int64_t)tk.cp * 256 + tk.prow0 + r) * NC;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) out[c] = y[c];
+}
+
+hipError_t launch_coupling(int nc, const CouplingTask* d_tasks, int ntasks, const PassArgs& pa,
+                           const double* halo, int64_t hstride, double* cpbuf, int ncp_slots,
+                           hipStream_t st) {
+  if (ntasks <= 0) return hipSuccess;
+  const hipError_t e = hipMemsetAsync(cpbuf, 0, sizeof(double) * (size_t)ncp_slots * 256 * nc, st);
+  if (e != hipSuccess) return e;
+#define CPL_CASE(N)                                                                         \
+  case N:                                                                                   \
+    hipLaunchKernelGGL(k_coupling<N>, dim3(ntasks), dim3(256), 0, st, d_tasks, pa, halo,    \
+                       hstride, cpbuf);                                                     \
+    break;
+  switch (nc) {
+    CPL_CASE(1) CPL_CASE(2) CPL_CASE(3) CPL_CASE(4) CPL_CASE(5) CPL_CASE(6) CPL_CASE(7) CPL_CASE(8)
+    CPL_CASE(9) CPL_CASE(10) CPL_CASE(11) CPL_CASE(12) CPL_CASE(13) CPL_CASE(14) CPL_CASE(15)
+    CPL_CASE(16)
+    default: return hipErrorInvalidValue;
+  }
+#undef CPL_CASE
+  return hipGetLastError();
+}
+
+// the halo a rank sends: per slot s (0: head of its first block, 1: tail of its
+// last), nc columns of hstride doubles (len[s] used, the rest zero)
+__global__ __launch_bounds__(256) void k_halo_pack(PassArgs pa, int nc, int64_t src0, int len0,
+                                                   int64_t src1, int len1, int64_t hstride,
+                                                   double* __restrict__ send) {
+  if (pa.run && !ldg(pa.run)) return;
+  const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= hstride) return;
+  const int s = blockIdx.y, c = blockIdx.z;
+  const int len = s ? len1 : len0;
+  const int64_t src = s ? src1 : src0;
+  send[((int64_t)s * nc + c) * hstride + j] = j < len ? pa.in[c][src + j] : 0.0;
+}
+
+hipError_t launch_halo_pack(const PassArgs& pa, int nc, int64_t src0, int len0, int64_t src1,
+                            int len1, int64_t hstride, double* send, hipStream_t st) {
+  hipLaunchKernelGGL(k_halo_pack, dim3((unsigned)((hstride + 255) / 256), 2, nc), dim3(256), 0, st,
+                     pa, nc, src0, len0, src1, len1, hstride, send);
+  return hipGetLastError();
+}
+
 hipError_t launch_sym_finalize(int nc, int cls, const SymPanel* d_panels, int npanels,
                                const PassArgs& pa, const double* rowpart, const double* colpart,
                                double* partials, hipStream_t st) {

@@ -117,6 +117,21 @@ class Engine:
         self.ctx.sgv_set_ld_block_csr(ld, b_global - self.b0, indptr.ctypes.data_as(hb._c_i64_p),
                                       indices.ctypes.data_as(hb._c_i64_p), hb.dptr(data))
 
+    def set_ld_coupling(self, ld, gb, nr, nc, C):
+        """Coupling between band pieces gb and gb + 1 (global indices) of LD matrix
+        ld: C = R[last nr rows of gb][first nc columns of gb + 1] (dense or
+        scipy sparse).  Called on every rank for every coupling; the matrix is
+        densified and sent only where this rank owns one of the two pieces."""
+        own = self.b0 <= gb < self.b1 or self.b0 <= gb + 1 < self.b1
+        ptr = None
+        if own:
+            D = C.toarray() if hasattr(C, "toarray") else np.asarray(C)
+            D = np.ascontiguousarray(D, dtype=np.float64)
+            if D.shape != (nr, nc):
+                raise ValueError("coupling %d has shape %s, expected (%d, %d)" % (gb, D.shape, nr, nc))
+            ptr = hb.dptr(D)
+        self.ctx.sgv_set_ld_coupling(int(ld), int(gb), int(nr), int(nc), ptr)
+
     def stored_bytes(self, ld):
         """Bytes one pass over LD matrix ld reads on this rank (blocks set so far)."""
         out = np.zeros(1)

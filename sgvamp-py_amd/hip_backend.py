@@ -58,6 +58,7 @@ _SIGS = {
     "sgv_set_ld_packing": [_vp, ctypes.c_int],
     "sgv_ld_block_format": [_vp, ctypes.c_int, ctypes.c_int, _c_int_p],
     "sgv_ld_stored_bytes": [_vp, ctypes.c_int, _c_dbl_p],
+    "sgv_set_ld_coupling": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dbl_p],
     "sgv_set_ridge": [_vp, ctypes.c_double],
     "sgv_set_cohort_n": [_vp, ctypes.c_int, ctypes.c_double],
     "sgv_set_vector": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p],

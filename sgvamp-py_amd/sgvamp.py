@@ -39,6 +39,31 @@ from partition import coarsen_blocks, detect_blocks_csr, detect_blocks_dense
 DENSE_BLOCK_LIMIT = int(os.environ.get("SGV_DENSE_BLOCK_LIMIT", str(16 << 30)))
 
 
+# Band pieces: a symmetric sparse LD block of at least 2 BAND_PIECE markers
+# whose entries stay within BAND_PIECE / 4 of the diagonal (windowed LD over a
+# whole chromosome) is cut into pieces of BAND_PIECE markers (the last one up
+# to twice that) that ranks own like LD blocks, consecutive pieces coupled by the
+# band's corner (sgv_set_ld_coupling).  The cut depends on the matrix only, never
+# on the rank count, so 1 and N ranks compute the same sums.  SGV_BAND_PIECE
+# (a multiple of 1024) changes the piece length, 0 disables the cut.
+BAND_PIECE = int(os.environ.get("SGV_BAND_PIECE", "65536"))
+
+
+def csr_bandwidth(U, chunk=1 << 16):
+    """max(j - i) over the entries (i, j) of a CSR matrix (rows in chunks)."""
+    bw = 0
+    n = U.shape[0]
+    ip, ix = U.indptr, U.indices
+    for r0 in range(0, n, chunk):
+        r1 = min(n, r0 + chunk)
+        a, b = int(ip[r0]), int(ip[r1])
+        if a == b:
+            continue
+        rows = np.repeat(np.arange(r0, r1, dtype=np.int64), np.diff(ip[r0:r1 + 1]))
+        bw = max(bw, int((ix[a:b].astype(np.int64) - rows).max()))
+    return bw
+
+
 def _dense_guard(n, why):
     need = 8.0 * n * n
     if need > DENSE_BLOCK_LIMIT:
@@ -108,6 +133,65 @@ class BlockLD:
             _dense_guard(self.block_sizes[b], "dense LD storage requested")
         eng.set_ld_block(ld, b, self.block(b))
 
+    def band_width(self, b):
+        """Bandwidth of block b (max j - i over its entries), None for a dense
+        source or a non-symmetric block."""
+        cache = self.__dict__.setdefault("_bw", {})
+        if b not in cache:
+            A = self.block_csr(b)
+            if A is None or (A != A.T).nnz != 0:
+                cache[b] = None
+            else:
+                import scipy.sparse
+
+                cache[b] = csr_bandwidth(scipy.sparse.triu(A, format="csr"))
+        return cache[b]
+
+    def pieces(self, cuts):
+        """The same matrix on a finer partition that cuts band blocks into pieces:
+        cuts[b] = the piece sizes of block b (one entry = not cut).  Returns the
+        piece-partitioned BlockLD (each piece the diagonal CSR block) and its
+        couplings {gb: C} between consecutive pieces of one block (gb = global
+        index of the upper piece, C = R[last nr rows of gb][first nc columns of
+        gb + 1], nr = min(bw, n_gb), nc = min(bw, n_gb+1))."""
+        import scipy.sparse
+
+        sizes, origin = [], []
+        for b, ps in enumerate(cuts):
+            o = 0
+            for n in ps:
+                sizes.append(int(n))
+                origin.append((b, o))
+                o += n
+        if len(sizes) == len(self.block_sizes):
+            return self, {}
+        src = self
+        last = {}   # the original block last sliced (pieces are loaded in order)
+
+        def loader(k):
+            b, o = origin[k]
+            if last.get("b") != b:
+                last.clear()
+                last.update(b=b, A=src.block_csr(b))
+            return last["A"][o:o + sizes[k], o:o + sizes[k]]
+
+        L = BlockLD(block_sizes=sizes, s=self.s, csr_loader=loader)
+        couplings = {}
+        k = 0
+        for b, ps in enumerate(cuts):
+            if len(ps) > 1:
+                A = src.block_csr(b)
+                bw = max(1, src.band_width(b) or 1)
+                o = 0
+                for i in range(len(ps) - 1):
+                    cut = o + ps[i]
+                    nr, nc = min(bw, ps[i]), min(bw, ps[i + 1])
+                    C = A[cut - nr:cut, cut:cut + nc]
+                    couplings[k + i] = (nr, nc, C)   # sparse; densified on upload
+                    o = cut
+            k += len(ps)
+        return L, couplings
+
     @classmethod
     def from_dense(cls, R, block_sizes=None, s=0.0):
         """A dense M x M LD matrix (the reference's .npy path, src/main.py:201-202);
@@ -160,6 +244,27 @@ class BlockLD:
             return out
 
         return BlockLD(block_sizes=sizes, loader=load, s=self.s)
+
+
+def band_cuts(lds, sizes, piece=None):
+    """Piece sizes per block of the common partition (see BAND_PIECE): a block is
+    cut when every LD matrix holds it as a symmetric sparse band of bandwidth <=
+    piece / 4 and it spans at least two pieces.  A function of the matrices
+    only (the same for every rank count)."""
+    piece = BAND_PIECE if piece is None else int(piece)
+    out = []
+    for b, n in enumerate(sizes):
+        n = int(n)
+        if piece <= 0 or n < 2 * piece:
+            out.append([n])
+            continue
+        bws = [L.band_width(b) for L in lds]
+        if any(w is None or w > piece // 4 for w in bws):
+            out.append([n])
+            continue
+        k = n // piece
+        out.append([piece] * (k - 1) + [n - piece * (k - 1)])
+    return out
 
 
 def common_partition(size_lists):
@@ -281,6 +386,14 @@ class VAMP:
         if sum(sizes) != self.M:
             raise ValueError("LD matrices cover %d markers, M = %d" % (sum(sizes), self.M))
         uniq = [L.regroup(sizes) for L in uniq]
+        couplings = [{} for _ in uniq]
+        if self.ld_packing:   # band blocks too long for one GPU: coupled pieces
+            cuts = band_cuts(uniq, sizes)
+            if any(len(c) > 1 for c in cuts):
+                split = [L.pieces(cuts) for L in uniq]
+                uniq = [x[0] for x in split]
+                couplings = [x[1] for x in split]
+                sizes = [n for c in cuts for n in c]
         self.engine = eng = Engine(sizes, K, ld_of, comm=self.comm, device=self.device,
                                           exchange=self.exchange)
         eng.set_ld_packing(self.ld_packing)
@@ -292,6 +405,9 @@ class VAMP:
         for l, L in enumerate(uniq):
             for b in range(eng.b0, eng.b1):
                 L.upload(eng, l, b, packed=self.ld_packing)
+            for gb in sorted(couplings[l]):   # every rank, every coupling (collective)
+                nr, nc, C = couplings[l][gb]
+                eng.set_ld_coupling(l, gb, nr, nc, C)
         eng.update_cg_exact()   # the run's CG column sets from the bytes stored (collective)
         rr = np.asarray(r, dtype=np.float64)
         rr = rr.reshape(K, -1) if rr.size == K * self.M else rr

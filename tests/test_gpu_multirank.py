@@ -106,3 +106,33 @@ def test_one_rank_exchange_rehearsal_bitwise(name, tmp_path):
         assert got.keys() == base.keys() and len(base) > 0
         for fn in base:
             assert got[fn] == base[fn], (ex, fn)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,K", [(2, 1), (3, 2)])
+def test_single_band_block_over_ranks(world, K):
+    """One band block (one chromosome of windowed LD, M = 100,000) cut into
+    coupled pieces of 16,384 markers and spread over `world` ranks (host
+    exchange on one GPU): every output file bitwise identical to the one-rank
+    run (tools/band_ranks_gpu.py), for K = 1 (VALU passes) and K = 2 (MFMA)."""
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SGV_EXCHANGE="host",
+                   SGV_BAND_PIECE="16384")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "band_ranks_gpu.py"),
+                                       str(K)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append(out)
+    for r, (p, out) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0, "rank %d failed:\n%s" % (r, out[-4000:])
+    assert "bitwise equal -> OK" in outs[0], outs[0][-3000:]

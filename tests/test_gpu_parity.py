@@ -847,6 +847,35 @@ def test_ld_matvec_band_vs_scipy(parts, ncol, s, kern):
     eng.close()
 
 
+@pytest.mark.parametrize("ncol", [1, 2, 3, 8, 16])
+def test_ld_matvec_coupled_pieces_vs_scipy(ncol):
+    """One band block cut into coupled pieces (sgvamp.band_cuts / BlockLD.pieces,
+    sgv_set_ld_coupling: the layout that lets ranks share one chromosome): the
+    pieces' passes plus the corner couplings equal scipy's CSR mat-vec of the
+    whole band (src/sgvamp.py:316) to 1e-12, on the VALU (1-2 columns) and MFMA
+    passes."""
+    from sgvamp import band_cuts
+
+    A = vo.banded_ld(70000, 700, seed=5, taps=12)
+    L = BlockLD.from_csr(A)
+    cuts = band_cuts([L], L.block_sizes, piece=16384)
+    assert [len(c) for c in cuts] == [4]
+    P, cpl = L.pieces(cuts)
+    assert sorted(cpl) == [0, 1, 2]
+    eng = Engine(P.block_sizes, K=1)
+    for b in range(len(P.block_sizes)):
+        P.upload(eng, 0, b)
+        assert eng.ld_block_format(0, b) == 2
+    for gb, (nr, nc, C) in cpl.items():
+        eng.set_ld_coupling(0, gb, nr, nc, C)
+    V = np.random.RandomState(ncol).normal(size=(ncol, A.shape[0]))
+    Y = eng.ld_matvec(0, V)
+    for j in range(ncol):
+        want = A @ V[j]
+        assert maxrel(Y[j], want) < 1e-12, (j, maxrel(Y[j], want))
+    eng.close()
+
+
 def test_band_block_roundtrip():
     """get_ld_block of a band block: the stored band, zeros outside it."""
     A = _band_matrix([(1500, 200)], seed=11)
