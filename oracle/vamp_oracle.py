@@ -256,6 +256,56 @@ class BlockLD:
         return (1 - self.s) * self.matvec_R(v) + self.s * v
 
 
+class CoupledLD:
+    """Band pieces with corner couplings: the layout that lets ranks share one
+    band block (one chromosome of windowed LD, src/main.py:199-200,251-257;
+    the build's sgv_set_ld_coupling).  This rank holds pieces gb0 .. gb0 +
+    len(pieces) - 1 (CSR, diagonal blocks of the band) and knows every
+    coupling {gb: (nr, nc, C)}, C = R[last nr rows of gb][first nc columns of
+    gb + 1].  R v = per-piece products, then the couplings added to the rows
+    they reach (gb's tail: C v_{gb+1}[:nc], gb + 1's head: C^T v_gb[-nr:]);
+    with a communicator the neighbours' head / tail rows come from an all-
+    gather, so 1 and N ranks add the same terms in the same order."""
+
+    def __init__(self, pieces, couplings, gb0=0, comm=None, s=0.0):
+        self.pieces = [P.tocsr() for P in pieces]
+        self.couplings = dict(couplings)
+        self.gb0 = gb0
+        self.comm = comm
+        self.s = s
+        self.sizes = [P.shape[0] for P in self.pieces]
+        self.bounds = np.cumsum([0] + self.sizes)
+        self.hmax = max([max(nr, nc) for nr, nc, _ in self.couplings.values()] or [0])
+
+    def matvec_R(self, v):
+        out = np.empty_like(v)
+        nb = len(self.pieces)
+        for k, P in enumerate(self.pieces):
+            out[self.bounds[k]:self.bounds[k + 1]] = P @ v[self.bounds[k]:self.bounds[k + 1]]
+        head = {self.gb0 + k: v[self.bounds[k]:self.bounds[k] + self.hmax] for k in range(nb)}
+        tail = {self.gb0 + k: v[max(self.bounds[k], self.bounds[k + 1] - self.hmax):self.bounds[k + 1]]
+                for k in range(nb)}
+        if self.comm is not None:   # the neighbours' pieces next to this rank's
+            first, last = self.gb0, self.gb0 + nb - 1
+            got = self.comm.allgather((first, head[first], last, tail[last]))
+            for f, h, l_, t in got:
+                head.setdefault(f, h)
+                tail.setdefault(l_, t)
+        for gb in sorted(self.couplings):
+            nr, nc, C = self.couplings[gb]
+            k = gb - self.gb0
+            if 0 <= k < nb:                  # gb's tail rows
+                out[self.bounds[k + 1] - nr:self.bounds[k + 1]] += C @ head[gb + 1][:nc]
+            if 0 <= k + 1 < nb:              # gb + 1's head rows
+                out[self.bounds[k + 1]:self.bounds[k + 1] + nc] += C.T @ tail[gb][-nr:]
+        return out
+
+    def matvec_Rs(self, v):
+        if self.s == 0.0:
+            return self.matvec_R(v)
+        return (1 - self.s) * self.matvec_R(v) + self.s * v
+
+
 class PanelLD:
     """Block-diagonal LD held as the upper triangle of each block in panels of
     ``H`` rows -- panel g of a block stores rows r0 = H*g .. r0+h-1 over columns

@@ -193,3 +193,94 @@ def test_socket_comm_collectives(world):
             [np.arange(3.0) + 10 * i for i in range(world)]))
         assert out["empty"].shape == (0,)
         assert abs(out["big"] - want_big) < 1e-6
+
+
+# ---- one band block over two ranks (coupled pieces) -----------------------------------
+_BAND = dict(M=70000, bw=600, N=5000, its=4, piece=16384)
+
+
+def _band_problem():
+    import scipy.sparse
+
+    from sgvamp import BlockLD, band_cuts
+
+    A = vo.banded_ld(_BAND["M"], _BAND["bw"], seed=9, taps=12)
+    L = BlockLD.from_csr(A)
+    cuts = band_cuts([L], L.block_sizes, piece=_BAND["piece"])
+    P, cpl = L.pieces(cuts)
+    pieces = [P.block_csr(k) for k in range(len(P.block_sizes))]
+    cpl = {gb: (nr, nc, C.toarray() if scipy.sparse.issparse(C) else C)
+           for gb, (nr, nc, C) in cpl.items()}
+    rs = np.random.RandomState(4)
+    M, N = _BAND["M"], _BAND["N"]
+    beta = np.zeros(M)
+    idx = rs.choice(M, M // 20, replace=False)
+    beta[idx] = rs.normal(0, np.sqrt(0.5 / len(idx)), len(idx))
+    x0 = beta * np.sqrt(N)
+    r = A @ x0 + rs.normal(0, 1.0, M)
+    kw = dict(rho=0.5, gamw=5.0, gam1=1e-6, prior_vars=[0.0, 0.5 / len(idx)],
+              prior_probs=[0.95, 0.05], seed=5)
+    return pieces, cpl, r, x0, kw
+
+
+def _band_rank(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), SGV_COMM_PORT=str(port))
+        from comm import world_from_env
+        from partition import partition_blocks
+
+        comm = world_from_env()
+        pieces, cpl, r, x0, kw = _band_problem()
+        sizes = [P.shape[0] for P in pieces]
+        ranges = partition_blocks(sizes, world)
+        b0, b1 = ranges[rank]
+        offs = np.cumsum([0] + sizes)
+        sl = slice(offs[b0], offs[b1])
+        L = vo.CoupledLD(pieces[b0:b1], cpl, gb0=b0, comm=comm)
+        red = vo.Reducer("blocked", bounds=L.bounds, comm=_GlooBlocks(comm))
+        streams = vo.ProbeStream(kw["seed"], 1)
+        probe = lambda k, it: streams.draw(k, _BAND["M"])[sl]
+        t = vo.infer([L], [0], [r[sl]], [_BAND["N"]], _BAND["its"], x0=x0[sl], reducer=red,
+                     M_total=_BAND["M"], probe=probe, **kw)
+        comm.barrier()
+        q.put((rank, np.array(t["xhat"]), np.array(t["cg_iters"]), (b0, b1)))
+    except Exception:  # surface the failure in the parent
+        import traceback
+
+        q.put((rank, "ERROR", traceback.format_exc(), None))
+
+
+def test_band_block_over_two_ranks_is_bit_identical():
+    """One band block cut into coupled pieces (the product's band_cuts /
+    BlockLD.pieces), two socket ranks owning two pieces each: the sharded
+    oracle -- pieces' products plus the corner couplings, the neighbour's head /
+    tail rows all-gathered -- is bitwise the one-rank run (VERDICT round 3,
+    item 6: one chromosome no longer means one GPU)."""
+    world = 2
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_band_rank, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        item = q.get(timeout=300)
+        assert not isinstance(item[1], str), item[2]
+        res[item[0]] = item
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0][3] == (0, 2) and res[1][3] == (2, 4)     # two pieces each
+    pieces, cpl, r, x0, kw = _band_problem()
+    L = vo.CoupledLD(pieces, cpl)
+    t = vo.infer([L], [0], [r], [_BAND["N"]], _BAND["its"], x0=x0,
+                 reducer=vo.Reducer("blocked", bounds=L.bounds), **kw)
+    xh = np.concatenate([res[k][1] for k in range(world)], axis=1)
+    np.testing.assert_array_equal(xh, np.array(t["xhat"]))
+    np.testing.assert_array_equal(res[0][2], np.array(t["cg_iters"]))
+    # and the pieces with their couplings are the band itself
+    A = vo.banded_ld(_BAND["M"], _BAND["bw"], seed=9, taps=12)
+    v = np.random.RandomState(0).normal(size=_BAND["M"])
+    np.testing.assert_allclose(L.matvec_R(v), A @ v, rtol=0, atol=1e-12)
