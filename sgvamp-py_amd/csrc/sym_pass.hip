@@ -246,36 +246,50 @@ hipError_t launch_sym_pass(int nc, int cls, const SymItem* d_items, int nitems,
 }
 
 // ---- coupled band pieces --------------------------------------------------
-// One workgroup per CouplingTask, one thread per output row: y[c] = sum over
-// k (in order) of m[k][row] * p[k][c] -- a fixed order on every rank, so the
-// coupling sums are the same whichever rank holds the source rows.  Remote
-// sources sit in the gathered halo [rank][2][nc][hstride]: task.src = 2 rank +
-// slot.  Rows of a slot no task writes stay as cleared by the caller.
+// One workgroup per (CouplingTask, 64-row quarter): thread (q, r) sums the
+// inner index range [q L, (q + 1) L) (L = ceil(inner / 4), in order) for output
+// row 64 y + r, and the 4 parts are added in order 0..3 -- a fixed order on
+// every rank, so the coupling sums are the same whichever rank holds the
+// source rows.  Remote sources sit in the gathered halo [rank][2][nc][hstride]:
+// task.src = 2 rank + slot.  Rows of a slot no task writes stay as cleared.
 template <int NC>
 __global__ __launch_bounds__(256) void k_coupling(const CouplingTask* __restrict__ tasks,
                                                   PassArgs pa, const double* __restrict__ halo,
                                                   int64_t hstride, double* __restrict__ cpbuf) {
+  __shared__ double part[3][64][NC];
   const CouplingTask tk = tasks[blockIdx.x];
   if (pa.run && !ldg(pa.run)) return;
-  const int r = threadIdx.x;
-  if (r >= tk.nrows) return;
-  const double* src[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c)
-    src[c] = tk.local ? pa.in[c] + tk.src : halo + (tk.src * NC + c) * hstride;
-  const double* m = tk.m + tk.row0 + r;
+  const int r = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int row = 64 * blockIdx.y + r;                 // within the task
+  const bool live = row < tk.nrows;
+  const int L = (tk.inner + 3) / 4;
+  const int k0 = q * L, k1 = min(tk.inner, k0 + L);
   double y[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) y[c] = 0.0;
+  if (live) {
+    const double* src[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c)
+      src[c] = tk.local ? pa.in[c] + tk.src : halo + (tk.src * NC + c) * hstride;
+    const double* m = tk.m + tk.row0 + row;
 #pragma unroll 4
-  for (int k = 0; k < tk.inner; ++k) {
-    const double a = m[(int64_t)k * tk.ldm];
+    for (int k = k0; k < k1; ++k) {
+      const double a = m[(int64_t)k * tk.ldm];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) y[c] += a * ldg(src[c] + k);
+      for (int c = 0; c < NC; ++c) y[c] += a * ldg(src[c] + k);
+    }
   }
-  double* out = cpbuf + ((int64_t)tk.cp * 256 + tk.prow0 + r) * NC;
+  if (q > 0) {
 #pragma unroll
-  for (int c = 0; c < NC; ++c) out[c] = y[c];
+    for (int c = 0; c < NC; ++c) part[q - 1][r][c] = y[c];
+  }
+  __syncthreads();
+  if (q == 0 && live) {
+    double* out = cpbuf + ((int64_t)tk.cp * 256 + tk.prow0 + row) * NC;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) out[c] = ((y[c] + part[0][r][c]) + part[1][r][c]) + part[2][r][c];
+  }
 }
 
 hipError_t launch_coupling(int nc, const CouplingTask* d_tasks, int ntasks, const PassArgs& pa,
@@ -286,7 +300,7 @@ hipError_t launch_coupling(int nc, const CouplingTask* d_tasks, int ntasks, cons
   if (e != hipSuccess) return e;
 #define CPL_CASE(N)                                                                         \
   case N:                                                                                   \
-    hipLaunchKernelGGL(k_coupling<N>, dim3(ntasks), dim3(256), 0, st, d_tasks, pa, halo,    \
+    hipLaunchKernelGGL(k_coupling<N>, dim3(ntasks, 4), dim3(256), 0, st, d_tasks, pa, halo, \
                        hstride, cpbuf);                                                     \
     break;
   switch (nc) {

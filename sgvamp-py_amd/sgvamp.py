@@ -47,6 +47,9 @@ DENSE_BLOCK_LIMIT = int(os.environ.get("SGV_DENSE_BLOCK_LIMIT", str(16 << 30)))
 # on the rank count, so 1 and N ranks compute the same sums.  SGV_BAND_PIECE
 # (a multiple of 1024) changes the piece length, 0 disables the cut.
 BAND_PIECE = int(os.environ.get("SGV_BAND_PIECE", "65536"))
+# widest band cut into pieces: a coupling is a dense bw x bw corner on each of
+# the two ranks (128 MB at 4,096); wider bands stay one block
+BAND_CUT_MAX_BW = 4096
 
 
 def csr_bandwidth(U, chunk=1 << 16):
@@ -249,8 +252,8 @@ class BlockLD:
 def band_cuts(lds, sizes, piece=None):
     """Piece sizes per block of the common partition (see BAND_PIECE): a block is
     cut when every LD matrix holds it as a symmetric sparse band of bandwidth <=
-    piece / 4 and it spans at least two pieces.  A function of the matrices
-    only (the same for every rank count)."""
+    min(piece / 4, BAND_CUT_MAX_BW) and it spans at least two pieces.  A function
+    of the matrices only (the same for every rank count)."""
     piece = BAND_PIECE if piece is None else int(piece)
     out = []
     for b, n in enumerate(sizes):
@@ -259,7 +262,7 @@ def band_cuts(lds, sizes, piece=None):
             out.append([n])
             continue
         bws = [L.band_width(b) for L in lds]
-        if any(w is None or w > piece // 4 for w in bws):
+        if any(w is None or w > min(piece // 4, BAND_CUT_MAX_BW) for w in bws):
             out.append([n])
             continue
         k = n // piece
