@@ -74,7 +74,7 @@ struct LdPlan {
   SymPanel* d_spanels = nullptr;
   int nstrips = 0;
   bool ragged = false;         // some strip item is narrower than its strip (band blocks)
-  bool pair = false;           // NC <= 8 passes run k_sym_mfma_pair (build_strips)
+  int pair = 0;                // k_sym_mfma_pair for 3-4 columns (1) / 3-8 (2) (build_strips)
   double stored_bytes = 0.0, dense_bytes = 0.0;
   // coupled band pieces: k_coupling tasks, panel slots of PassArgs::cpbuf, and
   // the halo this rank sends (head of its first block, tail of its last) when a
@@ -745,14 +745,15 @@ static double lpt_efficiency(std::vector<double> cost, int slots) {
 // NC <= 8 MFMA passes: the 4-wave kernel (two 4-wave workgroups per CU, 512
 // slots) or the wave-pair kernel (one 8-wave workgroup per CU, a strip in half
 // the time: 256 slots at half the cost) -- bitwise the same products, so the
-// choice is free per plan.  Auto: the pair kernel when its launch drains with
-// at least SGV_MF_PAIR_GAIN (default 3 %) less tail by the strips' model cost
-// (a few strips per slot: an 8-block share of the north star); SGV_MF_PAIR=0/1
-// (with SGV_AB=1) forces either.
-static bool mfma_pair_choice(const std::vector<SymStrip>& strips,
-                             const std::vector<SymItem>& sitems) {
+// choice is free per plan.  Auto (1): the pair kernel for 3-4-column passes
+// when its launch drains with at least SGV_MF_PAIR_GAIN (default 3 %) less tail
+// by the strips' model cost (a few strips per slot: an 8-block share of the
+// north star); SGV_MF_PAIR=0 / 1 (with SGV_AB=1) forces none / every 3-8-column
+// pass (2).
+static int mfma_pair_choice(const std::vector<SymStrip>& strips,
+                            const std::vector<SymItem>& sitems) {
   const char* e = ab_env("SGV_MF_PAIR");
-  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1';
+  if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1' ? 2 : 0;
   int dev = 0, ncu = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
     hipDeviceProp_t prop;
@@ -770,7 +771,7 @@ static bool mfma_pair_choice(const std::vector<SymStrip>& strips,
   const double pair = lpt_efficiency(cost, ncu);   // per slot: twice the speed, same ratio
   const char* g = std::getenv("SGV_MF_PAIR_GAIN");
   const double gain = g && *g ? std::atof(g) : 0.03;
-  return pair >= quad + gain;
+  return pair >= quad + gain ? 1 : 0;
 }
 
 // MFMA strips of one LD matrix from the class-1 (512-column) tables.  Chunk
@@ -844,7 +845,7 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
   pl->ragged = false;
   for (const SymStrip& st : strips)
     for (int i = 0; i < st.npan; ++i) pl->ragged |= sitems[st.it0 + i].nc < st.ncmax;
-  pl->pair = !pl->ragged && mfma_pair_choice(strips, sitems);
+  pl->pair = pl->ragged ? 0 : mfma_pair_choice(strips, sitems);
   CHK(upload_table(c, strips, &pl->d_strips));
   CHK(upload_table(c, sitems, &pl->d_sitems));
   CHK(upload_table(c, sp, &pl->d_spanels));

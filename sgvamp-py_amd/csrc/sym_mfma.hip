@@ -979,34 +979,42 @@ static int mf_xpose() {
   return v;
 }
 
-// SGV_MF_PAIR_MAP (A/B, with SGV_AB=1): k_sym_mfma_pair's wave map, default 0
+// SGV_MF_PAIR_MAP (A/B, with SGV_AB=1): k_sym_mfma_pair's form -- 0 waves 2s,
+// 2s + 1 per segment with a barrier per row group, 1 the pair on one SIMD, 2 / 3
+// those with per-pair LDS counters instead of the barriers; default 3 (best of
+// the four at 4 and 8 columns, profiles/r04/pairsync_ab.jsonl)
 static int mf_pair_map() {
   static const int v = [] {
     const char* e = ab_env("SGV_MF_PAIR_MAP");
-    return (e && e[0] >= '1' && e[0] <= '3') ? e[0] - '0' : 0;
+    return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
   }();
   return v;
 }
+
 
 // ragged: some strip item stops short of its strip's widest (band blocks): the
 // RAG kernels (default variant only: the A/B switches do not apply there)
 template <int NG, int NW, int PD>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
-                      const int* run, int pks, bool ragged, bool pair, hipStream_t st) {
+                      const int* run, int pks, bool ragged, int pair, hipStream_t st) {
   if (ragged)
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, true>), dim3(nstrips), dim3(NW * 64), 0,
                        st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (pair && mf_pair_map() == 2)   // 2: MAP 0 + counters, 3: MAP 1 + counters
-    hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0, 0, 1>), dim3(nstrips), dim3(512), 0, st, d_strips,
-                       d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (pair && mf_pair_map() == 3)
+  else if (pair >= (NG == 1 ? 1 : 2) && mf_pair_map() == 3)
+    // the plan's choice (capi.hip build_strips; bitwise the same products): 3-4
+    // pair 1: 3-4 columns only -- at 5-8 the pair form runs ~14 % slower per
+    // byte (profiles/r04/pairsync_ab.jsonl) and a short launch's tail does not
+    // pay it back; pair 2 (forced, SGV_MF_PAIR=1): every column count
     hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0, 1, 1>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (pair && mf_pair_map() == 1)
+  else if (pair >= (NG == 1 ? 1 : 2) && mf_pair_map() == 2)
+    hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0, 0, 1>), dim3(nstrips), dim3(512), 0, st, d_strips,
+                       d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (pair >= (NG == 1 ? 1 : 2) && mf_pair_map() == 1)
     hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0, 1>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (pair)   // the plan's choice (capi.hip build_strips): bitwise the same products
+  else if (pair >= (NG == 1 ? 1 : 2))
     hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else if (mf_pw() && mf_skip() && mf_defer() && mf_xpose() == 1)
@@ -1031,7 +1039,7 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
 
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                            const PassArgs& pa, int64_t mpad, double* d_pk, double* rowpart,
-                           double* colpart, bool ragged, bool pair, hipStream_t st) {
+                           double* colpart, bool ragged, int pair, hipStream_t st) {
   if (nc < 1 || nc > 16) return hipErrorInvalidValue;
   static const hipError_t band_skip_set = [] {   // SGV_BAND_SKIP=0: the A/B's old band steps
     const char* e = ab_env("SGV_BAND_SKIP");

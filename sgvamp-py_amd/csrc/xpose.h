@@ -47,7 +47,10 @@ __device__ __forceinline__ void xpose_perm(const d2* cf, d2* rf, bool l1, bool l
     unsigned v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const unsigned long long u = __builtin_bit_cast(unsigned long long, cf[r][e >> 1]);
+      // through a scalar: __builtin_bit_cast of a vector-element lvalue reads
+      // element 0 whatever the index (clang, ROCm 7.2)
+      const double d = cf[r][e >> 1];
+      const unsigned long long u = __builtin_bit_cast(unsigned long long, d);
       v[r] = (unsigned)(e & 1 ? u >> 32 : u);
     }
     xp_rows(v);
@@ -58,7 +61,8 @@ __device__ __forceinline__ void xpose_perm(const d2* cf, d2* rf, bool l1, bool l
     xp_rows(v);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      unsigned long long u = __builtin_bit_cast(unsigned long long, rf[r][e >> 1]);
+      const double d = rf[r][e >> 1];
+      unsigned long long u = __builtin_bit_cast(unsigned long long, d);
       u = e & 1 ? ((u & 0xFFFFFFFFull) | ((unsigned long long)v[r] << 32))
                 : ((u & 0xFFFFFFFF00000000ull) | v[r]);
       rf[r][e >> 1] = __builtin_bit_cast(double, u);
@@ -70,7 +74,8 @@ __device__ __forceinline__ void xpose_bperm(const d2* cf, d2* rf, int src4) {
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const unsigned long long u = __builtin_bit_cast(unsigned long long, cf[r][e]);
+      const double d = cf[r][e];   // a scalar first (see xpose_perm)
+      const unsigned long long u = __builtin_bit_cast(unsigned long long, d);
       const unsigned lo32 = (unsigned)__builtin_amdgcn_ds_bpermute(src4, (int)(unsigned)u);
       const unsigned hi32 = (unsigned)__builtin_amdgcn_ds_bpermute(src4, (int)(unsigned)(u >> 32));
       rf[r][e] = __builtin_bit_cast(double, (unsigned long long)lo32 | ((unsigned long long)hi32 << 32));
