@@ -248,6 +248,11 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
 #pragma unroll
         for (int q = 0; q < NG; ++q) drow[r][q] = 0.0;
       const bool colz = SKIP && dhalf && cur.r0 == c0;   // this panel's column B operands are 0
+      // a band item narrower than its strip (its panel's last 256 columns): a
+      // step wholly past its stored end adds only zeros -- skipped like the
+      // steps past the chunk (band_rag_skip, default on); per panel, so the
+      // deferred row MFMAs (DEF) know the item's last active step
+      const int ntp = (RAG && band_rag_skip()) ? min(nta, max(0, (cur.nc - cw0 + 31) / 32)) : nta;
       d2 rfb[DEF ? 2 : 1][4];                            // row fragments (DEF: this and the previous step)
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -263,11 +268,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
           load_cf(gb, gw, gH, gnc, gn, t + PD - NT, cfq[slot]);
           if (t + PD == NT) load_bcol(gr0, gH, gz, gn, bcn);
         }
-        if (t >= nta) continue;                        // wave-uniform: past the chunk
-        // a band item narrower than its strip (its panel's last 256 columns):
-        // a step wholly past its stored end adds only zeros -- skipped like the
-        // steps past the chunk (band_rag_skip, default on)
-        if (RAG && cw0 + 32 * t >= cur.nc && band_rag_skip()) continue;
+        if (t >= ntp) continue;                        // wave-uniform: past the chunk / item
         if (RAG && cur.nc < ncc) band_zero(cur.nc, t, cf);   // uniform: a band item's stored end
         if constexpr (XP == 1) {
           xpose_perm(cf, rf, xl1, xl0);
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
             }
           }
           // the row group's last active step: its own row MFMAs now
-          if (t == NT - 1 || t + 1 == nta) row_mfma(rf, t);
+          if (t == NT - 1 || t + 1 == ntp) row_mfma(rf, t);
         } else {
           if (!colz) {
 #pragma unroll
@@ -979,6 +980,16 @@ static int mf_xpose() {
   return v;
 }
 
+// SGV_BAND_DEF (A/B, with SGV_AB=1): band plans' NC <= 8 kernel with the
+// deferred row MFMAs (1, bitwise the same products) or without (0, round 3)
+static bool band_def() {
+  static const bool v = [] {
+    const char* e = ab_env("SGV_BAND_DEF");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 // SGV_MF_PAIR_MAP (A/B, with SGV_AB=1): k_sym_mfma_pair's form -- 0 waves 2s,
 // 2s + 1 per segment with a barrier per row group, 1 the pair on one SIMD, 2 / 3
 // those with per-pair LDS counters instead of the barriers; default 3 (best of
@@ -998,7 +1009,10 @@ template <int NG, int NW, int PD>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
                       const int* run, int pks, bool ragged, int pair, hipStream_t st) {
-  if (ragged)
+  if (ragged && band_def())
+    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, true, true>), dim3(nstrips),
+                       dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (ragged)
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, true>), dim3(nstrips), dim3(NW * 64), 0,
                        st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else if (pair >= (NG == 1 ? 1 : 2) && mf_pair_map() == 3)
@@ -1073,7 +1087,10 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
     case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
     case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
     default:
-      if (ragged)
+      if (ragged && mf16_pd() == 2)   // band plans at the dense plans' prefetch depth
+        hipLaunchKernelGGL((k_sym_mfma16<2, true, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
+                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
+      else if (ragged)
         hipLaunchKernelGGL((k_sym_mfma16<1, true, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
                            d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       else if (mf16_pd() == 2)
