@@ -981,11 +981,12 @@ static int mf_xpose() {
 }
 
 // SGV_BAND_DEF (A/B, with SGV_AB=1): band plans' NC <= 8 kernel with the
-// deferred row MFMAs (1, bitwise the same products) or without (0, round 3)
+// deferred row MFMAs (1, bitwise the same products) or without (0, default:
+// 2.15-2.16 vs 2.145-2.15 ms at M = 1e6, bw = 1,000, profiles/r04/band2_ab.jsonl)
 static bool band_def() {
   static const bool v = [] {
     const char* e = ab_env("SGV_BAND_DEF");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return v;
 }
@@ -1088,6 +1089,8 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
     case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
     default:
       if (ragged && mf16_pd() == 2)   // band plans at the dense plans' prefetch depth
+        // (7 VGPRs spilled, still -2.3 %: 2.58-2.59 vs 2.64-2.65 ms at M = 1e6, bw =
+        // 1,000, bitwise the same products, profiles/r04/band2_ab.jsonl)
         hipLaunchKernelGGL((k_sym_mfma16<2, true, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
                            d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       else if (ragged)
