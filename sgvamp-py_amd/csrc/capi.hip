@@ -75,6 +75,8 @@ struct LdPlan {
   int nstrips = 0;
   bool ragged = false;         // some strip item is narrower than its strip (band blocks)
   int pair = 0;                // k_sym_mfma_pair for 3-4 columns (1) / 3-8 (2) (build_strips)
+  int cw = 512;                // the MFMA strips' chunk width (256: band plans)
+  bool band256 = false;        // the strips were rebuilt from class-2 items
   double stored_bytes = 0.0, dense_bytes = 0.0;
   // coupled band pieces: k_coupling tasks, panel slots of PassArgs::cpbuf, and
   // the halo this rank sends (head of its first block, tail of its last) when a
@@ -726,6 +728,14 @@ static int mfma_strip_len() {
   return std::max(1, std::min(64, v));
 }
 
+// SGV_BAND_CW (A/B, with SGV_AB=1): band plans' MFMA strips over 256-column
+// chunks (default) or, as in round 3, 512-column ones whose first item is half
+// empty (the waves past its stored end idle)
+static bool band_cw256() {
+  const char* e = ab_env("SGV_BAND_CW");
+  return !(e && e[0] == '5');
+}
+
 // Longest-processing-time makespan of `cost` on `slots` identical slots, as a
 // fraction of the perfect split (the dispatcher hands the strips out in this
 // order, most panels first, to whichever slot frees first)
@@ -782,8 +792,11 @@ static int mfma_pair_choice(const std::vector<SymStrip>& strips,
 // and of panel G + 1's rows (offset 256, "other").  Dispatch order: most panels
 // first (the short strips fill the tail).
 static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
-                        const std::vector<SymPanel>& panels, LdPlan* pl) {
+                        const std::vector<SymPanel>& panels, LdPlan* pl, int cw = 512) {
   const int S = mfma_strip_len();
+  // chunk alignment classes: 512-column chunks start at 256 p + 512 k (panels of
+  // parity p share them), 256-column chunks at every 256 k (every panel)
+  const int NPAR = cw / SYM_H;
   std::vector<SymItem> sitems;
   std::vector<SymStrip> strips;
   std::vector<SymPanel> sp = panels;
@@ -792,23 +805,23 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
     if (c->ldb[ld][b].fmt != 1) continue;
     const int64_t n = c->bn[b];
     const int np = (int)c->ldb[ld][b].poff.size();
-    for (int p = 0; p < 2; ++p)
-      for (int64_t c0 = (int64_t)SYM_H * p; c0 < n; c0 += 2 * SYM_H) {
+    for (int p = 0; p < NPAR; ++p)
+      for (int64_t c0 = (int64_t)SYM_H * p; c0 < n; c0 += cw) {
         const int G = (int)(c0 / SYM_H);
         const int sb = (int)strips.size();
         // a band block's panel g reaches c0 iff c0 - 256 g < ext (ext = e
-        // panels: the panels G - 2 floor((e - 1) / 2), ..., G of this parity)
+        // panels: the panels G - NPAR floor((e - 1) / NPAR), ..., G of this class)
         const int64_t ext = c->ldb[ld][b].ext;
-        const int glo = ext > 0 ? std::max(p, G - 2 * (((int)(ext / SYM_H) - 1) / 2)) : p;
-        for (int g0 = glo; g0 <= G; g0 += 2 * S) {
+        const int glo = ext > 0 ? std::max(p, G - NPAR * (((int)(ext / SYM_H) - 1) / NPAR)) : p;
+        for (int g0 = glo; g0 <= G; g0 += NPAR * S) {
           SymStrip st;
           st.it0 = (int)sitems.size();
           st.npan = 0;
           st.slot = (int)strips.size();
           st.ncmax = 0;
-          for (int g = g0; g <= G && g < g0 + 2 * S; g += 2) {
+          for (int g = g0; g <= G && g < g0 + NPAR * S; g += NPAR) {
             const SymPanel& pn = panels[bp0 + g];
-            const int idx = pn.item_begin + (int)((c0 - (int64_t)SYM_H * g) / (2 * SYM_H));
+            const int idx = pn.item_begin + (int)((c0 - (int64_t)SYM_H * g) / cw);
             if (idx >= pn.item_end || items[idx].c0 != c0)
               return fail(c, SGV_ERR_STATE, "strip plan: item (%d, %lld) missing", g,
                           (long long)c0);
@@ -820,7 +833,7 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
         }
         sp[bp0 + G].own_sb = sb;
         sp[bp0 + G].own_se = (int)strips.size();
-        if (G + 1 < np) {
+        if (NPAR == 2 && G + 1 < np) {
           sp[bp0 + G + 1].oth_sb = sb;
           sp[bp0 + G + 1].oth_se = (int)strips.size();
         }
@@ -842,10 +855,13 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
       return wa > wb;
     });
   pl->nstrips = (int)strips.size();
+  pl->cw = cw;
   pl->ragged = false;
   for (const SymStrip& st : strips)
     for (int i = 0; i < st.npan; ++i) pl->ragged |= sitems[st.it0 + i].nc < st.ncmax;
-  pl->pair = pl->ragged ? 0 : mfma_pair_choice(strips, sitems);
+  if (cw != 512 && pl->ragged)
+    return fail(c, SGV_ERR_STATE, "strip plan: a %d-column strip with a narrower item", cw);
+  pl->pair = (pl->ragged || cw != 512) ? 0 : mfma_pair_choice(strips, sitems);
   CHK(upload_table(c, strips, &pl->d_strips));
   CHK(upload_table(c, sitems, &pl->d_sitems));
   CHK(upload_table(c, sp, &pl->d_spanels));
@@ -1039,13 +1055,25 @@ static int ensure_plan(sgv_ctx* c, int ld) {
       CHK(upload_table(c, order, &pl.d_items[cls]));
     }
     CHK(upload_table(c, panels, &pl.d_panels[cls]));
-    if (cls == 1) CHK(build_strips(c, ld, items, panels, &pl));
+    if (cls == 1) {
+      CHK(build_strips(c, ld, items, panels, &pl));
+      if (pl.ragged && band_cw256()) {   // band plan: 256-column strips (class 2)
+        if (pl.d_strips) HIPCHK(hipFree(pl.d_strips));
+        if (pl.d_sitems) HIPCHK(hipFree(pl.d_sitems));
+        if (pl.d_spanels) HIPCHK(hipFree(pl.d_spanels));
+        pl.d_strips = nullptr;
+        pl.d_sitems = nullptr;
+        pl.d_spanels = nullptr;
+        pl.band256 = true;
+      }
+    }
+    if (cls == 2 && pl.band256) CHK(build_strips(c, ld, items, panels, &pl, 256));
     const size_t ncmax = (size_t)sym_class_nc(cls);
     rowpart_need = std::max(rowpart_need, items.size() * SYM_H * ncmax);
     colpart_need = std::max(colpart_need, items.size() * ncmax * (size_t)cw);
   }
-  if (pl.npanels) {   // the MFMA pass: class-1 items with up to 16 columns
-    rowpart_need = std::max(rowpart_need, (size_t)pl.nitems[1] * SYM_H * MAXC);
+  if (pl.npanels) {   // the MFMA pass: class-1 (band: class-2) items with up to 16 columns
+    rowpart_need = std::max(rowpart_need, (size_t)pl.nitems[pl.band256 ? 2 : 1] * SYM_H * MAXC);
     colpart_need = std::max(colpart_need, (size_t)pl.nstrips * MAXC * 512);
     CHK(grow(c, &c->d_pk, &c->pk_cap, (size_t)c->Mpad * 16));
   }
@@ -1106,10 +1134,11 @@ static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa_in) {
     const int cls = mf ? 1 : sym_class(nc);
     if (mf) {
       HIPCHK(launch_sym_mfma(nc, pl.d_strips, pl.nstrips, pl.d_sitems, pa, c->Mpad, c->d_pk,
-                             c->d_rowpart, c->d_colpart, pl.ragged, pl.pair, c->st));
+                             c->d_rowpart, c->d_colpart, pl.ragged, pl.pair, pl.cw, c->st));
       HIPCHK(launch_sym_finalize_strip(nc, pl.d_spanels, pl.npanels, pa, c->d_rowpart,
                                        c->d_colpart, c->d_part, c->st));
-      c->aux_bytes += 2.0 * 8.0 * nc * ((double)pl.nitems[cls] * SYM_H + (double)pl.nstrips * 512);
+      c->aux_bytes += 2.0 * 8.0 * nc * ((double)pl.nitems[pl.band256 ? 2 : cls] * SYM_H +
+                                        (double)pl.nstrips * pl.cw);
       c->aux_bytes += 8.0 * (double)c->Mpad * ((nc <= 4 ? 4 : nc <= 8 ? 8 : 16) + nc);   // Pk pack
     } else {
       HIPCHK(launch_sym_pass(nc, cls, pl.d_items[cls], pl.nitems[cls], pa, c->d_rowpart,

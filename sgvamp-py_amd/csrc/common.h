@@ -333,7 +333,7 @@ hipError_t launch_sym_pass(int nc, int cls, const SymItem* d_items, int nitems,
                            const PassArgs& pa, double* rowpart, double* colpart, hipStream_t st);
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                            const PassArgs& pa, int64_t mpad, double* d_pk, double* rowpart,
-                           double* colpart, bool ragged, int pair, hipStream_t st);
+                           double* colpart, bool ragged, int pair, int cw, hipStream_t st);
 hipError_t launch_sym_finalize_strip(int nc, const SymPanel* d_panels, int npanels,
                                      const PassArgs& pa, const double* rowpart,
                                      const double* colpart, double* partials, hipStream_t st);

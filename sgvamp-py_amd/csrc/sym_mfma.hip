@@ -99,7 +99,12 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // its column MFMAs, so consecutive MFMAs of one accumulator chain sit 8 issues
 // apart instead of 4 (2 at NG = 1); every chain accumulates in the same order
 // (bitwise the same sums), the row fragments are double-buffered in registers.
-template <int NG, int NW, int PD, bool PW, bool SKIP, bool RAG = false, bool DEF = false, int XP = 0>
+// CW: the strips' chunk width -- 512 (class-1 items), or 256 (class-2 items,
+// band plans: a band panel's stored extent is a multiple of 256, so no item of
+// a 256-column strip is narrower than its strip; with 512-column chunks every
+// band strip's first item is half empty, its waves 2-3 idle)
+template <int NG, int NW, int PD, bool PW, bool SKIP, bool RAG = false, bool DEF = false, int XP = 0,
+          int CW = MF_CW>
 __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
                                                          const SymItem* __restrict__ sitems,
                                                          const double* __restrict__ pk, int ncol,
@@ -107,7 +112,8 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
                                                          double* __restrict__ colpart,
                                                          const int* __restrict__ run, int pks) {
   static_assert(NW == 4, "waves 0 and 1 own the diagonal half of a chunk");
-  constexpr int WC = MF_CW / NW;   // columns per wave (128)
+  static_assert(CW == 512 || CW == 256, "chunk width");
+  constexpr int WC = CW / NW;      // columns per wave (128; 64 at CW = 256)
   constexpr int NT = WC / 32;      // 32-column steps per wave
   static_assert(PD >= 1 && PD <= NT && NT % PD == 0, "prefetch depth divides the steps");
   constexpr int RW = 4 * NG;       // row-sum stride of wrow
@@ -709,10 +715,7 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
 //   16x16x4 f64 C/D layout (cdna_hip_programming.md): D[(l>>4) + 4r][l & 15].
 typedef double d4 __attribute__((ext_vector_type(4)));
 #define MFMA16(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
-constexpr int MF_WC = MF_CW / 4;
-constexpr int MF_NT = MF_WC / 32;
-
-template <int PD, bool SKIP, bool RAG = false>
+template <int PD, bool SKIP, bool RAG = false, int CW = MF_CW>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -720,6 +723,8 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
                                                      double* __restrict__ colpart,
                                                      const int* __restrict__ run) {
   constexpr int LDP = MF_LDP;
+  constexpr int MF_WC = CW / 4;    // columns per wave
+  constexpr int MF_NT = MF_WC / 32;
   __shared__ double red[2][4][256];
   __shared__ __attribute__((aligned(16))) double stg[4][16 * LDP];
   const SymStrip sp = strips[blockIdx.x];
@@ -1009,8 +1014,11 @@ static int mf_pair_map() {
 template <int NG, int NW, int PD>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
-                      const int* run, int pks, bool ragged, int pair, hipStream_t st) {
-  if (ragged && band_def())
+                      const int* run, int pks, bool ragged, int pair, int cw, hipStream_t st) {
+  if (cw == 256)   // band plans' 256-column strips (no item narrower than its strip)
+    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, false, true, 0, 256>), dim3(nstrips),
+                       dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (ragged && band_def())
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, true, true>), dim3(nstrips),
                        dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else if (ragged)
@@ -1054,7 +1062,7 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
 
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                            const PassArgs& pa, int64_t mpad, double* d_pk, double* rowpart,
-                           double* colpart, bool ragged, int pair, hipStream_t st) {
+                           double* colpart, bool ragged, int pair, int cw, hipStream_t st) {
   if (nc < 1 || nc > 16) return hipErrorInvalidValue;
   static const hipError_t band_skip_set = [] {   // SGV_BAND_SKIP=0: the A/B's old band steps
     const char* e = ab_env("SGV_BAND_SKIP");
@@ -1085,10 +1093,13 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
   // measured in DESIGN.md
   switch ((nc + 3) / 4) {
     // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
-    case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
-    case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
+    case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, cw, st); break;
+    case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, cw, st); break;
     default:
-      if (ragged && mf16_pd() == 2)   // band plans at the dense plans' prefetch depth
+      if (cw == 256)
+        hipLaunchKernelGGL((k_sym_mfma16<2, true, false, 256>), dim3(nstrips), dim3(256), 0, st,
+                           d_strips, d_sitems, d_pk, nc, rowpart, colpart, pa.run);
+      else if (ragged && mf16_pd() == 2)   // band plans at the dense plans' prefetch depth
         // (7 VGPRs spilled, still -2.3 %: 2.58-2.59 vs 2.64-2.65 ms at M = 1e6, bw =
         // 1,000, bitwise the same products, profiles/r04/band2_ab.jsonl)
         hipLaunchKernelGGL((k_sym_mfma16<2, true, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
