@@ -83,3 +83,37 @@ def test_banded_ld_generator_properties():
     rows = np.repeat(np.arange(1200), np.diff(R.indptr))
     assert np.max(np.abs(R.indices - rows)) == 100
     assert np.linalg.eigvalsh(R.toarray()).min() > -1e-12
+
+
+def test_band_cut_into_coupled_pieces():
+    """One band block (one chromosome of windowed LD) is cut into pieces that
+    ranks can own (sgvamp.band_cuts / BlockLD.pieces): pieces of P markers (the
+    last up to 2P), consecutive ones coupled by the band's corner; the pieces'
+    diagonal blocks plus the couplings (and their transposes) are the matrix
+    itself.  The cut is a function of the matrix only: no rank count enters."""
+    from sgvamp import BAND_CUT_MAX_BW, band_cuts
+
+    A = vo.banded_ld(70_000, 600, seed=9, taps=12)
+    L = BlockLD.from_csr(A)
+    assert L.band_width(0) == 600
+    cuts = band_cuts([L], L.block_sizes, piece=16384)
+    assert cuts == [[16384, 16384, 16384, 70_000 - 3 * 16384]]
+    P, cpl = L.pieces(cuts)
+    assert P.block_sizes == cuts[0] and sorted(cpl) == [0, 1, 2]
+    offs = np.cumsum([0] + P.block_sizes)
+    B = scipy.sparse.block_diag([P.block_csr(k) for k in range(4)], format="lil")
+    for gb, (nr, nc, C) in cpl.items():
+        assert (nr, nc) == (600, 600)
+        cut = offs[gb + 1]
+        B[cut - nr:cut, cut:cut + nc] = C
+        B[cut:cut + nc, cut - nr:cut] = C.T
+    assert abs(B.tocsr() - A).max() == 0.0
+    # not cut: too short, too wide a band, or no piece length
+    assert band_cuts([L], L.block_sizes, piece=65536) == [[70_000]]
+    assert band_cuts([L], L.block_sizes, piece=2048) == [[70_000]]          # bw > piece / 4
+    W = BlockLD.from_csr(vo.banded_ld(40_000, BAND_CUT_MAX_BW + 8, seed=1, taps=4))
+    assert band_cuts([W], W.block_sizes, piece=16384) == [[40_000]]         # bw > 4,096
+    assert band_cuts([L], L.block_sizes, piece=0) == [[70_000]]
+    # dense sources are never cut
+    D = BlockLD(blocks=[np.eye(2)])
+    assert band_cuts([D], D.block_sizes, piece=1) == [[2]]
