@@ -728,12 +728,14 @@ static int mfma_strip_len() {
   return std::max(1, std::min(64, v));
 }
 
-// SGV_BAND_CW (A/B, with SGV_AB=1): band plans' MFMA strips over 256-column
-// chunks (default) or, as in round 3, 512-column ones whose first item is half
-// empty (the waves past its stored end idle)
+// SGV_BAND_CW=256 (A/B, with SGV_AB=1): band plans' MFMA strips over 256-column
+// chunks (no item narrower than its strip) instead of 512-column ones whose
+// first item is half empty.  Not faster (M = 1e6, bw = 1,000: 2.25 vs 2.17 ms at 8
+// columns, even at 4 and 16; 200k / 2,000: -2 % at 8 -- the doubled row partials
+// eat what the idle waves gave back; profiles/r04/b256_ab.jsonl): default 512
 static bool band_cw256() {
   const char* e = ab_env("SGV_BAND_CW");
-  return !(e && e[0] == '5');
+  return e && e[0] == '2';
 }
 
 // Longest-processing-time makespan of `cost` on `slots` identical slots, as a

@@ -5,11 +5,11 @@
 # the coupled-piece / band-over-ranks tests on the default.
 set -o pipefail
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q -k "band or coupled" \
-    --timeout 200 --timeout-method thread > gpurun_out/r04_b256_parity.log 2>&1 || { echo "band256 parity FAILED"; tail -30 gpurun_out/r04_b256_parity.log; exit 1; }
-echo "band256 parity: $(tail -1 gpurun_out/r04_b256_parity.log)"
-SGV_AB=1 SGV_BAND_CW=512 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q -k "band or coupled" \
-    --timeout 200 --timeout-method thread > gpurun_out/r04_b512_parity.log 2>&1 || { echo "band512 parity FAILED"; tail -30 gpurun_out/r04_b512_parity.log; exit 1; }
-echo "band512 parity: $(tail -1 gpurun_out/r04_b512_parity.log)"
+    --timeout 200 --timeout-method thread > gpurun_out/r04_b256_parity.log 2>&1 || { echo "band default parity FAILED"; tail -30 gpurun_out/r04_b256_parity.log; exit 1; }
+echo "band default parity: $(tail -1 gpurun_out/r04_b256_parity.log)"
+SGV_AB=1 SGV_BAND_CW=256 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -q -k "band or coupled" \
+    --timeout 200 --timeout-method thread > gpurun_out/r04_b512_parity.log 2>&1 || { echo "band256 (A/B) parity FAILED"; tail -30 gpurun_out/r04_b512_parity.log; exit 1; }
+echo "band256 (A/B) parity: $(tail -1 gpurun_out/r04_b512_parity.log)"
 timeout -k 10 400 python -u -m pytest tests/test_gpu_multirank.py -x -q -k "single_band_block" \
     --timeout 280 --timeout-method thread > gpurun_out/r04_b256_ranks.log 2>&1 || { echo "band ranks FAILED"; tail -30 gpurun_out/r04_b256_ranks.log; exit 1; }
 echo "band over ranks: $(tail -1 gpurun_out/r04_b256_ranks.log)"
