@@ -93,7 +93,30 @@ def parse():
                         "without touching the GPU (checks the launch)")
     p.add_argument("--ld-format", choices=["packed", "dense"], default="packed",
                    help="LD block storage: packed symmetric panels (default) or full squares")
+    p.add_argument("--band", default=None, metavar="M,BW",
+                   help="one chromosome of windowed LD instead of the device-generated blocks: "
+                        "M markers, bandwidth BW (simulate.windowed_ld, CSR on the host: the "
+                        "reference's .npz / PLINK .ld path, src/main.py:199-200,251-257); long "
+                        "bands are cut into coupled pieces the ranks share")
     return p.parse_args()
+
+
+def band_problem(args, K):
+    """--band: the windowed LD (every rank builds the same CSR), r_k = R x0 +
+    N(0, 1) noise per cohort, x0 = beta * sqrt(N) with 5 % causal markers."""
+    from simulate import windowed_ld
+
+    M, bw = (int(x) for x in args.band.split(","))
+    A = windowed_ld(M, bw, seed=args.seed)
+    rs = np.random.RandomState(args.seed)
+    cm = max(1, M // 20)
+    beta = np.zeros(M)
+    beta[rs.choice(M, cm, replace=False)] = rs.normal(0, np.sqrt(0.5 / cm), cm)
+    x0 = beta * np.sqrt(args.nsamp)
+    Ax0 = A @ x0
+    r = np.stack([Ax0 + np.random.RandomState(args.seed + 1000 + k).normal(0.0, 1.0, M)
+                  for k in range(K)])
+    return A, r, x0, cm
 
 
 def make_problem(eng, comm, args):
@@ -336,39 +359,55 @@ def main():
     K = args.K
     t_setup = time.perf_counter()
     ld_of = list(range(K)) if args.distinct_ld else [0] * K
-    eng = Engine(sizes, K, ld_of=ld_of, comm=comm, device=device,
-                 exchange="host" if args.share_device else
-                 (None if args.exchange == "auto" else args.exchange))
-    eng.set_ld_packing(args.ld_format == "packed")
-    beta, _ = make_problem(eng, comm, args)
+    exchange = "host" if args.share_device else (None if args.exchange == "auto" else args.exchange)
     N_list = [args.nsamp] * K
     Nt = sum(N_list)
     a = np.array(N_list) / Nt
-    cm = int(eng.M * 0.5)
-    if args.prior == "matched":
+    if args.band:
+        band_A, band_r, x0, cm = band_problem(args, K)
+        M_run = band_A.shape[0]
+        eng = None
+    else:
+        eng = Engine(sizes, K, ld_of=ld_of, comm=comm, device=device, exchange=exchange)
+        eng.set_ld_packing(args.ld_format == "packed")
+        beta, _ = make_problem(eng, comm, args)
+        M_run = eng.M
+        cm = int(eng.M * 0.5)
+    if args.band:
+        prior = dict(prior_vars=[0.0, 0.5 / cm * N_list[0] / Nt], prior_probs=[0.95, 0.05])
+    elif args.prior == "matched":
         # simulated effect variance 0.8/cm in x = beta*sqrt(N_k) scale is 0.8/cm * N_k; the
         # reference scales slab variances by Nt (src/sgvamp.py:27): 0.8/cm * N_k / Nt
         prior = dict(prior_vars=[0.0, 0.8 / cm * N_list[0] / Nt], prior_probs=[0.5, 0.5])
     else:
         prior = dict(prior_vars=[0.0, 1.0], prior_probs=[0.99, 0.01])
     flags = dict(rho=0.5, gamw=5.0, gam1=1e-6, **prior)
-    eng.set_ridge(args.ridge)
     run = dict(cg_maxit=500, em_prior_maxit=100, learn_gamw=True, lmmse_damp=bool(args.lmmse_damp),
                prior_update="em", update_prior_from=1)
     tmp = args.out_dir or tempfile.mkdtemp(prefix="sgvamp_bench_")
     os.makedirs(tmp, exist_ok=True)
-    v = VAMP(N=N_list if K > 1 else N_list[0], Nt=Nt, M=eng.M, K=K, a=a, out_dir=tmp,
-             out_name="bench", comm=comm, seed=args.seed, write_files=not args.no_files, **flags)
-    x0 = beta * np.sqrt(N_list[0])                      # main.py:276-279
-    v.attach_engine(eng, x0=x0)
+    v = VAMP(N=N_list if K > 1 else N_list[0], Nt=Nt, M=M_run, K=K, a=a, out_dir=tmp,
+             out_name="bench", comm=comm, seed=args.seed, write_files=not args.no_files,
+             device=device, exchange=exchange, ld_packing=args.ld_format == "packed", **flags)
     # the warm-up steps queue no step past their last: the timers are reset
     # between the two loops while no step runs
-    v.begin(x0=x0, return_xhat=False, iterations=args.warmup, **run)
+    if args.band:   # the class seam's own set-up: the CSR, cut into coupled pieces when long
+        from sgvamp import BlockLD
+
+        v.begin(BlockLD.from_csr(band_A, s=args.ridge), band_r, x0=x0, return_xhat=False,
+                iterations=args.warmup, **run)
+        eng = v.engine
+        del band_A
+    else:
+        eng.set_ridge(args.ridge)
+        x0 = beta * np.sqrt(N_list[0])                      # main.py:276-279
+        v.attach_engine(eng, x0=x0)
+        v.begin(x0=x0, return_xhat=False, iterations=args.warmup, **run)
     eng.sync()
     comm.barrier()
     log("[bench] setup (device data generation) %.1f s, M=%d, blocks=%d x %d, N=%d, K=%d, ranks=%d"
-        % (time.perf_counter() - t_setup, eng.M, args.blocks, args.block_size, args.nsamp, K,
-           world))
+        % (time.perf_counter() - t_setup, eng.M, len(eng.block_sizes), max(eng.block_sizes),
+           args.nsamp, K, world))
 
     for it in range(args.warmup):
         rec = v.step(it)
@@ -423,7 +462,10 @@ def main():
     traffic, traffic_src = read_traffic(("k_sym_mfma" if mfma else "k_sym_pass")
                                         if args.ld_format == "packed" else "k_ld_pass",
                                         bytes_launch, K, eng.M)
-    if args.distinct_ld and K > 1:
+    if args.band:
+        cname = ("one chromosome of windowed LD (bandwidth %s, CSR -> packed band, %d coupled "
+                 "piece(s))" % (args.band.split(",")[1], len(eng.block_sizes)))
+    elif args.distinct_ld and K > 1:
         cname = "distinct per-cohort LD (the reference's ld_fpaths_list[rank] layout)"
     elif eng.M == 200000 and args.ridge == 0 and not args.lmmse_damp:
         cname = {1: "C2 (BASELINE.json configs[1])", 4: "C3 (BASELINE.json configs[2])"}.get(K, "custom")
@@ -450,17 +492,21 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: device generator following simulation/sim_gen_phen_mult.py "
-                "(Bin(2,0.4) genotypes, 50%% causal, h2=0.8), seed %d" % args.seed,
+        "data": ("synthetic: windowed LD (simulate.windowed_ld), r = R x0 + N(0,1), 5%% causal, "
+                 "seed %d" % args.seed) if args.band else
+                ("synthetic: device generator following simulation/sim_gen_phen_mult.py "
+                 "(Bin(2,0.4) genotypes, 50%% causal, h2=0.8), seed %d" % args.seed),
         "config": {
             "workload": "%s: K=%d cohort(s) %s, M=%d markers in %d LD blocks "
                         "of %d, N=%d per cohort, reference CLI default flags, output files written "
                         "each iteration, prior %s %s" % (cname, K, "with one LD matrix each"
                                                          if args.distinct_ld else "sharing one LD",
-                                                         eng.M, args.blocks,
-                                                         args.block_size, args.nsamp,
+                                                         eng.M, len(eng.block_sizes),
+                                                         max(eng.block_sizes), args.nsamp,
                                                          prior["prior_vars"], prior["prior_probs"]),
-            "K": K, "M": eng.M, "ld_blocks": args.blocks, "block_size": args.block_size,
+            "K": K, "M": eng.M, "ld_blocks": len(eng.block_sizes),
+            "block_size": args.block_size if not args.band else max(eng.block_sizes),
+            "band": args.band,
             "ld_matrices": eng.nld,
             "s": args.ridge, "lmmse_damp": bool(args.lmmse_damp),
             "N": args.nsamp, "parallelism": "LD blocks sharded over %d GPU rank(s)" % world,
@@ -508,7 +554,7 @@ def main():
         "effective_ld_gbps_end_to_end": passes * ld_bytes_total / dt / 1e9,
         "cg_iters_per_step": [r["cg_iters"] for r in recs],
     }
-    if rank == 0 and world == 1 and args.cpu_baseline == "auto":
+    if rank == 0 and world == 1 and args.cpu_baseline == "auto" and not args.band:
         log("[bench] cpu baseline ...")
         result["cpu_baseline"] = cpu_baseline(eng, args, dict(flags, **run), recs, x0)
     else:

@@ -31,6 +31,37 @@ import hip_backend as hb
 from engine import Engine
 
 
+def windowed_ld(n, bw, seed=0, taps=12):
+    """Synthetic windowed LD (PLINK --ld-window's shape, one chromosome): an
+    exactly symmetric positive semi-definite CSR matrix with unit diagonal and
+    entries only within bw of the diagonal, R = D B B^T D with B lower-banded
+    (each marker mixes `taps` earlier 'haplotype factors' at fixed offsets,
+    0 and bw among them, decaying with distance).  Built on the host with
+    scipy in O(n * taps^2); M = 1e6, bw = 1,000 takes ~15 s."""
+    import scipy.sparse
+
+    rs = np.random.RandomState(seed)
+    decay = max(bw / 3.0, 1.0)
+    offs = {0, bw}
+    if bw > 1:
+        offs |= set(rs.choice(np.arange(1, bw), min(bw - 1, taps), replace=False).tolist())
+    rows, cols, vals = [], [], []
+    for k in sorted(offs):
+        i = np.arange(k, n)
+        rows.append(i)
+        cols.append(i - k)
+        vals.append(rs.normal(size=n - k) * np.exp(-k / decay) + (1.0 if k == 0 else 0.0))
+    B = scipy.sparse.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))),
+                                shape=(n, n))
+    R = (B @ B.T).tocsr()
+    d = 1.0 / np.sqrt(R.diagonal())
+    R = scipy.sparse.diags(d) @ R @ scipy.sparse.diags(d)
+    R = ((R + R.T) * 0.5).tocsr()
+    R.sum_duplicates()
+    R.sort_indices()
+    return R
+
+
 def _write_ld(eng, ld, sizes, prefix):
     """One cohort's LD from the device: a .npy, or a manifest and one .npy per block."""
     if len(sizes) == 1:
