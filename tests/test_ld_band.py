@@ -117,3 +117,27 @@ def test_band_cut_into_coupled_pieces():
     # dense sources are never cut
     D = BlockLD(blocks=[np.eye(2)])
     assert band_cuts([D], D.block_sizes, piece=1) == [[2]]
+
+
+def test_product_windowed_ld_matches_the_oracle_generator():
+    """bench --band builds its LD with simulate.windowed_ld (product side); the
+    oracle's banded_ld is the same recipe, so band parity tests and the band
+    bench run the same matrices."""
+    from simulate import windowed_ld
+
+    for M, bw, taps in ((3000, 40, 12), (5000, 300, 4)):
+        A = windowed_ld(M, bw, seed=3, taps=taps)
+        B = vo.banded_ld(M, bw, seed=3, taps=taps)
+        assert A.nnz == B.nnz
+        assert abs(A - B).max() == 0.0
+
+
+def test_bench_band_problem_shapes():
+    import bench
+
+    class Args:
+        band, seed, nsamp = "4000,50", 2, 10_000
+
+    A, r, x0, cm = bench.band_problem(Args, 3)
+    assert A.shape == (4000, 4000) and r.shape == (3, 4000) and x0.shape == (4000,)
+    assert cm == 200 and np.count_nonzero(x0) == cm
