@@ -156,14 +156,17 @@ def main(argv=None):
             raise Exception("--bim-files is required when cohorts have different markers")
         M = M_list[0]
         i_maps = [list(range(M))] * K
-    if rank == 0:
-        logging.debug(f"Handling .bim file took {time.time() - ts} seconds \n")
+    logging.debug(f"Rank {rank}: Handling .bim file took {time.time() - ts} seconds \n")   # main.py:165
 
     # r and R (main.py:167-266)
     if rank == 0:
         logging.info("...loading R matrix and r vector\n")
     ts = time.time()
     r = np.stack([load_r(r_fpaths_list[k], M_list[k], N_list[k], i_maps[k], M) for k in range(K)])
+    # per-rank lines of main.py:193-194 (every rank holds all K cohorts' r here)
+    logging.info(f"Rank {rank} loaded r vector with shape {r.shape}\n")
+    logging.debug(f"Rank {rank}: Loading r vector took {time.time() - ts} seconds \n")
+    ts = time.time()
     by_path = {}
     lds = []
     if any(p.endswith(".ld") for p in ld_fpaths_list):
@@ -186,7 +189,9 @@ def main(argv=None):
     if rank == 0:
         logging.info(f"Loaded {len(by_path)} LD matrix/matrices, blocks {lds[0].block_sizes[:8]}"
                      f"{'...' if len(lds[0].block_sizes) > 8 else ''}\n")
-        logging.debug(f"Loading R and r took {time.time() - ts} seconds \n")
+    # main.py:262-263 (the LD is uploaded per rank: its blocks of the partition)
+    logging.info(f"Rank {rank} loaded R matrix with shape {(lds[0].M, lds[0].M)}\n")
+    logging.debug(f"Rank {rank}: Loading R matrix took {time.time() - ts} seconds \n")
 
     x0 = None
     if true_signal_fpath is not None:
