@@ -1138,7 +1138,7 @@ static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa_in) {
       HIPCHK(launch_sym_mfma(nc, pl.d_strips, pl.nstrips, pl.d_sitems, pa, c->Mpad, c->d_pk,
                              c->d_rowpart, c->d_colpart, pl.ragged, pl.pair, pl.cw, c->st));
       HIPCHK(launch_sym_finalize_strip(nc, pl.d_spanels, pl.npanels, pa, c->d_rowpart,
-                                       c->d_colpart, c->d_part, c->st));
+                                       c->d_colpart, c->d_part, pl.ragged, c->st));
       c->aux_bytes += 2.0 * 8.0 * nc * ((double)pl.nitems[pl.band256 ? 2 : cls] * SYM_H +
                                         (double)pl.nstrips * pl.cw);
       c->aux_bytes += 8.0 * (double)c->Mpad * ((nc <= 4 ? 4 : nc <= 8 ? 8 : 16) + nc);   // Pk pack

@@ -336,7 +336,8 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
                            double* colpart, bool ragged, int pair, int cw, hipStream_t st);
 hipError_t launch_sym_finalize_strip(int nc, const SymPanel* d_panels, int npanels,
                                      const PassArgs& pa, const double* rowpart,
-                                     const double* colpart, double* partials, hipStream_t st);
+                                     const double* colpart, double* partials, bool ragged,
+                                     hipStream_t st);
 hipError_t launch_sym_finalize(int nc, int cls, const SymPanel* d_panels, int npanels,
                                const PassArgs& pa, const double* rowpart, const double* colpart,
                                double* partials, hipStream_t st);

@@ -916,6 +916,78 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize_strip(
   fin_epilogue<NC>(pn, pa, y, partials, pre);
 }
 
+// The same sums with one thread per panel row holding all FIN_Q parts in
+// registers (part q: items item_begin + q, + FIN_Q, ..., then the own and other
+// strips q, q + FIN_Q, ...; parts added in order 0..3, then the coupling sum,
+// the epilogue and the panel's partial dots: wave butterfly over the same 64
+// rows, waves in order) -- every addition of k_sym_finalize_strip in the same
+// order, so bitwise the same outputs, in a 256-thread workgroup without the
+// cross-part LDS exchange (a band panel has ~3 items and 2 strips: the
+// 1024-thread form spends its time starting waves)
+template <int NC>
+__global__ __launch_bounds__(256) void k_sym_finalize_strip1(
+    const SymPanel* __restrict__ panels, PassArgs pa, const double* __restrict__ rowpart,
+    const double* __restrict__ colpart, double* __restrict__ partials) {
+  const SymPanel pn = panels[blockIdx.x];
+  if (pa.run && !ldg(pa.run)) return;
+  const int t = threadIdx.x;
+  const bool row = t < pn.H;
+  const int tr = row ? t : 0;
+  const int64_t idx = pn.voff + pn.r0 + tr;
+  double in[NC], dt[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    in[c] = pa.in[c][idx];
+    dt[c] = pa.dot[c] ? pa.dot[c][idx] : 0.0;
+  }
+  double y[FIN_Q][NC];
+#pragma unroll
+  for (int q = 0; q < FIN_Q; ++q)
+#pragma unroll
+    for (int c = 0; c < NC; ++c) y[q][c] = 0.0;
+#pragma unroll
+  for (int q = 0; q < FIN_Q; ++q) {
+#pragma unroll 2
+    for (int itm = pn.item_begin + q; itm < pn.item_end; itm += FIN_Q) {
+      const double* rp = rowpart + ((int64_t)itm * SYM_H + t) * NC;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) y[q][c] += ldg(rp + c);
+    }
+#pragma unroll 2
+    for (int sl = pn.own_sb + q; sl < pn.own_se; sl += FIN_Q) {
+      const double* cp = colpart + (int64_t)sl * NC * MF_CW + tr;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) y[q][c] += ldg(cp + c * MF_CW);
+    }
+#pragma unroll 2
+    for (int sl = pn.oth_sb + q; sl < pn.oth_se; sl += FIN_Q) {
+      const double* cp = colpart + (int64_t)sl * NC * MF_CW + SYM_H + tr;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) y[q][c] += ldg(cp + c * MF_CW);
+    }
+  }
+  __shared__ double s_w[4][NC];
+  const int lane = t & (WAVE - 1), wid = t / WAVE;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    double v = y[0][c];
+#pragma unroll
+    for (int p = 1; p < FIN_Q; ++p) v += y[p][c];
+    if (pn.cp >= 0) v += pa.cpbuf[((int64_t)pn.cp * 256 + t) * NC + c];   // coupled pieces
+    double acc = 0.0;
+    if (row) {
+      const double o = pa.c1[c] * v + pa.c2[c] * in[c];
+      pa.out[c][idx] = o;
+      if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * v + pa.ys0 * in[c];
+      if (pa.dot[c]) acc = dt[c] * o;
+    }
+    const double sm = wave_sum(acc);
+    if (lane == 0) s_w[wid][c] = sm;
+  }
+  __syncthreads();
+  if (t < NC) partials[(int64_t)pn.part * NC + t] = ((s_w[0][t] + s_w[1][t]) + s_w[2][t]) + s_w[3][t];
+}
+
 // Pk[i][c] = in[c][i] for c < ncol, 0 for ncol <= c < PKS (i over the padded
 // vector).  PKS = the columns the pass kernel's groups read: 4 (NC <= 4), 8
 // (NC <= 8), 16 -- a row is one cache line's worth of what is read, so the
@@ -996,6 +1068,16 @@ static bool band_def() {
   return v;
 }
 
+// SGV_BAND_PD (A/B, with SGV_AB=1): prefetch depth of band plans' NC <= 8
+// kernel -- 2 (default) or 4 steps in flight per wave (bitwise the same products)
+static int band_pd() {
+  static const int v = [] {
+    const char* e = ab_env("SGV_BAND_PD");
+    return (e && e[0] == '4') ? 4 : 2;
+  }();
+  return v;
+}
+
 // SGV_MF_PAIR_MAP (A/B, with SGV_AB=1): k_sym_mfma_pair's form -- 0 waves 2s,
 // 2s + 1 per segment with a barrier per row group, 1 the pair on one SIMD, 2 / 3
 // those with per-pair LDS counters instead of the barriers; default 3 (best of
@@ -1018,6 +1100,9 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
   if (cw == 256)   // band plans' 256-column strips (no item narrower than its strip)
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, false, true, 0, 256>), dim3(nstrips),
                        dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (ragged && band_pd() == 4)
+    hipLaunchKernelGGL((k_sym_mfma<NG, NW, 4, true, true, true>), dim3(nstrips), dim3(NW * 64), 0,
+                       st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else if (ragged && band_def())
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, true, true>), dim3(nstrips),
                        dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
@@ -1129,15 +1214,33 @@ extern "C" int sgv_diag_mf_trace(unsigned long long* out, int n) {
 }
 #endif
 
+// SGV_FIN_FORM (A/B, with SGV_AB=1): the strip finalize's form -- 4 = FIN_Q
+// threads per panel row (k_sym_finalize_strip), 1 = one thread per row with the
+// parts in registers (k_sym_finalize_strip1; bitwise the same outputs);
+// default: 1 for band plans at up to 8 columns (M = 1e6, bw = 1,000: 2.126-2.134
+// vs 2.156 ms per pass), 4 otherwise (dense 64 x 15,625 at 8 columns: 12.13 vs
+// 11.97-12.01 ms; 16 columns even; profiles/r04/fin_*.jsonl)
+static int fin_form(bool ragged, int nc) {
+  const char* e = ab_env("SGV_FIN_FORM");   // per launch (a getenv): tests switch it
+  const int v = (e && (e[0] == '1' || e[0] == '4')) ? e[0] - '0' : 0;
+  return v ? v : (ragged && nc <= 8) ? 1 : 4;
+}
+
 hipError_t launch_sym_finalize_strip(int nc, const SymPanel* d_panels, int npanels,
                                      const PassArgs& pa, const double* rowpart,
-                                     const double* colpart, double* partials, hipStream_t st) {
+                                     const double* colpart, double* partials, bool ragged,
+                                     hipStream_t st) {
   // the partials with the default cache policy: nontemporal loads measured
   // 0.5-3 % slower (profiles/r03/s4/fin_nt_ab.jsonl; they were just written)
+  const bool one = fin_form(ragged, nc) == 1;
 #define FIN_CASE(N)                                                                        \
   case N:                                                                                  \
-    hipLaunchKernelGGL(k_sym_finalize_strip<N>, dim3(npanels), dim3(256 * FIN_Q), 0, st, d_panels, \
-                       pa, rowpart, colpart, partials);                                    \
+    if (one)                                                                               \
+      hipLaunchKernelGGL(k_sym_finalize_strip1<N>, dim3(npanels), dim3(256), 0, st, d_panels, \
+                         pa, rowpart, colpart, partials);                                  \
+    else                                                                                   \
+      hipLaunchKernelGGL(k_sym_finalize_strip<N>, dim3(npanels), dim3(256 * FIN_Q), 0, st, \
+                         d_panels, pa, rowpart, colpart, partials);                        \
     break;
   switch (nc) {
     FIN_CASE(1) FIN_CASE(2) FIN_CASE(3) FIN_CASE(4) FIN_CASE(5) FIN_CASE(6) FIN_CASE(7) FIN_CASE(8)

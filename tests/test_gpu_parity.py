@@ -847,6 +847,34 @@ def test_ld_matvec_band_vs_scipy(parts, ncol, s, kern):
     eng.close()
 
 
+def test_finalize_forms_bitwise(monkeypatch):
+    """The strip finalize's two forms -- FIN_Q threads per panel row
+    (k_sym_finalize_strip) and one thread per row holding the FIN_Q parts in
+    registers (k_sym_finalize_strip1, the default for band plans at <= 8
+    columns) -- add the same terms in the same order: products bitwise equal
+    on a plan mixing dense and band blocks, 3..16 columns (the band VAMP tests
+    run the default form end to end)."""
+    monkeypatch.setenv("SGV_AB", "1")
+    A = _band_matrix([(3000, 300), (1500, None), (2600, 40)], seed=5)
+    L = BlockLD.from_csr(A, s=0.05)
+    out = {}
+    for form in ("1", "4"):
+        monkeypatch.setenv("SGV_FIN_FORM", form)
+        eng = Engine(L.block_sizes, K=1)
+        eng.set_ridge(0.05)
+        for b in range(len(L.block_sizes)):
+            L.upload(eng, 0, b)
+        assert {eng.ld_block_format(0, b) for b in range(len(L.block_sizes))} == {1, 2}
+        out[form] = [eng.ld_matvec(0, np.random.RandomState(nc).normal(size=(nc, A.shape[0])))
+                     for nc in (3, 5, 8, 11, 16)]
+        eng.close()
+    ref = vo.CsrLD(A, s=0.05)
+    for i, nc in enumerate((3, 5, 8, 11, 16)):
+        np.testing.assert_array_equal(out["1"][i], out["4"][i])
+        V = np.random.RandomState(nc).normal(size=(nc, A.shape[0]))
+        assert maxrel(out["1"][i][nc - 1], ref.matvec_Rs(V[nc - 1])) < 1e-12
+
+
 @pytest.mark.parametrize("ncol", [1, 2, 3, 8, 16])
 def test_ld_matvec_coupled_pieces_vs_scipy(ncol):
     """One band block cut into coupled pieces (sgvamp.band_cuts / BlockLD.pieces,
