@@ -165,6 +165,26 @@ def test_sharded_bench_equals_one_rank(name, flags, tmp_path):
         assert (tmp_path / "one" / f).read_bytes() == (tmp_path / "eight" / f).read_bytes(), f
 
 
+@pytest.mark.timeout(600)
+def test_band_bench_over_ranks_equals_one_rank(tmp_path):
+    """bench.py --band: one chromosome of windowed LD as a CSR through the class
+    seam, cut into coupled pieces (65,536 + 84,464); 2 ranks on one device (a
+    piece each, a halo all-gather per pass) write output files bitwise equal to
+    one rank's, and the line names the band workload."""
+    flags = ["--band", "150000,500", "--K", "2"]
+    one = _bench(tmp_path / "one", *flags)
+    two = _bench(tmp_path / "two", *flags, gpus=2)
+    _log("band", "one rank", one["cg_iters_per_step"], one["roofline"]["frac"])
+    assert one["config"]["band"] == "150000,500" and one["config"]["ld_blocks"] >= 2
+    assert "windowed LD" in one["config"]["workload"] and one["cpu_baseline"] is None
+    assert two["n_gpus"] == 2 and two["cg_iters_per_step"] == one["cg_iters_per_step"]
+    assert two["exchange"]["allgathers_per_step"] > 0
+    files = sorted(f for f in os.listdir(tmp_path / "one") if f.endswith((".bin", ".csv")))
+    assert len([f for f in files if f.endswith(".bin")]) == 3 * (2 + 1)
+    for f in files:
+        assert (tmp_path / "one" / f).read_bytes() == (tmp_path / "two" / f).read_bytes(), f
+
+
 def _gate_50(nblk, size, K, tmp_path, its=50):
     """50 outer iterations of the HIP path against the CPU oracle on the same
     inputs read back from the device (the bench's problem, prior and flags);
