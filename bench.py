@@ -85,6 +85,9 @@ def parse():
     p.add_argument("--prior", choices=["matched", "cli"], default="matched")
     p.add_argument("--ridge", type=float, default=0.0, help="--s of the CLI (C5: 0.1)")
     p.add_argument("--lmmse-damp", type=int, default=0, help="--lmmse-damp of the CLI (C5: 1)")
+    p.add_argument("--pause", type=float, default=0.0,
+                   help="seconds the device idles after set-up, before the warm-up steps "
+                        "(clock/thermal studies: the set-up's generator kernels heat the chip)")
     p.add_argument("--read-bw", type=int, default=1,
                    help="1: after the timed steps, measure the GPU's streaming-read rate "
                         "(roofline.box_stream_GBs)")
@@ -409,6 +412,9 @@ def main():
         % (time.perf_counter() - t_setup, eng.M, len(eng.block_sizes), max(eng.block_sizes),
            args.nsamp, K, world))
 
+    if args.pause > 0:
+        time.sleep(args.pause)
+        comm.barrier()
     for it in range(args.warmup):
         rec = v.step(it)
         log("[bench] warmup it=%d cg=%s passes=%d %.1f ms" % (it, rec["cg_iters"], rec["ld_passes"],

@@ -1097,6 +1097,15 @@ template <int NG, int NW, int PD>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
                       const int* run, int pks, bool ragged, int pair, int cw, hipStream_t st) {
+  // SGV_MF_RAG=1 (A/B, SGV_AB=1): the band plans' kernel for every plan (bitwise
+  // the same products).  It holds 2.2-2.3 GHz on band LD but 1.43-1.47 GHz on the
+  // north star's dense blocks, as the dense kernel does: the clock follows the
+  // data, not the instruction mix (profiles/r04/ragclk_*)
+  static const bool force_rag = [] {
+    const char* e = ab_env("SGV_MF_RAG");
+    return e && e[0] == '1';
+  }();
+  ragged = ragged || force_rag;
   if (cw == 256)   // band plans' 256-column strips (no item narrower than its strip)
     hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, false, true, 0, 256>), dim3(nstrips),
                        dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
