@@ -397,6 +397,13 @@ class VAMP:
                 uniq = [x[0] for x in split]
                 couplings = [x[1] for x in split]
                 sizes = [n for c in cuts for n in c]
+        nranks = self.comm.Get_size()
+        if len(sizes) < nranks:   # ranks own whole blocks / band pieces
+            raise ValueError(
+                "%d LD block(s) cannot be spread over %d ranks: run on at most %d GPU(s)%s"
+                % (len(sizes), nranks, len(sizes),
+                   ", or cut windowed LD into shorter pieces (SGV_BAND_PIECE, a multiple of "
+                   "1024, now %d)" % BAND_PIECE if self.ld_packing else ""))
         self.engine = eng = Engine(sizes, K, ld_of, comm=self.comm, device=self.device,
                                           exchange=self.exchange)
         eng.set_ld_packing(self.ld_packing)

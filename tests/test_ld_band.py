@@ -141,3 +141,25 @@ def test_bench_band_problem_shapes():
     A, r, x0, cm = bench.band_problem(Args, 3)
     assert A.shape == (4000, 4000) and r.shape == (3, 4000) and x0.shape == (4000,)
     assert cm == 200 and np.count_nonzero(x0) == cm
+
+
+def test_fewer_pieces_than_ranks_is_refused_with_a_hint(tmp_path):
+    """Ranks own whole LD blocks / band pieces: a chromosome cut into 2 pieces
+    cannot run on 3 ranks -- refused before any device work, naming the
+    piece-length switch (the cut itself never depends on the rank count)."""
+    import scipy.sparse  # noqa: F401
+    from comm import SingleComm
+    from sgvamp import VAMP
+
+    class ThreeRanks(SingleComm):
+        def Get_size(self):
+            return 3
+
+    M = 150_000
+    A = vo.banded_ld(M, 300, seed=4, taps=4)
+    L = BlockLD.from_csr(A)
+    v = VAMP(N=1000, Nt=1000, M=M, K=1, rho=0.5, gamw=1.0, gam1=1e-6, a=[1.0],
+             prior_vars=[0.0, 1e-3], prior_probs=[0.9, 0.1], out_dir=str(tmp_path),
+             out_name="x", comm=ThreeRanks(), write_files=False)
+    with pytest.raises(ValueError, match=r"2 LD block\(s\) cannot be spread over 3 ranks.*SGV_BAND_PIECE"):
+        v._setup(L, np.zeros(M), None)
