@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--M", type=int, default=200000)
     ap.add_argument("--bw", type=int, default=2000)
     ap.add_argument("--taps", type=int, default=12)
+    ap.add_argument("--fill", choices=["taps", "dense"], default="taps",
+                    help="dense: every entry within bw non-zero, genotype-LD-like values "
+                         "(N(0, 0.02^2) off the diagonal, 1 on it; a mat-vec study, not PSD)")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--ncols", default="1,2,8,16")
     ap.add_argument("--lib", default=None, help="A/B of builds: load this libsgvamp_hip.so")
@@ -40,7 +43,16 @@ def main():
     from sgvamp import BlockLD
 
     t0 = time.time()
-    A = vo.banded_ld(a.M, a.bw, seed=1, taps=a.taps)
+    if a.fill == "dense":
+        import scipy.sparse
+        rs0 = np.random.RandomState(1)
+        offs = list(range(1, a.bw + 1))
+        U = scipy.sparse.diags([rs0.normal(0.0, 0.02, a.M - k) for k in offs], offs,
+                               shape=(a.M, a.M), format="csr")
+        A = (U + U.T + scipy.sparse.identity(a.M, format="csr")).tocsr()
+        A.sort_indices()
+    else:
+        A = vo.banded_ld(a.M, a.bw, seed=1, taps=a.taps)
     L = BlockLD.from_csr(A)
     eng = Engine(L.block_sizes, K=1)
     for b in range(len(L.block_sizes)):
