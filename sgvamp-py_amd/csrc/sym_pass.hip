@@ -292,16 +292,97 @@ __global__ __launch_bounds__(256) void k_coupling(const CouplingTask* __restrict
   }
 }
 
+// The same sums with the source values staged through LDS: per chunk of CPL_CH
+// steps the workgroup loads each part's next CPL_CH source values (all NC
+// columns) once, and every row thread reads them from LDS (one broadcast per
+// column) instead of issuing NC global loads per inner index; the C loads of
+// CPL_U consecutive steps go out before their FMAs.  Every y[c] still adds its
+// terms in increasing k, parts combined in order 0..3: bitwise k_coupling.
+constexpr int CPL_CH = 32;
+constexpr int CPL_U = 8;
+template <int NC>
+__global__ __launch_bounds__(256) void k_coupling_lds(const CouplingTask* __restrict__ tasks,
+                                                      PassArgs pa, const double* __restrict__ halo,
+                                                      int64_t hstride, double* __restrict__ cpbuf) {
+  __shared__ double part[3][64][NC];
+  __shared__ double s_src[4][CPL_CH][NC];
+  const CouplingTask tk = tasks[blockIdx.x];
+  if (pa.run && !ldg(pa.run)) return;
+  const int r = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int row = 64 * blockIdx.y + r;                 // within the task
+  const bool live = row < tk.nrows;
+  const int L = (tk.inner + 3) / 4;
+  const int k0 = q * L, k1 = min(tk.inner, k0 + L);
+  const double* m = tk.m + tk.row0 + (live ? row : 0);
+  double y[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) y[c] = 0.0;
+  for (int i0 = 0; i0 < L; i0 += CPL_CH) {
+    // stage: value (part qq, step ii, column c) = src_c[qq L + i0 + ii] inside the part's range
+    for (int e = threadIdx.x; e < 4 * CPL_CH * NC; e += 256) {
+      const int c = e % NC, ii = (e / NC) % CPL_CH, qq = e / (NC * CPL_CH);
+      const int k = qq * L + i0 + ii;
+      const int kend = min(tk.inner, (qq + 1) * L);
+      double v = 0.0;
+      if (k < kend)
+        v = tk.local ? pa.in[c][tk.src + k] : halo[(tk.src * NC + c) * hstride + k];
+      s_src[qq][ii][c] = v;
+    }
+    __syncthreads();
+    const int n = min(CPL_CH, k1 - (k0 + i0));   // this part's steps in the chunk (may be <= 0)
+    if (live) {
+      int ii = 0;
+      for (; ii + CPL_U <= n; ii += CPL_U) {
+        double a[CPL_U];
+#pragma unroll
+        for (int u = 0; u < CPL_U; ++u) a[u] = m[(int64_t)(k0 + i0 + ii + u) * tk.ldm];
+#pragma unroll
+        for (int u = 0; u < CPL_U; ++u)
+#pragma unroll
+          for (int c = 0; c < NC; ++c) y[c] += a[u] * s_src[q][ii + u][c];
+      }
+      for (; ii < n; ++ii) {
+        const double a = m[(int64_t)(k0 + i0 + ii) * tk.ldm];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) y[c] += a * s_src[q][ii][c];
+      }
+    }
+    __syncthreads();
+  }
+  if (q > 0) {
+#pragma unroll
+    for (int c = 0; c < NC; ++c) part[q - 1][r][c] = y[c];
+  }
+  __syncthreads();
+  if (q == 0 && live) {
+    double* out = cpbuf + ((int64_t)tk.cp * 256 + tk.prow0 + row) * NC;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) out[c] = ((y[c] + part[0][r][c]) + part[1][r][c]) + part[2][r][c];
+  }
+}
+
+// SGV_CPL_FORM (A/B, with SGV_AB=1): 0 = k_coupling (global source loads per
+// inner index), 1 = k_coupling_lds (bitwise the same sums); default 1
+static int cpl_form() {
+  const char* e = ab_env("SGV_CPL_FORM");
+  return (e && e[0] == '0') ? 0 : 1;
+}
+
 hipError_t launch_coupling(int nc, const CouplingTask* d_tasks, int ntasks, const PassArgs& pa,
                            const double* halo, int64_t hstride, double* cpbuf, int ncp_slots,
                            hipStream_t st) {
   if (ntasks <= 0) return hipSuccess;
   const hipError_t e = hipMemsetAsync(cpbuf, 0, sizeof(double) * (size_t)ncp_slots * 256 * nc, st);
   if (e != hipSuccess) return e;
+  const bool lds = cpl_form() == 1;
 #define CPL_CASE(N)                                                                         \
   case N:                                                                                   \
-    hipLaunchKernelGGL(k_coupling<N>, dim3(ntasks, 4), dim3(256), 0, st, d_tasks, pa, halo, \
-                       hstride, cpbuf);                                                     \
+    if (lds)                                                                                \
+      hipLaunchKernelGGL(k_coupling_lds<N>, dim3(ntasks, 4), dim3(256), 0, st, d_tasks, pa, \
+                         halo, hstride, cpbuf);                                             \
+    else                                                                                    \
+      hipLaunchKernelGGL(k_coupling<N>, dim3(ntasks, 4), dim3(256), 0, st, d_tasks, pa,     \
+                         halo, hstride, cpbuf);                                             \
     break;
   switch (nc) {
     CPL_CASE(1) CPL_CASE(2) CPL_CASE(3) CPL_CASE(4) CPL_CASE(5) CPL_CASE(6) CPL_CASE(7) CPL_CASE(8)

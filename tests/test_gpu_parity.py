@@ -904,6 +904,37 @@ def test_ld_matvec_coupled_pieces_vs_scipy(ncol):
     eng.close()
 
 
+def test_coupling_forms_bitwise(monkeypatch):
+    """The corner-coupling sums of coupled band pieces with the source values
+    staged through LDS (k_coupling_lds, default) and read from global memory per
+    inner index (k_coupling, SGV_CPL_FORM=0): the same additions in the same
+    order, so the products are bitwise equal (1..16 columns, widths that leave
+    partial LDS chunks and unroll tails)."""
+    from sgvamp import band_cuts
+
+    monkeypatch.setenv("SGV_AB", "1")
+    A = vo.banded_ld(50000, 613, seed=7, taps=9)
+    L = BlockLD.from_csr(A)
+    cuts = band_cuts([L], L.block_sizes, piece=16384)
+    P, cpl = L.pieces(cuts)
+    assert len(cpl) >= 2
+    out = {}
+    for form in ("0", "1"):
+        monkeypatch.setenv("SGV_CPL_FORM", form)
+        eng = Engine(P.block_sizes, K=1)
+        for b in range(len(P.block_sizes)):
+            P.upload(eng, 0, b)
+        for gb, (nr, nc, C) in cpl.items():
+            eng.set_ld_coupling(0, gb, nr, nc, C)
+        out[form] = [eng.ld_matvec(0, np.random.RandomState(nc).normal(size=(nc, A.shape[0])))
+                     for nc in (1, 2, 5, 8, 16)]
+        eng.close()
+    for i, nc in enumerate((1, 2, 5, 8, 16)):
+        np.testing.assert_array_equal(out["1"][i], out["0"][i])
+        V = np.random.RandomState(nc).normal(size=(nc, A.shape[0]))
+        assert maxrel(out["1"][i][0], A @ V[0]) < 1e-12
+
+
 def test_band_block_roundtrip():
     """get_ld_block of a band block: the stored band, zeros outside it."""
     A = _band_matrix([(1500, 200)], seed=11)
