@@ -904,6 +904,34 @@ def test_ld_matvec_coupled_pieces_vs_scipy(ncol):
     eng.close()
 
 
+@pytest.mark.parametrize("M,bw,piece,taps", [(33333, 1200, 5120, 7), (20001, 3, 4096, 2),
+                                              (41000, 1024, 4096, 12)])
+def test_coupled_pieces_ragged_vs_scipy(M, bw, piece, taps):
+    """Coupled band pieces on awkward shapes: an odd M whose last piece is not a
+    whole number of panels and a bandwidth just under piece / 4 (1,200 x 1,200
+    corners), a 3-wide band (3 x 3 corners), and a bandwidth
+    that is an exact panel multiple -- all against scipy's CSR mat-vec at 1, 3,
+    8 and 16 columns."""
+    from sgvamp import band_cuts
+
+    A = vo.banded_ld(M, bw, seed=M % 97, taps=taps)
+    L = BlockLD.from_csr(A)
+    cuts = band_cuts([L], L.block_sizes, piece=piece)
+    assert len(cuts[0]) >= 2, cuts
+    P, cpl = L.pieces(cuts)
+    eng = Engine(P.block_sizes, K=1)
+    for b in range(len(P.block_sizes)):
+        P.upload(eng, 0, b)
+    for gb, (nr, nc, C) in cpl.items():
+        eng.set_ld_coupling(0, gb, nr, nc, C)
+    for ncol in (1, 3, 8, 16):
+        V = np.random.RandomState(ncol).normal(size=(ncol, M))
+        Y = eng.ld_matvec(0, V)
+        for j in range(ncol):
+            assert maxrel(Y[j], A @ V[j]) < 1e-12, (ncol, j)
+    eng.close()
+
+
 def test_coupling_forms_bitwise(monkeypatch):
     """The corner-coupling sums of coupled band pieces with the source values
     staged through LDS (k_coupling_lds, default) and read from global memory per
