@@ -254,6 +254,57 @@ def test_cli_banded_npz_vs_oracle(tmp_path):
         assert _maxrel(xb, np.asarray(t["xhat"][it]).ravel()) < 1e-8, it
 
 
+def test_cli_one_chromosome_band_over_two_ranks(tmp_path):
+    """One chromosome of windowed LD as one .npz (src/main.py:199-200): main.py
+    cuts the band into coupled pieces (65,536 + 84,464 markers), and `--gpus 2`
+    puts one piece on each rank (halo exchange of the corner sources, both
+    ranks on device 0 with the host exchange) -- every output .bin file and the
+    cohort / metrics CSVs bitwise the single-process run's."""
+    import subprocess
+    import sys
+
+    import scipy.sparse
+
+    import main
+    from oracle import vamp_oracle as vo
+
+    M, bw, N = 150_000, 500, 5000
+    A = vo.banded_ld(M, bw, seed=12, taps=8)
+    scipy.sparse.save_npz(tmp_path / "R.npz", A)
+    rs = np.random.RandomState(8)
+    cm = M // 40
+    beta = np.zeros(M)
+    beta[rs.choice(M, cm, replace=False)] = rs.normal(0, np.sqrt(0.5 / cm), cm)
+    np.save(tmp_path / "r.npy", A @ (beta * np.sqrt(N)) + rs.normal(size=M))
+    np.save(tmp_path / "beta.npy", beta)
+
+    def argv(out):
+        return ["--ld-files", str(tmp_path / "R.npz"), "--r-files", str(tmp_path / "r.npy"),
+                "--true-signal-file", str(tmp_path / "beta.npy"), "--out-dir", str(out),
+                "--out-name", "chr", "--N", str(N), "--M", str(M), "--K", "1",
+                "--iterations", "4", "--prior-vars", "0,%r" % (0.5 / cm),
+                "--prior-probs", "0.97,0.03", "--seed", "3"]
+
+    one = tmp_path / "one"
+    one.mkdir()
+    main.main(argv(one))
+    two = tmp_path / "two"
+    two.mkdir()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["SGV_EXCHANGE"] = "host"
+    p = subprocess.run([sys.executable, os.path.join(root, "sgvamp-py_amd", "main.py")] + argv(two)
+                       + ["--gpus", "2", "--device", "0"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-3000:])
+    files = sorted(f for f in os.listdir(one) if f.endswith((".bin", ".csv")))
+    assert len([f for f in files if f.endswith(".bin")]) == 8
+    assert files == sorted(f for f in os.listdir(two) if f.endswith((".bin", ".csv")))
+    for f in files:
+        assert (one / f).read_bytes() == (two / f).read_bytes(), f
+
+
 def test_simulate_writes_cli_inputs(tmp_path):
     """simulate.py (simulation/sim_gen_phen_mult.py on the device): per cohort its
     own genotypes, block-diagonal LD as a manifest of block files, r, y, beta and
