@@ -109,12 +109,13 @@ def test_one_rank_exchange_rehearsal_bitwise(name, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,K", [(2, 1), (3, 2)])
-def test_single_band_block_over_ranks(world, K):
+@pytest.mark.parametrize("world,K,prior", [(2, 1, "em"), (3, 2, "em"), (2, 2, "mle")])
+def test_single_band_block_over_ranks(world, K, prior):
     """One band block (one chromosome of windowed LD, M = 100,000) cut into
     coupled pieces of 16,384 markers and spread over `world` ranks (host
     exchange on one GPU): every output file bitwise identical to the one-rank
-    run (tools/band_ranks_gpu.py), for K = 1 (VALU passes) and K = 2 (MFMA)."""
+    run (tools/band_ranks_gpu.py), for K = 1 (VALU passes) and K = 2 (MFMA),
+    with the EM prior update and with the MLE one (fsolve over the sharded sums)."""
     port = _free_port()
     procs = []
     for r in range(world):
@@ -122,7 +123,7 @@ def test_single_band_block_over_ranks(world, K):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SGV_EXCHANGE="host",
                    SGV_BAND_PIECE="16384")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "band_ranks_gpu.py"),
-                                       str(K)], env=env, stdout=subprocess.PIPE,
+                                       str(K), prior], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))
     outs = []
     for p in procs:

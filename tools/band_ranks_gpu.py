@@ -35,14 +35,14 @@ def problem(K):
     return A, r, x0, len(idx)
 
 
-def run(comm, K, out):
+def run(comm, K, out, prior_update="em"):
     A, r, x0, cm = problem(K)
     L = BlockLD.from_csr(A)
     v = VAMP(N=[N] * K, Nt=N * K, M=M, K=K, rho=0.5, gamw=5.0, gam1=1e-6, a=[1.0 / K] * K,
              prior_vars=[0.0, 0.5 / cm * N / (N * K)], prior_probs=[0.95, 0.05], out_dir=out,
              out_name="band", seed=11, comm=comm, device=0)
     v.infer(L, r, ITS, x0=x0, cg_maxit=500, em_prior_maxit=100, learn_gamw=True,
-            lmmse_damp=False, prior_update="em", update_prior_from=1)
+            lmmse_damp=False, prior_update=prior_update, update_prior_from=1)
     comm.barrier()
     info = dict(pieces=len(v.engine.block_sizes), local=(v.engine.b0, v.engine.b1),
                 cg=[h["cg_iters"] for h in v.history])
@@ -52,16 +52,17 @@ def run(comm, K, out):
 
 def main():
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+    pu = sys.argv[2] if len(sys.argv) > 2 else "em"   # prior update: em / mle
     comm = world_from_env()
     rank = comm.Get_rank()
     out = comm.bcast(tempfile.mkdtemp(prefix="band_ranks_") if rank == 0 else None)
-    info = run(comm, K, out)
+    info = run(comm, K, out, pu)
     print("[band_ranks] rank %d of %d: pieces %d, local %s, cg %s" % (
         rank, comm.Get_size(), info["pieces"], info["local"], info["cg"]), flush=True)
     ok = True
     if rank == 0:
         solo = tempfile.mkdtemp(prefix="band_one_")
-        info1 = run(SingleComm(), K, solo)
+        info1 = run(SingleComm(), K, solo, pu)
         assert info1["pieces"] == info["pieces"] and info["pieces"] > comm.Get_size(), info
         files = sorted(f for f in os.listdir(solo))
         assert files == sorted(os.listdir(out)), (files, os.listdir(out))
@@ -71,8 +72,8 @@ def main():
             if a != b:
                 print("[band_ranks] MISMATCH %s" % f, flush=True)
                 ok = False
-        print("[band_ranks] K=%d %d ranks vs one rank: %d files %s" % (
-            K, comm.Get_size(), len(files), "bitwise equal -> OK" if ok else "DIFFER"), flush=True)
+        print("[band_ranks] K=%d %s %d ranks vs one rank: %d files %s" % (
+            K, pu, comm.Get_size(), len(files), "bitwise equal -> OK" if ok else "DIFFER"), flush=True)
     comm.barrier()
     sys.exit(0 if ok else 1)
 
