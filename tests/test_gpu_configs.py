@@ -30,7 +30,7 @@ import pytest
 import hip_backend as hb
 from engine import Engine
 from oracle import vamp_oracle as vo
-from sgvamp import VAMP
+from sgvamp import VAMP, BlockLD
 from tests.conftest import ROOT
 
 sys.path.insert(0, ROOT)
@@ -263,3 +263,42 @@ def test_north_star_50_iterations_vs_oracle(K, tmp_path):
     compared per iteration."""
     errs, _, _ = _gate_50(64, 15625, K, tmp_path)
     assert max(errs) < 1e-5, max(errs)
+
+
+@pytest.mark.timeout(900)
+def test_band_full_size_vs_oracle(tmp_path):
+    """The band path at full size: bench.py --band's problem (one chromosome of
+    windowed LD, M = 1e6, bw = 1,000, K = 4, cut into 15 coupled pieces) through
+    the class seam, 10 outer iterations against the oracle running scipy's CSR
+    mat-vec on the same matrix (the reference's operator for .npz LD,
+    src/main.py:199-200, src/sgvamp.py:316,332), same probes and flags: xhat within
+    1e-8 relative per iteration, CG and EM counts equal (~45 s on the box:
+    profiles/r04/band_gate_full_size.log)."""
+    its, K, N = 10, 4, NSAMP
+    A, r, x0, cm = bench.band_problem(argparse.Namespace(band="1000000,1000", seed=SEED,
+                                                         nsamp=N), K)
+    M = A.shape[0]
+    prior = dict(prior_vars=[0.0, 0.5 / cm * N / (N * K)], prior_probs=[0.95, 0.05])
+    run = dict(cg_maxit=500, em_prior_maxit=100, learn_gamw=True, lmmse_damp=False,
+               prior_update="em", update_prior_from=1)
+    v = VAMP(N=[N] * K, Nt=N * K, M=M, K=K, rho=0.5, gamw=5.0, gam1=1e-6, a=[1.0 / K] * K,
+             out_dir=str(tmp_path), out_name="band", seed=SEED, write_files=False, **prior)
+    xh = v.infer(BlockLD.from_csr(A), r, its, x0=x0, **run)
+    hist = [(h["cg_iters"], h.get("em_steps")) for h in v.history]
+    pieces = list(v.engine.block_sizes)
+    v.engine.close()
+    assert len(pieces) == 15
+    _log("band 1e6 K=4: GPU %d iterations done" % its)
+    t = vo.infer([vo.CsrLD(A)], [0] * K, [r[k] for k in range(K)], [N] * K, its, rho=0.5, gamw=5.0,
+                 gam1=1e-6, x0=x0, seed=SEED,
+                 reducer=vo.Reducer("blocked", bounds=np.concatenate([[0], np.cumsum(pieces)])),
+                 rs_recurrence=True, **prior, **run)
+    errs = [maxrel(xh[it].ravel() / np.sqrt(N * K), np.asarray(t["xhat"][it]).ravel())
+            for it in range(its)]
+    _log("band 1e6 K=4: max rel xhat err per iteration", ["%.2e" % e for e in errs])
+    cg = ([list(map(list, h[0])) for h in hist], [list(map(list, x)) for x in t["cg_iters"]])
+    _log("band 1e6 K=4: CG counts equal in %d/%d iterations" % (
+        sum(a == b for a, b in zip(*cg)), its))
+    assert max(errs) < 1e-8, errs
+    assert cg[0] == cg[1]
+    assert [h[1] for h in hist][1:] == list(t["em_steps"])

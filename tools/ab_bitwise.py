@@ -29,7 +29,7 @@ def main():
     import hip_backend
     hip_backend.load(a.lib)
     from engine import Engine
-    from oracle import vamp_oracle as vo
+    from simulate import windowed_ld
     from sgvamp import VAMP, BlockLD
     from tests.golden import Case
 
@@ -52,7 +52,7 @@ def main():
         for nc in (1, 2, 3, 5, 8, 12, 16):
             print("matvec %s nc=%d %s" % (fmt, nc, h(eng.ld_matvec(0, V[:nc]))))
         eng.close()
-    A = vo.banded_ld(6000, 700, seed=3)
+    A = windowed_ld(6000, 700, seed=3, taps=40)
     L = BlockLD.from_csr(A)
     eng = Engine(L.block_sizes, K=1)
     L.upload(eng, 0, 0)

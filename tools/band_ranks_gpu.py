@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """One chromosome of windowed LD over N ranks on ONE GPU (host exchange): a
-single band block (oracle.vamp_oracle.banded_ld) cut into coupled pieces
+single band block (simulate.windowed_ld) cut into coupled pieces
 (SGV_BAND_PIECE), the pieces spread over the ranks, VAMP run for a few
 iterations; rank 0 reruns on one rank and requires every output file to be
 bitwise identical (one block no longer means one GPU).
@@ -18,14 +18,14 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "sgvamp-py_amd"))
 
 from comm import SingleComm, world_from_env  # noqa: E402
-from oracle import vamp_oracle as vo  # noqa: E402
+from simulate import windowed_ld  # noqa: E402
 from sgvamp import VAMP, BlockLD  # noqa: E402
 
 M, BW, N, ITS = 100000, 600, 5000, 5
 
 
 def problem(K):
-    A = vo.banded_ld(M, BW, seed=7, taps=12)
+    A = windowed_ld(M, BW, seed=7, taps=12)
     rs = np.random.RandomState(3)
     beta = np.zeros(M)
     idx = rs.choice(M, M // 20, replace=False)

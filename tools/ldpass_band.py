@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """LD-pass microbenchmark for sparse / windowed LD stored as packed bands
 (sgv_set_ld_block_csr): one band of M markers and bandwidth bw built on the host
-(oracle.vamp_oracle.banded_ld, a few taps so it is cheap at any size), uploaded as
+(simulate.windowed_ld, a few taps so it is cheap at any size), uploaded as
 CSR, then kernel time per pass (HIP events) for 1..16 right-hand sides.  The
 stored bytes are the band's panels (round_up(256 + bw, 256) columns per 256-row
 panel); the "csr_equiv" rate counts the 12 B per stored nonzero (8-B value +
@@ -39,7 +39,7 @@ def main():
         import hip_backend
         hip_backend.load(a.lib, strict=False)
     from engine import Engine
-    from oracle import vamp_oracle as vo
+    from simulate import windowed_ld
     from sgvamp import BlockLD
 
     t0 = time.time()
@@ -52,7 +52,7 @@ def main():
         A = (U + U.T + scipy.sparse.identity(a.M, format="csr")).tocsr()
         A.sort_indices()
     else:
-        A = vo.banded_ld(a.M, a.bw, seed=1, taps=a.taps)
+        A = windowed_ld(a.M, a.bw, seed=1, taps=a.taps)
     L = BlockLD.from_csr(A)
     eng = Engine(L.block_sizes, K=1)
     for b in range(len(L.block_sizes)):
