@@ -1012,6 +1012,49 @@ def test_vamp_band_ld_vs_oracle(K, s, damp, tmp_path):
     v.engine.close()
 
 
+@pytest.mark.parametrize("s,damp", [(0.0, False), (0.05, True)])
+def test_vamp_distinct_band_pieces_vs_oracle(s, damp, tmp_path, monkeypatch):
+    """Two cohorts each with its own windowed LD (the reference's
+    ld_fpaths_list[rank] layout, src/main.py:173) over one chromosome of 60,000
+    markers, bandwidths 400 and 700: both bands cut at the same 16,384-marker
+    pieces, each piece with its own couplings per LD matrix -- whole VAMP
+    iterations against the oracle running scipy's CSR mat-vec on each cohort's
+    matrix: xhat <= 1e-8 relative, CG counts and EM steps exact."""
+    import sgvamp
+
+    monkeypatch.setattr(sgvamp, "BAND_PIECE", 16384)
+    M, N, K = 60000, 5000, 2
+    As = [vo.banded_ld(M, 400, seed=31, taps=10), vo.banded_ld(M, 700, seed=32, taps=10)]
+    rs = np.random.RandomState(6)
+    cm = M // 25
+    beta = np.zeros(M)
+    beta[rs.choice(M, cm, replace=False)] = rs.normal(0, np.sqrt(0.5 / cm), cm) * np.sqrt(N)
+    r = [As[k] @ beta + rs.normal(size=M) * np.sqrt(0.5) for k in range(K)]
+    Ns = [float(N)] * K
+    Nt = sum(Ns)
+    prior_vars, prior_probs = [0.0, 0.5 / cm], [0.95, 0.05]
+    Ls = [BlockLD.from_csr(A, s=s) for A in As]
+    v = VAMP(N=Ns, Nt=Nt, M=M, K=K, rho=0.5, gamw=2.0, gam1=1e-6, a=np.array(Ns) / Nt,
+             prior_vars=prior_vars, prior_probs=prior_probs, out_dir=str(tmp_path),
+             out_name="dband", seed=9, write_files=False)
+    its = 5
+    xh = v.infer(Ls, np.stack(r), its, x0=beta, lmmse_damp=damp, prior_update="em")
+    pieces = list(v.engine.block_sizes)
+    assert len(pieces) == 3 and v.engine.nld == 2
+    assert {v.engine.ld_block_format(l, b) for l in range(2) for b in range(3)} == {2}
+    v.engine.close()
+    t = vo.infer([vo.CsrLD(A, s=s) for A in As], [0, 1], r, Ns, its, rho=0.5, gamw=2.0,
+                 gam1=1e-6, prior_vars=prior_vars, prior_probs=prior_probs, x0=beta, seed=9,
+                 lmmse_damp=damp, rs_recurrence=True,
+                 reducer=vo.Reducer("blocked", bounds=np.concatenate([[0], np.cumsum(pieces)])))
+    for it in range(its):
+        ref = np.asarray(t["xhat"][it]).ravel()
+        got = xh[it].ravel() / np.sqrt(Nt)
+        assert maxrel(got, ref) < 1e-8, (it, maxrel(got, ref))
+    assert [h["cg_iters"] for h in v.history] == [[list(c) for c in x] for x in t["cg_iters"]]
+    assert [h.get("em_steps") for h in v.history][1:] == list(t["em_steps"])
+
+
 @pytest.mark.parametrize("name", ["k1_long50", "k4_long50", "c1"])
 def test_north_star_gate_vs_reference(name, tmp_path):
     """The north star's accuracy gate pinned to the reference itself: xhat
