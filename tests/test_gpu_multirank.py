@@ -109,7 +109,7 @@ def test_one_rank_exchange_rehearsal_bitwise(name, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,K,prior", [(2, 1, "em"), (3, 2, "em"), (2, 2, "mle")])
+@pytest.mark.parametrize("world,K,prior", [(2, 1, "em"), (3, 2, "em"), (4, 4, "em"), (2, 2, "mle")])
 def test_single_band_block_over_ranks(world, K, prior):
     """One band block (one chromosome of windowed LD, M = 100,000) cut into
     coupled pieces of 16,384 markers and spread over `world` ranks (host
