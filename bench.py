@@ -550,10 +550,21 @@ def main():
             "ms_per_step": max(x["ms"] for x in xs_all) / steps,
             "frac_of_step": (max(x["ms"] for x in xs_all) / steps) / (dt / steps * 1e3),
             "bytes_per_step_per_rank": xs["bytes"] / steps,
+            # the EM prior loop's exchange mode per loop, chosen by the cost model
+            # (capi.hip em_costs) from the per-all-gather latency measured at
+            # set-up (sgv_exchange_probe, the slowest rank's): the last decision
+            # with both predicted costs, and the loops run in each mode
             "em_mode": xs["em_mode"],
-            "em_rep_max_km": xs["em_rep_max_km"],
-            "em_rep_max_km_source": "env SGV_EM_REP_MAX_KM" if os.environ.get("SGV_EM_REP_MAX_KM")
-                                    else "default (tunable; not measured on xGMI)",
+            "em_loops": {"replicated": xs["em_loops_replicated"],
+                         "per_step": xs["em_loops_per_step"]},
+            "em_model": {"latency_us": xs["latency_us"], "latency_source": xs["latency_source"],
+                         "predicted_steps": xs["em_pred_steps"],
+                         "predicted_replicated_us": xs["em_pred_replicated_us"],
+                         "predicted_per_step_us": xs["em_pred_per_step_us"],
+                         "replicated_possible": xs["em_replicated_possible"]},
+            # exact CG column sets: host wall time waiting for a stop test before
+            # the passes could be enqueued (upper bound of the device bubble)
+            "host_wait_ms_per_step": max(x["host_wait_ms"] for x in xs_all) / steps,
             "K_times_M": K * eng.M,
         },
         "ld_passes_per_step": passes / steps,

@@ -376,12 +376,26 @@ int sgv_timers(sgv_ctx* ctx, double* t6, int reset);
  * out[0] = all-gathers issued, out[1] = ms spent in them (RCCL: HIP events
  * around each ncclAllGather on the ctx stream, the wait for the slowest peer
  * included; host exchange: wall time of the callback), out[2] = bytes this rank
- * contributed, out[3] = EM prior loop mode (1 replicated: r1 all-gathered once
- * per loop; 0 one exchange per EM step; -1 no communicator), out[4] = the
- * replicated-EM threshold in cohort-markers (env SGV_EM_REP_MAX_KM, read when
- * the communicator is set up; default 2^20), out[5] = 1 RCCL, 2 host exchange,
- * 0 none.  reset != 0 zeroes out[0..2]. */
-int sgv_exchange_stats(sgv_ctx* ctx, double* out6, int reset);
+ * contributed, out[3] = the last EM prior loop's mode (1 replicated: r1
+ * all-gathered once per loop; 0 one exchange per EM step; -1 no communicator or
+ * no loop yet), out[4] = the per-all-gather latency (us) the EM cost model uses,
+ * out[5] = 1 RCCL, 2 host exchange, 0 none, out[6] / out[7] = EM loops run
+ * replicated / per step, out[8] / out[9] = the last decision's predicted cost
+ * (us) of the replicated / per-step loop, out[10] = the steps it predicted,
+ * out[11] = host ms spent waiting for exact-CG stop tests before enqueuing the
+ * passes, out[12] = the latency's source (0 default 25 us, 1 env
+ * SGV_XCHG_LAT_US of rank 0, 2 sgv_exchange_probe), out[13] = 1 if the
+ * replicated loop can run (K <= 32, <= 128 blocks in all).  reset != 0 zeroes
+ * out[0..2], out[6..7] and out[11]. */
+int sgv_exchange_stats(sgv_ctx* ctx, double* out14, int reset);
+
+/* Measure the per-all-gather latency of this job's exchange (the CG's ordered
+ * reduction of 16 values: per-block sums, all-gather, ordered total; `reps`
+ * times on the ctx stream) and make the maximum over ranks the EM cost model's
+ * latency on every rank.  Collective (every rank, between steps); *us_out =
+ * the agreed latency in us (0 without a communicator).  The probe's
+ * all-gathers are not counted in sgv_exchange_stats. */
+int sgv_exchange_probe(sgv_ctx* ctx, int reps, double* us_out);
 
 /* Synchronise the ctx stream. */
 int sgv_sync(sgv_ctx* ctx);

@@ -75,8 +75,11 @@ struct LdPlan {
   int nstrips = 0;
   bool ragged = false;         // some strip item is narrower than its strip (band blocks)
   int pair = 0;                // k_sym_mfma_pair for 3-4 columns (1) / 3-8 (2) (build_strips)
-  int cw = 512;                // the MFMA strips' chunk width (256: band plans)
-  bool band256 = false;        // the strips were rebuilt from class-2 items
+  // block groups of the MFMA pass (contiguous blocks): group g's strips are
+  // d_strips[gs[g] .. gs[g+1]), its panels d_spanels[gp[g] .. gp[g+1]) -- group
+  // g's finalize runs on the side stream while group g + 1's strips run
+  int ngrp = 1;
+  std::vector<int> gs, gp;
   double stored_bytes = 0.0, dense_bytes = 0.0;
   // coupled band pieces: k_coupling tasks, panel slots of PassArgs::cpbuf, and
   // the halo this rank sends (head of its first block, tail of its last) when a
@@ -112,16 +115,8 @@ const char* sgv::ab_env(const char* name) {
   return on ? v : nullptr;
 }
 
-// chunk-width class of the packed pass for nc columns (CW = 1024 >> cls);
-// SGV_SYM_WIDE=0 selects the narrower supported class (A/B tuning)
-static int sym_class(int nc) {
-  static const int narrow = [] {
-    const char* e = ab_env("SGV_SYM_WIDE");
-    return (e && e[0] == '0') ? 1 : 0;
-  }();
-  const int base = nc <= 2 ? 0 : nc <= 4 ? 1 : nc <= 8 ? 2 : 3;
-  return std::min(3, base + (nc <= 8 ? narrow : 0));
-}
+// chunk-width class of the packed VALU pass for nc columns (CW = 1024 >> cls)
+static int sym_class(int nc) { return nc <= 2 ? 0 : nc <= 4 ? 1 : nc <= 8 ? 2 : 3; }
 // default number of right-hand sides from which packed passes run on the f64
 // matrix cores (sym_mfma.hip, class-1 items); env SGV_MFMA_MIN overrides,
 // 0 disables; per context: sgv_set_mfma_min
@@ -139,16 +134,9 @@ static int cg_pipe_default() {
   return (e && e[0] == '0') ? 0 : 1;
 }
 constexpr int CG_RING = 4;   // mirror slots of the pipelined CG
+constexpr int MAXGRP = 8;    // block groups of one MFMA pass (pass_groups)
 constexpr int NOUT_SLOTS = 3;   // pinned output slots (a writer reads one while two steps run)
 
-// SGV_EM_FUSE=0: the device EM loop keeps three launches per step at one rank (A/B)
-static bool em_fuse_default() {
-  static const bool v = [] {
-    const char* e = ab_env("SGV_EM_FUSE");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
 // SGV_CG_EXACT=0: the pipelined CG's pass of iteration it also carries the
 // columns that stop at it's own test (one iteration of look-ahead; A/B);
 // sgv_set_cg_exact sets the run's mode (the Engine: from the global LD size)
@@ -201,6 +189,11 @@ struct sgv_ctx {
   double* h_halo = nullptr;      // pinned staging of the host exchange (same layout)
   size_t h_halo_cap = 0;
   int packing = 1;               // 1: packed symmetric storage for symmetric blocks
+  // MFMA passes in block groups (LdPlan::ngrp): the finalize of each group on
+  // st_fin behind its strips' event, joined back into st at the pass end
+  hipStream_t st_fin = nullptr;
+  hipEvent_t ev_grp[MAXGRP] = {};
+  hipEvent_t ev_fin = nullptr;
   double* d_rowpart = nullptr;   // k_sym_pass row partials
   double* d_colpart = nullptr;   // k_sym_pass column partials
   size_t rowpart_cap = 0, colpart_cap = 0, part_cap = 0;
@@ -265,6 +258,8 @@ struct sgv_ctx {
   double* x0 = nullptr;
   // reductions
   double* d_part = nullptr;
+  double* d_part2 = nullptr;    // the LMMSE init's partials when they share an exchange
+  size_t part2_cap = 0;
   double* d_bsum = nullptr;
   double* d_bsum_all = nullptr;
   int* d_counts = nullptr;
@@ -308,7 +303,21 @@ struct sgv_ctx {
   // reductions -- the reference's r1 all-gather + redundant EM (sgvamp.py:228-259)
   // instead of one exchange per EM step.  Global chunk table in global block
   // order (the same sums as one rank); gathered r1 as [nranks][K][mpad_max].
-  bool em_rep = false;
+  bool em_rep = false;          // the replicated loop's buffers are set up (em_rep_setup)
+  // EM exchange cost model (em_mode_pick): the per-all-gather latency in force
+  // (us; the same on every rank: rank 0's at set-up, or the probe's maximum over
+  // ranks), its source (0 default, 1 env SGV_XCHG_LAT_US, 2 measured by
+  // sgv_exchange_probe), the steps of the last EM loop (the next one's
+  // prediction), the last decision's predicted costs and the loops per mode
+  double xlat_us = 25.0;
+  int xlat_src = 0;
+  int em_prev_steps = -1;
+  int em_last_rep = -1;
+  double em_pred_rep_us = 0.0, em_pred_ps_us = 0.0, em_pred_steps = 0.0;
+  double em_loops_rep = 0.0, em_loops_ps = 0.0;
+  // exact CG column sets: host time spent waiting for a stop test before the
+  // passes can be enqueued (the device bubble's upper bound)
+  double host_wait_ms = 0.0;
   int nchg = 0, nblkg = 0;
   int64_t mpad_max = 0;
   ChunkDesc* d_chg = nullptr;
@@ -458,14 +467,9 @@ static int allgather_timed(sgv_ctx* c, const double* d_send, double* d_recv, siz
   return SGV_OK;
 }
 
-// partials [nparts][nv] -> d_dst[map.d[v]] (global, ordered); stays on device
-static int reduce_dev(sgv_ctx* c, int nv, const int* d_begin, const Map16& map, double* d_dst,
-                      int op = 0) {
-  if (!c->comm && !c->host_ag) {   // one rank: fused, bitwise the same as the two steps
-    HIPCHK(launch_reduce_local(c->d_part, nv, d_begin, c->nblk, map, d_dst, c->st, op));
-    return SGV_OK;
-  }
-  HIPCHK(launch_reduce_blocks(c->d_part, nv, d_begin, c->nblk, c->d_bsum, c->st, op));
+// the exchange half of an ordered reduction: d_bsum [nblk][nv] (this rank's
+// per-block sums) -> all ranks' -> d_dst[map.d[v]] in global block order
+static int reduce_exchange(sgv_ctx* c, int nv, const Map16& map, double* d_dst, int op) {
   const double* src = c->d_bsum;
   int nr = 1, nbm = c->nblk;
   if (c->comm) {
@@ -486,6 +490,35 @@ static int reduce_dev(sgv_ctx* c, int nv, const int* d_begin, const Map16& map, 
   }
   HIPCHK(launch_reduce_total(src, nr, nbm, nv, c->d_counts, map, d_dst, c->st, op));
   return SGV_OK;
+}
+
+// partials [nparts][nv] -> d_dst[map.d[v]] (global, ordered); stays on device
+static int reduce_dev(sgv_ctx* c, int nv, const int* d_begin, const Map16& map, double* d_dst,
+                      int op = 0) {
+  if (!c->comm && !c->host_ag) {   // one rank: fused, bitwise the same as the two steps
+    HIPCHK(launch_reduce_local(c->d_part, nv, d_begin, c->nblk, map, d_dst, c->st, op));
+    return SGV_OK;
+  }
+  HIPCHK(launch_reduce_blocks(c->d_part, nv, d_begin, c->nblk, c->d_bsum, c->st, op));
+  return reduce_exchange(c, nv, map, d_dst, op);
+}
+
+// Two ordered sums in ONE exchange (with a communicator): source A (partials
+// partA [part][nvA] over beginA -> d_dst[0 .. nvA)) and the pass partials
+// (c->d_part [part][nvB] over beginB -> d_dst[offB + mapB.d[v]]).  Each value
+// is the same per-block sums in the same global block order as its own
+// reduce_dev: bitwise the two separate reductions.
+static int reduce_dev2(sgv_ctx* c, const double* partA, int nvA, const int* beginA, int nvB,
+                       const int* beginB, const Map16& mapB, int offB, double* d_dst) {
+  const int nv = nvA + nvB;
+  if (nv > MAXNV || (!c->comm && !c->host_ag))
+    return fail(c, SGV_ERR_STATE, "reduce_dev2: %d values, or no communicator", nv);
+  HIPCHK(launch_reduce_blocks(partA, nvA, beginA, c->nblk, c->d_bsum, c->st, 0, nv, 0));
+  HIPCHK(launch_reduce_blocks(c->d_part, nvB, beginB, c->nblk, c->d_bsum, c->st, 0, nv, nvA));
+  Map16 m;
+  for (int v = 0; v < nvA; ++v) m.d[v] = v;
+  for (int v = 0; v < nvB; ++v) m.d[nvA + v] = offB + mapB.d[v];
+  return reduce_exchange(c, nv, m, d_dst, 0);
 }
 
 // the ordered total is stored by the reduction kernel straight into h_tot
@@ -707,18 +740,6 @@ static int grow(sgv_ctx* c, double** buf, size_t* cap, size_t need) {
   return SGV_OK;
 }
 
-// VALU-pass items dispatched largest first (env SGV_SYM_LPT=0: panel/chunk order)
-static bool sym_lpt() {
-  const char* e = ab_env("SGV_SYM_LPT");
-  return !(e && e[0] == '0');
-}
-
-// MFMA-pass finalize panels dispatched most work first (bitwise the same; NC = 16
-// -0.8 % per pass, profiles/r03/fin_lpt_ab.jsonl); env SGV_FIN_LPT=0: panel order
-static bool fin_lpt() {
-  const char* e = ab_env("SGV_FIN_LPT");
-  return !(e && e[0] == '0');
-}
 
 // panels per MFMA strip (env SGV_MFMA_STRIP, read when a plan is built; 1 =
 // one (panel, chunk) item per workgroup)
@@ -728,14 +749,26 @@ static int mfma_strip_len() {
   return std::max(1, std::min(64, v));
 }
 
-// SGV_BAND_CW=256 (A/B, with SGV_AB=1): band plans' MFMA strips over 256-column
-// chunks (no item narrower than its strip) instead of 512-column ones whose
-// first item is half empty.  Not faster (M = 1e6, bw = 1,000: 2.25 vs 2.17 ms at 8
-// columns, even at 4 and 16; 200k / 2,000: -2 % at 8 -- the doubled row partials
-// eat what the idle waves gave back; profiles/r04/b256_ab.jsonl): default 512
-static bool band_cw256() {
-  const char* e = ab_env("SGV_BAND_CW");
-  return e && e[0] == '2';
+// Block groups of the MFMA pass (SGV_PASS_GROUPS with SGV_AB=1 forces a count):
+// by default one group per ~4 rounds of strips on the device's workgroup slots,
+// at most 4 -- a group's finalize then overlaps the next group's strips on a
+// second stream.  The grouping changes no sum (strips and panels are the same
+// work items in another launch), so products are bitwise the same for every
+// count; it is a function of this rank's plan only.
+static int pass_groups(int nstrips, int nblk, int slots) {
+  const char* e = ab_env("SGV_PASS_GROUPS");
+  int g = e ? std::atoi(e) : nstrips / std::max(1, 4 * slots);
+  return std::max(1, std::min(std::min(g, 8), nblk));
+}
+
+static int device_cus() {
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+      ncu = prop.multiProcessorCount;
+  }
+  return ncu;
 }
 
 // Longest-processing-time makespan of `cost` on `slots` identical slots, as a
@@ -758,20 +791,14 @@ static double lpt_efficiency(std::vector<double> cost, int slots) {
 // slots) or the wave-pair kernel (one 8-wave workgroup per CU, a strip in half
 // the time: 256 slots at half the cost) -- bitwise the same products, so the
 // choice is free per plan.  Auto (1): the pair kernel for 3-4-column passes
-// when its launch drains with at least SGV_MF_PAIR_GAIN (default 3 %) less tail
-// by the strips' model cost (a few strips per slot: an 8-block share of the
-// north star); SGV_MF_PAIR=0 / 1 (with SGV_AB=1) forces none / every 3-8-column
-// pass (2).
+// when its launch drains with at least 3 % less tail by the strips' model cost
+// (a few strips per slot: an 8-block share of the north star); SGV_MF_PAIR=0 / 1
+// (with SGV_AB=1) forces none / every 3-8-column pass (2).
 static int mfma_pair_choice(const std::vector<SymStrip>& strips,
                             const std::vector<SymItem>& sitems) {
   const char* e = ab_env("SGV_MF_PAIR");
   if (e && (e[0] == '0' || e[0] == '1')) return e[0] == '1' ? 2 : 0;
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) == hipSuccess) {
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
-      ncu = prop.multiProcessorCount;
-  }
+  const int ncu = device_cus();
   std::vector<double> cost;
   cost.reserve(strips.size());
   for (const SymStrip& st : strips) {
@@ -781,9 +808,7 @@ static int mfma_pair_choice(const std::vector<SymStrip>& strips,
   }
   const double quad = lpt_efficiency(cost, 2 * ncu);
   const double pair = lpt_efficiency(cost, ncu);   // per slot: twice the speed, same ratio
-  const char* g = std::getenv("SGV_MF_PAIR_GAIN");
-  const double gain = g && *g ? std::atof(g) : 0.03;
-  return pair >= quad + gain ? 1 : 0;
+  return pair >= quad + 0.03 ? 1 : 0;
 }
 
 // MFMA strips of one LD matrix from the class-1 (512-column) tables.  Chunk
@@ -791,22 +816,24 @@ static int mfma_pair_choice(const std::vector<SymStrip>& strips,
 // g = p, p + 2, ..., G = c0 / 256 (the diagonal panel); they are cut into strips
 // of up to S panels in increasing order, colpart slots numbered per chunk.
 // The chunk's strips hold the column sums of panel G's rows (offset 0, "own")
-// and of panel G + 1's rows (offset 256, "other").  Dispatch order: most panels
-// first (the short strips fill the tail).
+// and of panel G + 1's rows (offset 256, "other").  Dispatch order: by block
+// group (pass_groups), then most panels first (the short strips fill the tail).
 static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
-                        const std::vector<SymPanel>& panels, LdPlan* pl, int cw = 512) {
+                        const std::vector<SymPanel>& panels, LdPlan* pl) {
+  constexpr int cw = 512;
   const int S = mfma_strip_len();
-  // chunk alignment classes: 512-column chunks start at 256 p + 512 k (panels of
-  // parity p share them), 256-column chunks at every 256 k (every panel)
-  const int NPAR = cw / SYM_H;
+  constexpr int NPAR = cw / SYM_H;   // 512-column chunks start at 256 p + 512 k
   std::vector<SymItem> sitems;
   std::vector<SymStrip> strips;
+  std::vector<int> sblk;             // block of each strip (creation order)
   std::vector<SymPanel> sp = panels;
+  std::vector<int> pblk(panels.size(), 0);
   int bp0 = 0;
   for (int b = 0; b < c->nblk; ++b) {
     if (c->ldb[ld][b].fmt != 1) continue;
     const int64_t n = c->bn[b];
     const int np = (int)c->ldb[ld][b].poff.size();
+    for (int g = 0; g < np; ++g) pblk[bp0 + g] = b;
     for (int p = 0; p < NPAR; ++p)
       for (int64_t c0 = (int64_t)SYM_H * p; c0 < n; c0 += cw) {
         const int G = (int)(c0 / SYM_H);
@@ -832,6 +859,7 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
             ++st.npan;
           }
           strips.push_back(st);
+          sblk.push_back(b);
         }
         sp[bp0 + G].own_sb = sb;
         sp[bp0 + G].own_se = (int)strips.size();
@@ -842,28 +870,68 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
       }
     bp0 += np;
   }
-  // most panels first, creation order within a count.  Measured slower
-  // (profiles/r03/s4/): ordering by stored bytes (2-10 %) and XCD-contiguous
-  // eighths of the creation order, each most panels first (north star +5 %,
-  // 8 x 25,000 +4-7 %, the 8-block share -1 %)
-  std::stable_sort(strips.begin(), strips.end(),
-                   [](const SymStrip& a, const SymStrip& b) { return a.npan > b.npan; });
-  // finalize dispatch order (a panel's sums do not depend on it): most row and
-  // column parts first, so the one-item panels at the blocks' ends fill the tail
-  if (fin_lpt())
-    std::stable_sort(sp.begin(), sp.end(), [](const SymPanel& a, const SymPanel& b) {
-      const int wa = (a.item_end - a.item_begin) + (a.own_se - a.own_sb) + (a.oth_se - a.oth_sb);
-      const int wb = (b.item_end - b.item_begin) + (b.own_se - b.own_sb) + (b.oth_se - b.oth_sb);
-      return wa > wb;
+  // block groups: contiguous blocks, balanced by stored bytes
+  const int ncu = device_cus();
+  std::vector<int> grp(c->nblk, 0);
+  int ngrp = pass_groups((int)strips.size(), c->nblk, 2 * ncu);
+  {
+    double tot = 0.0;
+    for (int b = 0; b < c->nblk; ++b) tot += c->ldb[ld][b].stored_bytes;
+    double acc = 0.0;
+    for (int b = 0; b < c->nblk; ++b) {
+      grp[b] = std::min(ngrp - 1, (int)(acc / tot * ngrp));
+      acc += c->ldb[ld][b].stored_bytes;
+    }
+    ngrp = grp[c->nblk - 1] + 1;
+  }
+  // group, then most panels first, creation order within a count.  Measured
+  // slower (profiles/r03/s4/): ordering by stored bytes (2-10 %) and
+  // XCD-contiguous eighths of the creation order (north star +5 %, 8 x 25,000
+  // +4-7 %, the 8-block share -1 %)
+  {
+    std::vector<int> ord(strips.size());
+    for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) {
+      if (grp[sblk[x]] != grp[sblk[y]]) return grp[sblk[x]] < grp[sblk[y]];
+      return strips[x].npan > strips[y].npan;
     });
+    std::vector<SymStrip> o(strips.size());
+    pl->gs.assign(ngrp + 1, 0);
+    for (size_t i = 0; i < ord.size(); ++i) {
+      o[i] = strips[ord[i]];
+      pl->gs[grp[sblk[ord[i]]] + 1] = (int)i + 1;
+    }
+    for (int g = 1; g <= ngrp; ++g) pl->gs[g] = std::max(pl->gs[g], pl->gs[g - 1]);
+    strips.swap(o);
+  }
+  // finalize dispatch order (a panel's sums do not depend on it): by group, then
+  // most row and column parts first, so the one-item panels at the blocks' ends
+  // fill the tail (NC = 16 -0.8 % per pass, profiles/r03/fin_lpt_ab.jsonl)
+  {
+    std::vector<int> ord(sp.size());
+    for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
+    auto work = [&](const SymPanel& a) {
+      return (a.item_end - a.item_begin) + (a.own_se - a.own_sb) + (a.oth_se - a.oth_sb);
+    };
+    std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) {
+      if (grp[pblk[x]] != grp[pblk[y]]) return grp[pblk[x]] < grp[pblk[y]];
+      return work(sp[x]) > work(sp[y]);
+    });
+    std::vector<SymPanel> o(sp.size());
+    pl->gp.assign(ngrp + 1, 0);
+    for (size_t i = 0; i < ord.size(); ++i) {
+      o[i] = sp[ord[i]];
+      pl->gp[grp[pblk[ord[i]]] + 1] = (int)i + 1;
+    }
+    for (int g = 1; g <= ngrp; ++g) pl->gp[g] = std::max(pl->gp[g], pl->gp[g - 1]);
+    sp.swap(o);
+  }
+  pl->ngrp = ngrp;
   pl->nstrips = (int)strips.size();
-  pl->cw = cw;
   pl->ragged = false;
   for (const SymStrip& st : strips)
     for (int i = 0; i < st.npan; ++i) pl->ragged |= sitems[st.it0 + i].nc < st.ncmax;
-  if (cw != 512 && pl->ragged)
-    return fail(c, SGV_ERR_STATE, "strip plan: a %d-column strip with a narrower item", cw);
-  pl->pair = (pl->ragged || cw != 512) ? 0 : mfma_pair_choice(strips, sitems);
+  pl->pair = pl->ragged ? 0 : mfma_pair_choice(strips, sitems);
   CHK(upload_table(c, strips, &pl->d_strips));
   CHK(upload_table(c, sitems, &pl->d_sitems));
   CHK(upload_table(c, sp, &pl->d_spanels));
@@ -1050,32 +1118,19 @@ static int ensure_plan(sgv_ctx* c, int ld) {
       // dispatch order: largest items first (rows x columns), so the small edge
       // items fill the tail of the launch; the `item` field keeps the partial slot
       std::vector<SymItem> order = items;
-      if (sym_lpt())
-        std::stable_sort(order.begin(), order.end(), [](const SymItem& a, const SymItem& b) {
-          return (int64_t)a.H * a.nc > (int64_t)b.H * b.nc;
-        });
+      std::stable_sort(order.begin(), order.end(), [](const SymItem& a, const SymItem& b) {
+        return (int64_t)a.H * a.nc > (int64_t)b.H * b.nc;
+      });
       CHK(upload_table(c, order, &pl.d_items[cls]));
     }
     CHK(upload_table(c, panels, &pl.d_panels[cls]));
-    if (cls == 1) {
-      CHK(build_strips(c, ld, items, panels, &pl));
-      if (pl.ragged && band_cw256()) {   // band plan: 256-column strips (class 2)
-        if (pl.d_strips) HIPCHK(hipFree(pl.d_strips));
-        if (pl.d_sitems) HIPCHK(hipFree(pl.d_sitems));
-        if (pl.d_spanels) HIPCHK(hipFree(pl.d_spanels));
-        pl.d_strips = nullptr;
-        pl.d_sitems = nullptr;
-        pl.d_spanels = nullptr;
-        pl.band256 = true;
-      }
-    }
-    if (cls == 2 && pl.band256) CHK(build_strips(c, ld, items, panels, &pl, 256));
+    if (cls == 1) CHK(build_strips(c, ld, items, panels, &pl));
     const size_t ncmax = (size_t)sym_class_nc(cls);
     rowpart_need = std::max(rowpart_need, items.size() * SYM_H * ncmax);
     colpart_need = std::max(colpart_need, items.size() * ncmax * (size_t)cw);
   }
-  if (pl.npanels) {   // the MFMA pass: class-1 (band: class-2) items with up to 16 columns
-    rowpart_need = std::max(rowpart_need, (size_t)pl.nitems[pl.band256 ? 2 : 1] * SYM_H * MAXC);
+  if (pl.npanels) {   // the MFMA pass: class-1 items with up to 16 columns
+    rowpart_need = std::max(rowpart_need, (size_t)pl.nitems[1] * SYM_H * MAXC);
     colpart_need = std::max(colpart_need, (size_t)pl.nstrips * MAXC * 512);
     CHK(grow(c, &c->d_pk, &c->pk_cap, (size_t)c->Mpad * 16));
   }
@@ -1135,12 +1190,32 @@ static int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa_in) {
     const bool mf = c->mfma_min > 0 && nc >= c->mfma_min;
     const int cls = mf ? 1 : sym_class(nc);
     if (mf) {
-      HIPCHK(launch_sym_mfma(nc, pl.d_strips, pl.nstrips, pl.d_sitems, pa, c->Mpad, c->d_pk,
-                             c->d_rowpart, c->d_colpart, pl.ragged, pl.pair, pl.cw, c->st));
-      HIPCHK(launch_sym_finalize_strip(nc, pl.d_spanels, pl.npanels, pa, c->d_rowpart,
-                                       c->d_colpart, c->d_part, pl.ragged, c->st));
-      c->aux_bytes += 2.0 * 8.0 * nc * ((double)pl.nitems[pl.band256 ? 2 : cls] * SYM_H +
-                                        (double)pl.nstrips * pl.cw);
+      HIPCHK(launch_pk(pa, nc, c->Mpad, c->d_pk, c->st));
+      if (pl.ngrp <= 1) {
+        HIPCHK(launch_sym_mfma(nc, pl.d_strips, pl.nstrips, pl.d_sitems, pa, c->d_pk,
+                               c->d_rowpart, c->d_colpart, pl.ragged, pl.pair, c->st));
+        HIPCHK(launch_sym_finalize_strip(nc, pl.d_spanels, pl.npanels, pa, c->d_rowpart,
+                                         c->d_colpart, c->d_part, pl.ragged, c->st));
+      } else {
+        // group g's strips on the ctx stream, its finalize on the side stream
+        // behind them: the finalize (and the launch tail) of g overlaps g + 1's
+        // strips.  Same work items, so the products are bitwise the one-launch
+        // pass's; the pass's events (e0 on st, e1 after the join) span both
+        for (int g = 0; g < pl.ngrp; ++g) {
+          HIPCHK(launch_sym_mfma(nc, pl.d_strips + pl.gs[g], pl.gs[g + 1] - pl.gs[g],
+                                 pl.d_sitems, pa, c->d_pk, c->d_rowpart, c->d_colpart, pl.ragged,
+                                 pl.pair, c->st));
+          HIPCHK(hipEventRecord(c->ev_grp[g % MAXGRP], c->st));
+          HIPCHK(hipStreamWaitEvent(c->st_fin, c->ev_grp[g % MAXGRP], 0));
+          HIPCHK(launch_sym_finalize_strip(nc, pl.d_spanels + pl.gp[g], pl.gp[g + 1] - pl.gp[g],
+                                           pa, c->d_rowpart, c->d_colpart, c->d_part, pl.ragged,
+                                           c->st_fin));
+        }
+        HIPCHK(hipEventRecord(c->ev_fin, c->st_fin));
+        HIPCHK(hipStreamWaitEvent(c->st, c->ev_fin, 0));
+      }
+      c->aux_bytes += 2.0 * 8.0 * nc * ((double)pl.nitems[cls] * SYM_H +
+                                        (double)pl.nstrips * 512);
       c->aux_bytes += 8.0 * (double)c->Mpad * ((nc <= 4 ? 4 : nc <= 8 ? 8 : 16) + nc);   // Pk pack
     } else {
       HIPCHK(launch_sym_pass(nc, cls, pl.d_items[cls], pl.nitems[cls], pa, c->d_rowpart,
@@ -1298,8 +1373,22 @@ static int event_spin(sgv_ctx* c, hipEvent_t ev) {
 // the same iterates bit for bit there).  Where the smaller set crosses a kernel
 // boundary (NC <= 2 runs the VALU pass, 3..16 the MFMA pass) the surviving
 // columns' sums are formed in another order: equal to rounding.
+// With a communicator the CG prologue's sums (|b|^2, |r0|^2: the LMMSE init
+// kernel's partials, `m0`) ride in the exchange of iteration 0's p.q instead of
+// one of their own: the first pass runs on p0 = r0 for every column before the
+// stop test of iteration 0 is known (as the look-ahead pass does), then
+// k_cg_init and the test follow the shared reduction.  Same values, one
+// exchange fewer per LMMSE; only where one LD matrix serves every column.
+struct CgMerge0 {
+  const double* part = nullptr;   // [chunk][2 MAXC] (k_lmmse_init)
+  double rtol = 0.0;
+  double* const* X = nullptr;     // k_cg_init zeroes X, R_s X of |b| == 0 columns
+  double* const* RX = nullptr;
+};
+
 static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const double* atol,
-                       int maxiter, const int* active_in, int* iters, int* info, int* passes) {
+                       int maxiter, const int* active_in, int* iters, int* info, int* passes,
+                       const CgMerge0* m0 = nullptr) {
   const int ncol = cc.ncol;
   unsigned mask = 0;
   if (rho0) {
@@ -1323,7 +1412,7 @@ static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const d
   // one rank: iteration it's r.r reduction and the control of it + 1 are one
   // launch (k_cg_reduce_ctl), enqueued at the end of it, when that one
   // workgroup's reduction is short (fused_ctl_pays); SGV_EM_FUSE=0 A/B
-  const bool fuse = !c->comm && !c->host_ag && fused_ctl_pays(MAXC, c->nblk) && em_fuse_default();
+  const bool fuse = !c->comm && !c->host_ag && fused_ctl_pays(MAXC, c->nblk);
   // exact sets pay only where fewer columns make a pass cheaper: the MFMA pass
   // (>= 3 columns of one LD matrix, cost by groups of 4); the VALU pass costs
   // the same at 1 and 2 columns (C2: 3.19 vs 3.21 ms), so K = 1 and distinct-LD
@@ -1348,7 +1437,8 @@ static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const d
                             c->aux_bytes};
     int npass = 0;
     CgState* slot = c->h_cgm + (it % CG_RING);
-    if (it == 0 || !fuse) {
+    const bool merge = m0 && it == 0;   // the prologue's sums ride with this p.q
+    if ((it == 0 || !fuse) && !merge) {
       HIPCHK(launch_cg_ctl(c->d_cgs, slot, c->d_rhonew, it, ncol, -1, c->st));
       HIPCHK(hipEventRecord(c->ev_cg[it % CG_RING], c->st));
     }
@@ -1365,7 +1455,10 @@ static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const d
     }
     const bool pre = exact && it > 0;   // the test of `it` read before its passes
     if (pre) {
+      const auto tw = std::chrono::steady_clock::now();
       CHK(event_spin(c, c->ev_cg[it % CG_RING]));
+      c->host_wait_ms +=
+          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw).count();
       last = slot;
       if (!last->any) break;            // only the (no-op) p update was enqueued
       mask = 0;
@@ -1391,16 +1484,25 @@ static int cg_loop_dev(sgv_ctx* c, const CgCols& cc, const double* rho0, const d
       if (!nc) continue;
       pa.ys1 = 1.0 - cc.s;   // Y = R_s p = (1-s) R p + s p
       pa.ys0 = cc.s;
-      pa.run = &c->d_cgs->any;
+      pa.run = merge ? nullptr : &c->d_cgs->any;   // merge: the state is set after it
       CHK(ld_pass(c, ld, nc, pa));
-      CHK(reduce_dev(c, nc, ld_parts(c, ld), map, c->d_pq));
+      if (merge) {   // [|b|^2, |r0|^2] -> d_tot[0 .. 2 MAXC), p.q -> d_tot[2 MAXC + j]
+        CHK(reduce_dev2(c, m0->part, 2 * MAXC, c->d_ch_begin, nc, ld_parts(c, ld), map, 2 * MAXC,
+                        c->d_tot));
+        HIPCHK(launch_cg_init(c->d_cgs, c->d_tot, m0->rtol, ncol, c->d_ch, c->nch, m0->X, m0->RX,
+                              c->st));
+        HIPCHK(launch_cg_ctl(c->d_cgs, slot, c->d_rhonew, it, ncol, -1, c->st));
+        HIPCHK(hipEventRecord(c->ev_cg[it % CG_RING], c->st));
+      } else {
+        CHK(reduce_dev(c, nc, ld_parts(c, ld), map, c->d_pq));
+      }
       ++npass;
     }
     // alpha = rho / p.q; x += alpha p; r -= alpha q; r.r (:412-415)
     XrArgs xa{};
     xa.ncol = ncol;
     xa.mask = mask;
-    xa.pq = c->d_pq;
+    xa.pq = merge ? c->d_tot + 2 * MAXC : c->d_pq;
     xa.st = c->d_cgs;
     for (int j = 0; j < ncol; ++j) {
       xa.X[j] = cc.X[j];
@@ -1514,6 +1616,13 @@ extern "C" int sgv_create(int device, int K, int nld, const int* ld_of, int nblk
     return cleanup(fail(nullptr, SGV_ERR_HIP, "hipStreamCreate"));
   if (hipStreamCreateWithFlags(&c->st_copy, hipStreamNonBlocking) != hipSuccess)
     return cleanup(fail(nullptr, SGV_ERR_HIP, "hipStreamCreate"));
+  if (hipStreamCreateWithFlags(&c->st_fin, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(nullptr, SGV_ERR_HIP, "hipStreamCreate"));
+  for (int g = 0; g < MAXGRP; ++g)
+    if (hipEventCreateWithFlags(&c->ev_grp[g], hipEventDisableTiming) != hipSuccess)
+      return cleanup(fail(nullptr, SGV_ERR_HIP, "hipEventCreate"));
+  if (hipEventCreateWithFlags(&c->ev_fin, hipEventDisableTiming) != hipSuccess)
+    return cleanup(fail(nullptr, SGV_ERR_HIP, "hipEventCreate"));
 
   // marker layout
   int64_t off = 0, voff = 0;
@@ -1655,6 +1764,7 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   }
   (void)hipSetDevice(c->dev);
   if (c->st) (void)hipStreamSynchronize(c->st);
+  if (c->st_fin) (void)hipStreamSynchronize(c->st_fin);
   if (c->comm) (void)ncclCommDestroy(c->comm);
   if (c->h_bsum) (void)hipHostFree(c->h_bsum);
   if (c->h_bsum_all) (void)hipHostFree(c->h_bsum_all);
@@ -1687,6 +1797,7 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   (void)hipFree(c->d_ch_begin);
   (void)hipFree(c->pool);
   (void)hipFree(c->d_part);
+  if (c->d_part2) (void)hipFree(c->d_part2);
   (void)hipFree(c->d_bsum);
   if (c->d_bsum_all) (void)hipFree(c->d_bsum_all);
   (void)hipFree(c->d_counts);
@@ -1733,6 +1844,11 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
     if (c->ev_out[i]) (void)hipEventDestroy(c->ev_out[i]);
     if (c->ev_pack[i]) (void)hipEventDestroy(c->ev_pack[i]);
   }
+  if (c->st_fin) (void)hipStreamSynchronize(c->st_fin);
+  for (hipEvent_t e : c->ev_grp)
+    if (e) (void)hipEventDestroy(e);
+  if (c->ev_fin) (void)hipEventDestroy(c->ev_fin);
+  if (c->st_fin) (void)hipStreamDestroy(c->st_fin);
   if (c->st_copy) (void)hipStreamDestroy(c->st_copy);
   if (c->st) (void)hipStreamDestroy(c->st);
   delete c;
@@ -1799,47 +1915,61 @@ static int gather_f64(sgv_ctx* c, const double* d_send, double* d_recv, size_t c
 
 // With a communicator the EM prior loop either runs REPLICATED (every rank's r1
 // all-gathered once per loop, then the one-rank loop over all M markers on every
-// rank) or with ONE EXCHANGE PER EM STEP (each rank sums its own markers; the
-// per-block partials are all-gathered every step, stream-ordered, the loop
-// still device-driven).  Per outer iteration with E EM steps:
-//   replicated: gather 8 K M bytes + E x (k_em over K M + one-workgroup reduce)
-//   per step:   E x (k_em over K M / N + all-gather latency + ordered total)
-// k_em is f64-VALU bound (exp, divisions: ~44 us at K M = 4e6 on one MI355X,
-// plus ~35 us of reduction/control) while one small all-gather costs ~10-30 us
-// over xGMI, so the replicated loop pays only below about a million
-// cohort-markers (C2: K M = 2e5 -> replicated; north star: 4e6 -> per step).
-// SGV_EM_REP=0/1 (with SGV_AB=1) forces either.
-// The threshold is a tunable, not a measurement of this machine's xGMI:
-// SGV_EM_REP_MAX_KM overrides the default (read when the communicator is set
-// up), and sgv_exchange_stats reports the value in force and the mode chosen.
-constexpr double EM_REP_MAX_KM_DEFAULT = 1048576.0;
-static double em_rep_max_km() {
-  const char* e = std::getenv("SGV_EM_REP_MAX_KM");
-  if (e && *e) {
-    char* end = nullptr;
-    const double v = std::strtod(e, &end);
-    if (end != e && v >= 0.0) return v;
-  }
-  return EM_REP_MAX_KM_DEFAULT;
+// rank -- the reference's own structure, src/sgvamp.py:228-259) or with ONE
+// EXCHANGE PER EM STEP (each rank sums its own markers; the per-block partials
+// are all-gathered every step, stream-ordered, the loop still device-driven).
+// Both give the same bits (ordered per-block sums in global block order), so
+// the mode is chosen per EM loop by a cost model whose one machine parameter is
+// the per-all-gather latency L (the same value on every rank, so every rank
+// picks the same mode):
+//   replicated: L + 8 K M (N-1)/N / B + S x (k_em(K M) + T_rep)
+//   per step:   S x (k_em(K M / N) + T_ps + L)
+// S = the steps the loop enqueues (the predicted EM steps + the one queued
+// past the last), predicted as the previous loop's (the first loop: maxit);
+// k_em(n) = 5 us + 11 ps per cohort-marker (f64-VALU bound: 44 us at 4e6 on one
+// MI355X), T_rep = 35 us (the one-workgroup reduction + control over every
+// block), T_ps = 15 us (per-block sums, ordered total, control: 3 launches),
+// B = 100 GB/s (an xGMI all-gather of MBs).  L: 25 us by default, env
+// SGV_XCHG_LAT_US (rank 0's value), or measured (sgv_exchange_probe).
+// SGV_EM_REP=0/1 (with SGV_AB=1) forces either mode.
+constexpr double EM_K_FIX_US = 5.0, EM_K_PER_CM_US = 1.1e-5, EM_T_REP_US = 35.0,
+                 EM_T_PS_US = 15.0, EM_AG_GBS = 100.0;
+static void em_costs(const sgv_ctx* c, double steps, double* rep_us, double* ps_us) {
+  const double km = (double)c->K * (double)c->Mtot, n = (double)c->nranks, L = c->xlat_us;
+  *rep_us = L + 8.0 * km * (n - 1.0) / n / (EM_AG_GBS * 1e3) +
+            steps * (EM_K_FIX_US + EM_K_PER_CM_US * km + EM_T_REP_US);
+  *ps_us = steps * (EM_K_FIX_US + EM_K_PER_CM_US * km / n + EM_T_PS_US + L);
 }
-static bool em_rep_choice(const sgv_ctx* c) {
-  if (c->K > MAXK) return false;   // the replicated loop runs one cohort group
+// the mode of the next EM loop (maxit steps at most); records the prediction
+static bool em_mode_pick(sgv_ctx* c, int maxit) {
+  if (!c->em_rep) return false;
+  const double steps = (double)std::min(maxit, (c->em_prev_steps < 0 ? maxit : c->em_prev_steps) + 1);
+  em_costs(c, steps, &c->em_pred_rep_us, &c->em_pred_ps_us);
+  c->em_pred_steps = steps;
   const char* e = ab_env("SGV_EM_REP");
-  if (e) return e[0] != '0';
-  return (double)c->K * (double)c->Mtot <= em_rep_max_km();
+  const bool rep = e ? e[0] != '0' : c->em_pred_rep_us < c->em_pred_ps_us;
+  c->em_last_rep = rep ? 1 : 0;
+  (rep ? c->em_loops_rep : c->em_loops_ps) += 1.0;
+  return rep;
 }
 
-// replicated EM tables: every rank's block sizes (gathered), the global chunk
-// table and the gathered-r1 buffers
+// At communicator set-up: every rank's block sizes and the latency parameter
+// (rank 0's) are gathered; then, where the replicated loop can run (K <= MAXK,
+// every block within the one-workgroup reduction), the global chunk table and
+// the gathered-r1 buffers
 static int em_rep_setup(sgv_ctx* c, const int* nblk_per_rank) {
-  if (!em_rep_choice(c)) return SGV_OK;
   int nbg = 0;
   for (int r = 0; r < c->nranks; ++r) nbg += nblk_per_rank[r];
-  if (nbg > EM_CTL_MAXBLK) return SGV_OK;   // one-workgroup reduction cap: per-step exchange
-  const size_t nb = (size_t)c->nbmax;
+  const size_t nb = (size_t)c->nbmax + 1;   // [block sizes..., latency]
   double *d_s = nullptr, *d_r = nullptr;
   std::vector<double> hs(nb, 0.0), hr(nb * c->nranks, 0.0);
   for (int b = 0; b < c->nblk; ++b) hs[b] = (double)c->bn[b];
+  {
+    const char* e = std::getenv("SGV_XCHG_LAT_US");
+    char* end = nullptr;
+    const double v = (e && *e) ? std::strtod(e, &end) : -1.0;
+    hs[nb - 1] = (e && end != e && v >= 0.0) ? v : -1.0;
+  }
   double *h_s = nullptr, *h_r = nullptr;
   int rc = SGV_OK;
   if (hipMalloc(&d_s, sizeof(double) * nb) != hipSuccess ||
@@ -1859,6 +1989,11 @@ static int em_rep_setup(sgv_ctx* c, const int* nblk_per_rank) {
   if (h_s) (void)hipHostFree(h_s);
   if (h_r) (void)hipHostFree(h_r);
   CHK(rc);
+  if (hr[nb - 1] >= 0.0) {   // rank 0's SGV_XCHG_LAT_US
+    c->xlat_us = hr[nb - 1];
+    c->xlat_src = 1;
+  }
+  if (c->K > MAXK || nbg > EM_CTL_MAXBLK) return SGV_OK;   // per-step exchange only
   // per-rank padded layouts (the rule of sgv_create), then the global chunks
   std::vector<std::vector<int64_t>> bv(c->nranks);
   int64_t mpmax = PADV;
@@ -2304,10 +2439,13 @@ extern "C" int sgv_synth_r(sgv_ctx* c, int k, uint64_t seed, int64_t marker0, in
 // ---------------------------------------------------------------------------
 // denoiser (src/sgvamp.py:93-114, 270-291)
 // ---------------------------------------------------------------------------
-// denoiser kernel + the ordered reduction of its derivative sums into h_tot[0..K)
+// denoiser kernel + the ordered reduction of its derivative sums into h_tot[0..K);
+// metrics: the four metrics sums of the new xhat1 (sgv_metrics) in the same
+// reduction, h_tot[K .. K + 3] (one exchange instead of two with a communicator;
+// not with more than MAXK cohorts) -- returns whether they were fused
 static int denoise_enqueue(sgv_ctx* c, const double* gam1s, const double* a, double lam,
                            int nslab, const double* omegas, const double* sigmas, double rho,
-                           int damp) {
+                           int damp, bool metrics = false, bool* fused = nullptr) {
   DenoiseArgs da{};
   da.xhat1 = c->xhat1;
   da.nslab = nslab;
@@ -2347,11 +2485,14 @@ static int denoise_enqueue(sgv_ctx* c, const double* gam1s, const double* a, dou
     }
     da.inner = c->d_inner;
   }
+  const bool met = metrics && ng == 1;
+  if (fused) *fused = met;
   for (int g = 0; g < ng; ++g) {
     group(g);
     da.write_x = g == 0 ? 1 : 0;
+    da.x0 = met ? c->x0 : nullptr;
     HIPCHK(launch_denoise(c->d_ch, c->nch, da, c->d_part, c->st));
-    CHK(reduce_dev(c, da.K, c->d_ch_begin, identity_map(), c->h_tot + g * MAXK));
+    CHK(reduce_dev(c, da.K + (met ? 4 : 0), c->d_ch_begin, identity_map(), c->h_tot + g * MAXK));
   }
   return SGV_OK;
 }
@@ -2421,12 +2562,11 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
     for (int l = 0; l < nslab; ++l) hi->om[l] = om[l];
     HIPCHK(hipMemcpyAsync(c->d_ems, hi, sizeof(EmState), hipMemcpyHostToDevice, c->st));
     for (EmArgs& e : eg) e.st = c->d_ems;
-    // one rank: reduction + control in one launch (k_em_reduce_ctl, same bits);
-    // SGV_EM_FUSE=0 A/B.  With a communicator: the replicated EM (em_rep_setup)
-    // runs the same one-rank loop over every rank's gathered r1.
-    const bool rep = c->em_rep;
-    const bool fuse = rep || (!c->comm && !c->host_ag && fused_ctl_pays(EM_NV, c->nblk) &&
-                              em_fuse_default());
+    // one rank: reduction + control in one launch (k_em_reduce_ctl, same bits).
+    // With a communicator: the replicated EM (em_rep_setup) runs the same
+    // one-rank loop over every rank's gathered r1.
+    const bool rep = em_mode_pick(c, maxit);
+    const bool fuse = rep || (!c->comm && !c->host_ag && fused_ctl_pays(EM_NV, c->nblk));
     const ChunkDesc* ech = rep ? c->d_chg : c->d_ch;
     const int* ebeg = rep ? c->d_chg_begin : c->d_ch_begin;
     const int enb = rep ? c->nblkg : c->nblk, ench = rep ? c->nchg : c->nch;
@@ -2462,6 +2602,7 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
     for (int l = 0; l < nslab; ++l) omegas_io[l] = last->om[l];
     if (steps_out) *steps_out = last->steps;
     if (final_err_out) *final_err_out = last->err;
+    c->em_prev_steps = last->steps;   // the same on every rank
     return SGV_OK;
   }
   double om_err = 0.0, lam_err = 0.0;
@@ -2673,13 +2814,8 @@ extern "C" int sgv_mle_update(sgv_ctx* c, const double* gam1s, const double* a, 
   x[L] = std::isnan(*gam_io) ? 1.0 : *gam_io;
   MleFn f{c, gam1s, a, L, sigma2, omega0, 0.0, SGV_OK, {}, {}, false};
   CHK(sgv_mle_exp_max(c, gam1s, L, sigma2, &f.exp_max));           // :152, once per update
-  // :179; SGV_MLE_JAC=0 (with SGV_AB=1): the Jacobian point by point
-  static const bool jb = [] {
-    const char* e = ab_env("SGV_MLE_JAC");
-    return !(e && e[0] == '0');
-  }();
-  const int ier = sgv_fsolve_jac(L + 1, mle_lagrangian, jb ? mle_jacobian : nullptr, &f, x,
-                                 nullptr, nullptr);
+  // :179 (the forward-difference Jacobian's points batched, mle_jacobian)
+  const int ier = sgv_fsolve_jac(L + 1, mle_lagrangian, mle_jacobian, &f, x, nullptr, nullptr);
   if (f.rc != SGV_OK) return f.rc;
   if (ier != 1) {                                                 // :181-184
     *status_out = SGV_MLE_NOT_CONVERGED;
@@ -2800,10 +2936,22 @@ static int lmmse_group(sgv_ctx* c, int g0, int Kg, const double* gamw, const dou
     ia.col.RXp[j] = c->rs_rec ? c->RXp[2 * g0 + j] : nullptr;
     ia.warm[j] = c->xnz[2 * g0 + j];
   }
-  HIPCHK(launch_lmmse_init(c->d_ch, c->nch, ia, c->d_part, c->st));
   double tot[2 * MAXC];
   const bool dev_init = c->cg_pipe;   // CG prologue on the device: no host round trip
-  if (dev_init) {
+  // with a communicator and one LD matrix for the group's columns: the prologue's
+  // sums share iteration 0's exchange (cg_loop_dev, CgMerge0)
+  bool one_ld = true;
+  for (int k = 1; k < K; ++k) one_ld &= c->ld_of[g0 + k] == c->ld_of[g0];
+  const bool merge0 = dev_init && (c->comm || c->host_ag) && one_ld;
+  if (merge0) CHK(grow(c, &c->d_part2, &c->part2_cap, (size_t)c->nch * 2 * MAXC));
+  HIPCHK(launch_lmmse_init(c->d_ch, c->nch, ia, merge0 ? c->d_part2 : c->d_part, c->st));
+  CgMerge0 mg;
+  if (merge0) {
+    mg.part = c->d_part2;
+    mg.rtol = rtol;
+    mg.X = c->X.data() + 2 * g0;
+    mg.RX = c->RX0.data() + 2 * g0;
+  } else if (dev_init) {
     CHK(reduce_dev(c, 2 * MAXC, c->d_ch_begin, identity_map(), c->d_tot));
     HIPCHK(launch_cg_init(c->d_cgs, c->d_tot, rtol, ncol, c->d_ch, c->nch, c->X.data() + 2 * g0,
                           c->RX0.data() + 2 * g0, c->st));
@@ -2842,7 +2990,8 @@ static int lmmse_group(sgv_ctx* c, int g0, int Kg, const double* gamw, const dou
     }
   }
   cc.s = s;
-  CHK(dev_init ? cg_loop_dev(c, cc, nullptr, nullptr, cg_maxit, active, iters, info, &passes)
+  CHK(dev_init ? cg_loop_dev(c, cc, nullptr, nullptr, cg_maxit, active, iters, info, &passes,
+                             merge0 ? &mg : nullptr)
                : cg_run(c, cc, rhov, atol, cg_maxit, active, iters, info, &passes));
 
   // damping, u.Sigma2_u, xhat2.r, x.any() (:322-323, 338, 352)
@@ -3168,13 +3317,78 @@ extern "C" int sgv_exchange_stats(sgv_ctx* c, double* out, int reset) {
   if (!out) return fail(c, SGV_ERR_ARG, "sgv_exchange_stats: out is null");
   CHK(stream_wait(c));
   resolve_timers(c);
+  const bool cm = c->comm || c->host_ag;
   out[0] = c->xchg_n;
   out[1] = c->xchg_ms;
   out[2] = c->xchg_bytes;
-  out[3] = (c->comm || c->host_ag) ? (c->em_rep ? 1.0 : 0.0) : -1.0;
-  out[4] = em_rep_max_km();
+  out[3] = cm ? (double)c->em_last_rep : -1.0;
+  out[4] = c->xlat_us;
   out[5] = c->comm ? 1.0 : c->host_ag ? 2.0 : 0.0;
-  if (reset) c->xchg_n = c->xchg_ms = c->xchg_bytes = 0.0;
+  out[6] = c->em_loops_rep;
+  out[7] = c->em_loops_ps;
+  out[8] = cm ? c->em_pred_rep_us : 0.0;
+  out[9] = cm ? c->em_pred_ps_us : 0.0;
+  out[10] = c->em_pred_steps;
+  out[11] = c->host_wait_ms;
+  out[12] = (double)c->xlat_src;
+  out[13] = c->em_rep ? 1.0 : 0.0;
+  if (reset) {
+    c->xchg_n = c->xchg_ms = c->xchg_bytes = 0.0;
+    c->em_loops_rep = c->em_loops_ps = 0.0;
+    c->host_wait_ms = 0.0;
+  }
+  return SGV_OK;
+}
+
+// The per-all-gather latency of this job's exchange, measured: `reps` ordered
+// reductions of MAXC values over the per-block partials (the CG's own exchange:
+// per-block sums, all-gather, ordered total) on the ctx stream, after one
+// untimed; RCCL: HIP events around them (the wait for the slowest peer
+// included), host exchange: wall time.  The maximum over ranks becomes the EM
+// cost model's L on every rank (em_costs).  Collective: every rank calls it,
+// between steps.  *us_out = the agreed latency (0 without a communicator).
+extern "C" int sgv_exchange_probe(sgv_ctx* c, int reps, double* us_out) {
+  ENTER(c);
+  if (!us_out || reps < 1) return fail(c, SGV_ERR_ARG, "sgv_exchange_probe: bad arguments");
+  *us_out = 0.0;
+  if (!c->comm && !c->host_ag) return SGV_OK;
+  CHK(stream_wait(c));
+  resolve_timers(c);
+  const double n0 = c->xchg_n, ms0 = c->xchg_ms, b0 = c->xchg_bytes;
+  CHK(reduce_dev(c, MAXC, c->d_ch_begin, identity_map(), c->d_tot));   // untimed
+  CHK(stream_wait(c));
+  hipEvent_t e0, e1;
+  CHK(event_pair(c, &e0, &e1));
+  const auto t0 = std::chrono::steady_clock::now();
+  HIPCHK(hipEventRecord(e0, c->st));
+  for (int r = 0; r < reps; ++r) CHK(reduce_dev(c, MAXC, c->d_ch_begin, identity_map(), c->d_tot));
+  HIPCHK(hipEventRecord(e1, c->st));
+  CHK(stream_wait(c));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+  c->evpool.push_back(e0);
+  c->evpool.push_back(e1);
+  const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const double us = 1e3 * (c->comm ? (double)ms : wall) / reps;
+  // agree: every rank's value, the maximum
+  CHK(ensure_stage(c, sizeof(double) * (1 + (size_t)c->nranks)));
+  CHK(ensure_hstage(c, sizeof(double) * (1 + (size_t)c->nranks)));
+  double* hs = (double*)c->h_stage;
+  double* ds = (double*)c->d_stage;
+  hs[0] = us;
+  HIPCHK(hipMemcpyAsync(ds, hs, sizeof(double), hipMemcpyHostToDevice, c->st));
+  CHK(gather_f64(c, ds, ds + 1, 1, hs, hs + 1));
+  HIPCHK(hipMemcpyAsync(hs + 1, ds + 1, sizeof(double) * c->nranks, hipMemcpyDeviceToHost, c->st));
+  CHK(stream_wait(c));
+  resolve_timers(c);
+  double agreed = 0.0;
+  for (int r = 0; r < c->nranks; ++r) agreed = std::max(agreed, hs[1 + r]);
+  c->xlat_us = agreed;
+  c->xlat_src = 2;
+  c->xchg_n = n0;   // the probe is not the job's exchange
+  c->xchg_ms = ms0;
+  c->xchg_bytes = b0;
+  *us_out = agreed;
   return SGV_OK;
 }
 
@@ -3254,13 +3468,17 @@ static int step_impl(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
   if (nslab < 1 || nslab > MAXL) return fail(c, SGV_ERR_ARG, "sgv_step: nslab=%d", nslab);
   // denoiser (:270-291); the output copies and metrics (:281-283, 379-387) are
   // queued behind it before the host waits for the derivative sums
+  bool met_fused = false;
   CHK(denoise_enqueue(c, gam1s, a, *lam_io, nslab, omegas_io, sigmas, rho,
-                      (flags & SGV_STEP_DENOISE_DAMP) ? 1 : 0));
+                      (flags & SGV_STEP_DENOISE_DAMP) ? 1 : 0, (flags & SGV_STEP_METRICS) != 0,
+                      &met_fused));
   HIPCHK(hipEventRecord(c->ev_den, c->st));
   if (out_slot >= 0) CHK(sgv_outputs_begin(c, out_slot));
-  if (flags & SGV_STEP_METRICS) CHK(sgv_metrics_begin(c));
+  if ((flags & SGV_STEP_METRICS) && !met_fused) CHK(sgv_metrics_begin(c));
   CHK(event_spin(c, c->ev_den));
   std::vector<double> der(c->h_tot, c->h_tot + K), alpha1(K), gam2(K);
+  if (met_fused)   // the metrics' ordered sums (sgv_metrics order), long done
+    for (int j = 0; j < 4; ++j) res[1 + 2 * K + j] = c->h_tot[K + j];
   for (int k = 0; k < K; ++k) {
     double a1 = der[k] / (double)c->Mtot;                           // np.mean (:285)
     if (flags & SGV_STEP_ALPHA1_DAMP) a1 = rho * a1 + (1 - rho) * alpha1_prev[k];   // :290-291
@@ -3274,7 +3492,7 @@ static int step_impl(sgv_ctx* c, int it, int flags, int em_maxit, int nslab,
                 (flags & SGV_STEP_LMMSE_DAMP) ? 1 : 0, rho, (flags & SGV_STEP_LEARN_GAMW) ? 1 : 0,
                 out, cg_out, &passes));
   ires[1] = passes;
-  if (flags & SGV_STEP_METRICS) CHK(sgv_metrics_end(c, res + 1 + 2 * K));   // long done
+  if ((flags & SGV_STEP_METRICS) && !met_fused) CHK(sgv_metrics_end(c, res + 1 + 2 * K));
   // inputs of a chained next step: src/sgvamp.py:347, 363-374 (gamw clamped to
   // >= 1 after it is logged, as Python's max(gamw, 1.0))
   sgv_ctx::Chain& ch = c->chain;

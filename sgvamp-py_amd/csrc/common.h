@@ -331,9 +331,12 @@ int ld_pass_rows_per_group();
 // chunk-width class cls: CW = 1024 >> cls columns per work item
 hipError_t launch_sym_pass(int nc, int cls, const SymItem* d_items, int nitems,
                            const PassArgs& pa, double* rowpart, double* colpart, hipStream_t st);
+// MFMA pass (sym_mfma.hip): launch_pk interleaves the columns into Pk, then
+// launch_sym_mfma runs strips d_strips[0 .. nstrips) (one block group or all)
+hipError_t launch_pk(const PassArgs& pa, int nc, int64_t mpad, double* d_pk, hipStream_t st);
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
-                           const PassArgs& pa, int64_t mpad, double* d_pk, double* rowpart,
-                           double* colpart, bool ragged, int pair, int cw, hipStream_t st);
+                           const PassArgs& pa, const double* d_pk, double* rowpart,
+                           double* colpart, bool ragged, int pair, hipStream_t st);
 hipError_t launch_sym_finalize_strip(int nc, const SymPanel* d_panels, int npanels,
                                      const PassArgs& pa, const double* rowpart,
                                      const double* colpart, double* partials, bool ragged,
@@ -347,8 +350,11 @@ hipError_t launch_sym_finalize(int nc, int cls, const SymPanel* d_panels, int np
 // total[v] = sum over all ranks' blocks in global block order, written to
 // dst[map.d[v]].
 // op 0: ordered sum; op 1: min (exact in any order)
+// (ostride > 0: block b's values at bsum[b * ostride + ooff ..], two sources
+// sharing one exchange)
 hipError_t launch_reduce_blocks(const double* d_part, int nv, const int* d_begin, int nblk,
-                                double* d_bsum, hipStream_t st, int op = 0);
+                                double* d_bsum, hipStream_t st, int op = 0, int ostride = 0,
+                                int ooff = 0);
 hipError_t launch_reduce_local(const double* d_part, int nv, const int* d_begin, int nblk,
                                const Map16& map, double* d_dst, hipStream_t st, int op = 0);
 hipError_t launch_reduce_total(const double* d_bsum_all, int nranks, int nbmax, int nv,
@@ -373,6 +379,10 @@ struct DenoiseArgs {
   // launch_den_inner; only the first group writes xhat1 (with the damping)
   const double* inner;
   int write_x;
+  // non-null (with write_x, no cohort groups): the metrics sums of the written
+  // xhat1 against x0 (k_metrics' four, in its order) ride in the same partials,
+  // after the K derivative sums -- one ordered reduction for both
+  const double* x0;
 };
 hipError_t launch_denoise(const ChunkDesc* d_ch, int nch, const DenoiseArgs& a, double* d_part,
                           hipStream_t st);

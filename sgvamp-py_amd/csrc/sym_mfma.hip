@@ -36,7 +36,6 @@
 // order).
 // Dcol accumulates over all rows of the strip in registers; every order is fixed.
 #include "common.h"
-#include "xpose.h"
 
 namespace sgv {
 
@@ -72,12 +71,6 @@ __device__ __forceinline__ void lds_order() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// SGV_BAND_SKIP=0 (A/B, with SGV_AB=1; read by the host at launch and passed
-// in the strip flags would cost a register -- a device constant is enough):
-// band strips' all-zero steps run their MFMAs as before
-__constant__ int c_band_rag_skip = 1;
-__device__ __forceinline__ bool band_rag_skip() { return c_band_rag_skip != 0; }
-
 constexpr int MF_CW = 512;   // chunk width (class 1 items)
 constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conflict-free both ways
 
@@ -90,45 +83,34 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // take zero B operands there (exact: R * 0 adds 0).  Row sums are still written
 // per (panel, chunk) item.  Panel descriptors are wave-uniform (SGPRs); the
 // prefetch of the next row group crosses panel boundaries through selects.
-// PW: each wave keeps its row sums of the whole panel in its own LDS rows
+// Each wave keeps its row sums of the whole panel in its own LDS rows
 // (wrow[wave][row][4 NG]); the four waves' values are added, in wave order, once
-// per panel when the item's row partials are written -- the same additions as
-// the per-row-group exchange through red[] (PW = false), with one barrier pair
-// per panel instead of a barrier per 16-row group.
+// per panel when the item's row partials are written (one barrier pair per
+// panel).  Steps at or past the chunk's last column take no LDS or MFMA work.
 // DEF: a step's row MFMAs are deferred into the next step and interleaved with
 // its column MFMAs, so consecutive MFMAs of one accumulator chain sit 8 issues
 // apart instead of 4 (2 at NG = 1); every chain accumulates in the same order
 // (bitwise the same sums), the row fragments are double-buffered in registers.
-// CW: the strips' chunk width -- 512 (class-1 items), or 256 (class-2 items,
-// band plans: a band panel's stored extent is a multiple of 256, so no item of
-// a 256-column strip is narrower than its strip; with 512-column chunks every
-// band strip's first item is half empty, its waves 2-3 idle)
-template <int NG, int NW, int PD, bool PW, bool SKIP, bool RAG = false, bool DEF = false, int XP = 0,
-          int CW = MF_CW>
-__global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
-                                                         const SymItem* __restrict__ sitems,
-                                                         const double* __restrict__ pk, int ncol,
-                                                         double* __restrict__ rowpart,
-                                                         double* __restrict__ colpart,
-                                                         const int* __restrict__ run, int pks) {
-  static_assert(NW == 4, "waves 0 and 1 own the diagonal half of a chunk");
-  static_assert(CW == 512 || CW == 256, "chunk width");
-  constexpr int WC = CW / NW;      // columns per wave (128; 64 at CW = 256)
+// RAG: some item of the strip stops short of the strip's widest (band plans).
+template <int NG, int PD, bool RAG = false, bool DEF = false>
+__global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
+                                                     const SymItem* __restrict__ sitems,
+                                                     const double* __restrict__ pk, int ncol,
+                                                     double* __restrict__ rowpart,
+                                                     double* __restrict__ colpart,
+                                                     const int* __restrict__ run, int pks) {
+  constexpr int NW = 4;            // waves 0 and 1 own the diagonal half of a chunk
+  constexpr int WC = MF_CW / NW;   // columns per wave
   constexpr int NT = WC / 32;      // 32-column steps per wave
   static_assert(PD >= 1 && PD <= NT && NT % PD == 0, "prefetch depth divides the steps");
   constexpr int RW = 4 * NG;       // row-sum stride of wrow
-  // PW: wrow[NW][SYM_H][RW]; else red[2][NW][256] then rbuf[SYM_H * RW]: a
-  // panel's row sums collect in rbuf and leave as one contiguous 16-B-store
-  // burst per (panel, chunk) item
-  constexpr int ROWBUF = PW ? NW * SYM_H * RW : 2 * NW * 256 + SYM_H * RW;
-  __shared__ __attribute__((aligned(16))) double rowbuf[ROWBUF];
+  __shared__ __attribute__((aligned(16))) double rowbuf[NW * SYM_H * RW];   // wrow
   // the per-wave transpose tile: 16 rows x 32 columns, 16-B piece (row r, pair
-  // p) at slot 16 r + (p ^ (r & 3)) -- unpadded (4 KiB, so PW's 64 KiB of row
+  // p) at slot 16 r + (p ^ (r & 3)) -- unpadded (4 KiB, so the 64 KiB of row
   // sums and the tiles fit two workgroups per CU) and conflict-free both ways:
   // a write's 16-lane quarter covers one row, a row-fragment read's quarter
   // (rows 4q + (l & 3), pairs 4((l >> 2) & 3) + (l >> 4)) 16 distinct slots mod 16
-  __shared__ __attribute__((aligned(16))) double stg[XP == 0 ? NW : 1][16 * 32];
-  double* rbuf = rowbuf + 2 * NW * 256;
+  __shared__ __attribute__((aligned(16))) double stg[NW][16 * 32];
   const SymStrip sp = strips[blockIdx.x];
   if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
   MF_TRACE_BEGIN
@@ -138,20 +120,18 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   const int pc = hi + 4 * bq;                          // this lane's column pair in a fragment
   SymItem cur = sitems[sp.it0];
   const int c0 = cur.c0, ncc = sp.ncmax;               // the strip's chunk, widest item
-  const int PKS = pks;             // Pk row stride (k_pack): 4 NG, or 16 (A/B)
+  const int PKS = pks;             // Pk row stride (k_pack): 4 NG
   const double* pkb = pk + (int64_t)cur.voff * PKS;   // Pk of this block (block-relative index)
   const int cw0 = wid * WC;                            // first chunk column of this wave
   const bool dhalf = cw0 < SYM_H;                      // wave inside a diagonal panel's diag block
-  // SKIP: a wave's 32-column steps at or past the chunk's last column (the
+  // A wave's 32-column steps at or past the chunk's last column (the
   // ragged last chunk of a panel: 4 % of the north star's steps) take no LDS or
   // MFMA work -- their row-part B operands are 0 and their column sums are never
   // read, so every kept sum is bitwise the same; nor do the column MFMAs of the
   // diagonal-block waves of a diagonal panel (B = 0 there).  The loads stay, so
   // the load count is the same on every path.
-  const int nta = SKIP ? min(NT, max(0, (ncc - cw0 + 31) / 32)) : NT;
-  double* sb = stg[XP == 0 ? wid : 0];
-  const bool xl1 = (lane & 2) != 0, xl0 = (lane & 1) != 0;   // XP = 1: quad lane bits
-  const int xsrc4 = 4 * (16 * n4 + 4 * bq + hi);               // XP = 2: source lane x 4
+  const int nta = min(NT, max(0, (ncc - cw0 + 31) / 32));
+  double* sb = stg[wid];
 
   // row-part B operands: P at this wave's columns, reused by every row group
   double brow[NT][2][NG];
@@ -225,7 +205,6 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   for (int p = 0; p < PD; ++p) load_cf(curb, cur.w, cur.H, cur.nc, 0, p, cfq[p]);
   load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
 
-  int gg = 0;                                          // row groups done (LDS buffer parity)
 #pragma unroll 1
   for (int s = 0; s < sp.npan; ++s) {                  // uniform over the workgroup
     const bool more = s + 1 < sp.npan;
@@ -233,7 +212,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
     const uint64_t nxb = more ? pbase(nx) : (uint64_t)pkb;
     const int ng = (cur.H + 15) / 16;
 #pragma unroll 1
-    for (int g = 0; g < ng; ++g, ++gg) {
+    for (int g = 0; g < ng; ++g) {
       // the next row group: this panel's g + 1, or the next panel's first
       const bool same = g + 1 < ng;
       const uint64_t gb = same ? curb : nxb;
@@ -253,12 +232,12 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int q = 0; q < NG; ++q) drow[r][q] = 0.0;
-      const bool colz = SKIP && dhalf && cur.r0 == c0;   // this panel's column B operands are 0
+      const bool colz = dhalf && cur.r0 == c0;   // this panel's column B operands are 0
       // a band item narrower than its strip (its panel's last 256 columns): a
       // step wholly past its stored end adds only zeros -- skipped like the
-      // steps past the chunk (band_rag_skip, default on); per panel, so the
-      // deferred row MFMAs (DEF) know the item's last active step
-      const int ntp = (RAG && band_rag_skip()) ? min(nta, max(0, (cur.nc - cw0 + 31) / 32)) : nta;
+      // steps past the chunk; per panel, so the deferred row MFMAs (DEF) know
+      // the item's last active step
+      const int ntp = RAG ? min(nta, max(0, (cur.nc - cw0 + 31) / 32)) : nta;
       d2 rfb[DEF ? 2 : 1][4];                            // row fragments (DEF: this and the previous step)
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -276,20 +255,14 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
         }
         if (t >= ntp) continue;                        // wave-uniform: past the chunk / item
         if (RAG && cur.nc < ncc) band_zero(cur.nc, t, cf);   // uniform: a band item's stored end
-        if constexpr (XP == 1) {
-          xpose_perm(cf, rf, xl1, xl0);
-        } else if constexpr (XP == 2) {
-          xpose_bperm(cf, rf, xsrc4);
-        } else {
-          lds_order();                                 // previous step's tile reads issued
+        lds_order();                                   // previous step's tile reads issued
 #pragma unroll
-          for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[a];
-          lds_order();                                 // tile written
-          // the row fragment reads go out right behind the writes (a wave's DS
-          // operations execute in order); the column MFMAs cover their latency
+        for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[a];
+        lds_order();                                   // tile written
+        // the row fragment reads go out right behind the writes (a wave's DS
+        // operations execute in order); the column MFMAs cover their latency
 #pragma unroll
-          for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
-        }
+        for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
         // the MFMA burst at raised wave priority: the SIMD's other wave, whose
         // loads are in flight, takes the issue slots back when this one drains
         // (NC = 4/8 0.7-1.5 % faster per pass on two boxes; NC = 16 1 % slower,
@@ -345,45 +318,20 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
         }
         __builtin_amdgcn_s_setprio(0);
       }
-      // row sums: the 4 blocks (lanes differing in bits 2,3), then the waves in order
-      if constexpr (PW) {
-        double* wb = rowbuf + (wid * SYM_H + 16 * g) * RW;
+      // row sums: the 4 blocks (lanes differing in bits 2,3; DPP row rotations),
+      // kept per wave for the panel
+      double* wb = rowbuf + (wid * SYM_H + 16 * g) * RW;
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-          for (int q = 0; q < NG; ++q) {
-            double v = drow[r][q];
-            v = v + row_ror<12>(v);
-            v = v + row_ror<8>(v);
-            if (bq == 0) wb[(4 * r + hi) * RW + 4 * q + n4] = v;   // D row 4r + m (m = hi)
-          }
-      } else {
-        double* rb = rowbuf + ((gg & 1) * NW + wid) * 256;
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int q = 0; q < NG; ++q) {
-            double v = drow[r][q];
-            // lanes bq = 0: (v0 + v1) + (v2 + v3), block b's value at lane + 4b
-            // (DPP row rotations: VALU moves, no LDS round trip)
-            v = v + row_ror<12>(v);
-            v = v + row_ror<8>(v);
-            if (bq == 0) rb[((4 * r + hi) << 4) + 4 * q + n4] = v;   // D row 4r + m (m = hi)
-          }
-        __syncthreads();
-        if (threadIdx.x < 256) {
-          const int t = threadIdx.x, row = t >> 4, cc = t & 15;
-          if (16 * g + row < cur.H && cc < ncol) {
-            const double* red = rowbuf + (gg & 1) * NW * 256;
-            double v = red[t];
-#pragma unroll
-            for (int w = 1; w < NW; ++w) v += red[w * 256 + t];
-            rbuf[(16 * g + row) * ncol + cc] = v;
-          }
+        for (int q = 0; q < NG; ++q) {
+          double v = drow[r][q];
+          v = v + row_ror<12>(v);
+          v = v + row_ror<8>(v);
+          if (bq == 0) wb[(4 * r + hi) * RW + 4 * q + n4] = v;   // D row 4r + m (m = hi)
         }
-      }
     }
-    if constexpr (PW) {   // the item's H x ncol row sums: waves in order, contiguous in rowpart
+    {   // the item's H x ncol row sums: waves in order, contiguous in rowpart
       __syncthreads();
       const int n = cur.H * ncol;
       double* dst = rowpart + (int64_t)cur.item * SYM_H * ncol;
@@ -405,16 +353,6 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
           dst[2 * i] = v[0];
       }
       __syncthreads();    // the waves' rows are read before the next panel writes them
-    } else {   // the item's H x ncol row sums, contiguous in rowpart
-      __syncthreads();
-      const int n = cur.H * ncol;
-      double* dst = rowpart + (int64_t)cur.item * SYM_H * ncol;
-      for (int i = threadIdx.x; 2 * i < n; i += NW * 64) {
-        if (2 * i + 1 < n)
-          *(d2*)(dst + 2 * i) = *(const d2*)(rbuf + 2 * i);
-        else
-          dst[2 * i] = rbuf[2 * i];
-      }
     }
     cur = nx;
     curb = nxb;
@@ -436,7 +374,7 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
   MF_TRACE_END
 }
 
-// Wave-pair form of k_sym_mfma (PW, SKIP; no band items): one 8-wave workgroup
+// Wave-pair form of k_sym_mfma (no band items): one 8-wave workgroup
 // per strip, TWO waves per 128-column segment, each owning 64 columns (two
 // 32-column steps).  Every sum is the 4-wave kernel's, bit for bit:
 //  * a column's sum is one MFMA chain over the strip's rows in one wave, as
@@ -454,13 +392,13 @@ __global__ __launch_bounds__(NW * 64, 2) void k_sym_mfma(const SymStrip* __restr
 // the form can be chosen per partition.  One barrier per 16-row group: the
 // hand-off (first wave: accumulators out before it; second wave: in after it,
 // double-buffered by row-group parity).
-// MAP 0: waves 2s, 2s + 1 hold segment s (the pair on two SIMDs); MAP 1: waves
-// s, s + 4 (waves are dealt to SIMDs round-robin: the pair shares one SIMD, each
-// SIMD runs one first and one second half)
-// SYNC 0: one workgroup barrier per row group; SYNC 1: each pair syncs on its
-// own LDS counters (the first wave up to HS - 1 row groups ahead, a ring of HS
-// hand-off slots), barriers only at panel ends
-template <int NG, int PD, int XP, int MAP = 0, int SYNC = 0>
+// Waves s and s + 4 hold segment s (waves are dealt to SIMDs round-robin: the
+// pair shares one SIMD, each SIMD runs one first and one second half); each
+// pair syncs on its own LDS counters (the first wave up to HS - 1 row groups
+// ahead, a ring of HS hand-off slots), barriers only at panel ends.  The other
+// forms measured -- pair on two SIMDs, a barrier per row group -- were slower
+// 
+template <int NG, int PD>
 __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __restrict__ strips,
                                                           const SymItem* __restrict__ sitems,
                                                           const double* __restrict__ pk, int ncol,
@@ -473,16 +411,16 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
   static_assert(PD >= 1 && PD <= NT && NT % PD == 0, "prefetch depth divides the steps");
   constexpr int RW = 4 * NG;
   __shared__ __attribute__((aligned(16))) double wrow[4 * SYM_H * RW];   // [segment][row][4 NG]
-  constexpr int HS = SYNC ? 3 : 2;                                        // hand-off slots
+  constexpr int HS = 3;                                                    // hand-off slots
   __shared__ __attribute__((aligned(16))) double hand[HS][4][4 * NG][WAVE];   // [gg % HS][segment][r, q][lane]
-  __shared__ int hready[4], hdone[4];   // SYNC: row groups handed / taken per segment
-  __shared__ __attribute__((aligned(16))) double stg[XP == 0 ? NW : 1][16 * 32];
+  __shared__ int hready[4], hdone[4];   // row groups handed / taken per segment
+  __shared__ __attribute__((aligned(16))) double stg[NW][16 * 32];
   const SymStrip sp = strips[blockIdx.x];
   if (run && !ldg(run)) return;
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-  const int seg = MAP ? (wid & 3) : (wid >> 1);        // 128-column segment
-  const int h = MAP ? (wid >> 2) : (wid & 1);            // half
+  const int seg = wid & 3;                               // 128-column segment
+  const int h = wid >> 2;                                // half
   const int lo = lane & 15, hi = lane >> 4, bq = (lane >> 2) & 3, n4 = lane & 3;
   const int pc = hi + 4 * bq;
   SymItem cur = sitems[sp.it0];
@@ -494,9 +432,7 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
   // the segment's active 32-column steps (the 4-wave kernel's nta), this wave's share
   const int nta_seg = min(4, max(0, (ncc - seg * 128 + 31) / 32));
   const int nta = min(NT, max(0, nta_seg - NT * h));
-  double* sb = stg[XP == 0 ? wid : 0];
-  const bool xl1 = (lane & 2) != 0, xl0 = (lane & 1) != 0;
-  const int xsrc4 = 4 * (16 * n4 + 4 * bq + hi);
+  double* sb = stg[wid];
 
   double brow[NT][2][NG];
 #pragma unroll
@@ -547,10 +483,8 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
 #pragma unroll
   for (int p = 0; p < PD; ++p) load_cf(curb, cur.w, cur.H, 0, p, cfq[p]);
   load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
-  if (SYNC) {
-    if (threadIdx.x < 4) hready[threadIdx.x] = hdone[threadIdx.x] = 0;
-    __syncthreads();
-  }
+  if (threadIdx.x < 4) hready[threadIdx.x] = hdone[threadIdx.x] = 0;
+  __syncthreads();
   auto lds_wait_ge = [&](int* ctr, int v) {
     while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v)
       __builtin_amdgcn_s_sleep(1);
@@ -608,18 +542,12 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
         }
         if (t >= nta) continue;
         d2* rf = rfs[t];
-        if constexpr (XP == 1) {
-          xpose_perm(cf, rf, xl1, xl0);
-        } else if constexpr (XP == 2) {
-          xpose_bperm(cf, rf, xsrc4);
-        } else {
-          lds_order();
+        lds_order();
 #pragma unroll
-          for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[a];
-          lds_order();
+        for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[a];
+        lds_order();
 #pragma unroll
-          for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
-        }
+        for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
         __builtin_amdgcn_s_setprio(1);
         if (!colz) {
 #pragma unroll
@@ -635,23 +563,20 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
       }
       double* hs = &hand[gg % HS][seg][0][0];
       if (h == 0) {
-        if (SYNC) lds_wait_ge(&hdone[seg], gg - HS + 1);   // slot gg % HS taken back
+        lds_wait_ge(&hdone[seg], gg - HS + 1);   // slot gg % HS taken back
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int q = 0; q < NG; ++q) hs[(r * NG + q) * WAVE + lane] = drow[r][q];
-        if (SYNC)
-          __hip_atomic_store(&hready[seg], gg + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&hready[seg], gg + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
-      if (!SYNC) __syncthreads();   // hand-off of row group gg (and the reads of gg - 2)
       if (h == 1) {
-        if (SYNC) lds_wait_ge(&hready[seg], gg + 1);
+        lds_wait_ge(&hready[seg], gg + 1);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
           for (int q = 0; q < NG; ++q) drow[r][q] = hs[(r * NG + q) * WAVE + lane];
-        if (SYNC)
-          __hip_atomic_store(&hdone[seg], gg + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&hdone[seg], gg + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int t = 0; t < NT; ++t)
@@ -715,7 +640,7 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
 //   16x16x4 f64 C/D layout (cdna_hip_programming.md): D[(l>>4) + 4r][l & 15].
 typedef double d4 __attribute__((ext_vector_type(4)));
 #define MFMA16(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
-template <int PD, bool SKIP, bool RAG = false, int CW = MF_CW>
+template <int PD, bool RAG = false>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -723,7 +648,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
                                                      double* __restrict__ colpart,
                                                      const int* __restrict__ run) {
   constexpr int LDP = MF_LDP;
-  constexpr int MF_WC = CW / 4;    // columns per wave
+  constexpr int MF_WC = MF_CW / 4; // columns per wave
   constexpr int MF_NT = MF_WC / 32;
   __shared__ double red[2][4][256];
   __shared__ __attribute__((aligned(16))) double stg[4][16 * LDP];
@@ -737,7 +662,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
   const double* pkb = pk + (int64_t)cur.voff * 16;    // Pk of this block (block-relative index)
   const int cw0 = wid * MF_WC;                         // first chunk column of this wave
   const bool dhalf = cw0 < SYM_H;
-  const int nta = SKIP ? min(MF_NT, max(0, (ncc - cw0 + 31) / 32)) : MF_NT;   // as k_sym_mfma
+  const int nta = min(MF_NT, max(0, (ncc - cw0 + 31) / 32));   // as k_sym_mfma
 
   double* sb = stg[wid];
   // row-part B operands (P at this wave's columns), reused by every row group
@@ -813,7 +738,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
 #pragma unroll
       for (int a = 0; a < 4; ++a) bcol[a] = bcn[a];
       d4 drow0 = d4{0.0, 0.0, 0.0, 0.0}, drow1 = drow0;
-      const bool colz = SKIP && dhalf && cur.r0 == c0;
+      const bool colz = dhalf && cur.r0 == c0;
 #pragma unroll
       for (int t = 0; t < MF_NT; ++t) {
         d2 cf[4], rf[4];
@@ -828,7 +753,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
           if (t + PD == MF_NT) load_bcol(gr0, gH, gz, gn, bcn);
         }
         if (t >= nta) continue;
-        if (RAG && cw0 + 32 * t >= cur.nc && band_rag_skip()) continue;   // as k_sym_mfma
+        if (RAG && cw0 + 32 * t >= cur.nc) continue;   // as k_sym_mfma
         if (RAG && cur.nc < ncc) band_zero(cur.nc, t, cf);
         lds_order();                                   // previous step's tile reads done
 #pragma unroll
@@ -1003,174 +928,31 @@ __global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpa
   pk[t] = c < ncol ? pa.in[c][i] : 0.0;
 }
 
-// SGV_MF_PW (A/B, with SGV_AB=1): 0 = the per-row-group exchange of the row
-// sums (k_sym_mfma<.., false>), default 1 = per-wave panel rows
-static bool mf_pw() {
-  static const bool v = [] {
-    const char* e = ab_env("SGV_MF_PW");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
-// SGV_MF_SKIP (A/B, with SGV_AB=1): default 1 = no LDS/MFMA work on steps past
-// the chunk (bitwise the same products; the 8-block share 2-4 % faster per pass,
-// the 64-block north star unchanged -- profiles/r03/skip_ab.jsonl); 0 = every step
-static bool mf_skip() {
-  static const bool v = [] {
-    const char* e = ab_env("SGV_MF_SKIP");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
-// SGV_MF_DEFER (A/B, with SGV_AB=1): default 1 = row MFMAs deferred into the
-// next step (k_sym_mfma<.., DEF>: bitwise the same products; NC = 4 passes
-// 1-2 % faster, NC = 8 within noise -- profiles/r03/s4/mf_defer_ab.jsonl);
-// 0 = a step's row MFMAs right behind its column MFMAs
-static bool mf_defer() {
-  static const bool v = [] {
-    const char* e = ab_env("SGV_MF_DEFER");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
-// SGV_MF16_PD (A/B, with SGV_AB=1): prefetch depth of k_sym_mfma16, default 2
-// (bitwise the same products; C5's pass -1.3 %, the 8-block share -2.5 %, M = 1e6
-// at 16 columns within noise -- profiles/r03/s4/mf16_pd_ab.jsonl), 1 = one step
-static int mf16_pd() {
-  static const int v = [] {
-    const char* e = ab_env("SGV_MF16_PD");
-    return (e && e[0] == '1') ? 1 : 2;
-  }();
-  return v;
-}
-
-// SGV_MF_XPOSE (A/B, with SGV_AB=1): the row fragment's transpose -- default 0
-// through the per-wave LDS tile, 1 permlane swaps + quad DPP, 2 ds_bpermute
-static int mf_xpose() {
-  static const int v = [] {
-    const char* e = ab_env("SGV_MF_XPOSE");
-    return (e && (e[0] == '1' || e[0] == '2')) ? e[0] - '0' : 0;
-  }();
-  return v;
-}
-
-// SGV_BAND_DEF (A/B, with SGV_AB=1): band plans' NC <= 8 kernel with the
-// deferred row MFMAs (1, bitwise the same products) or without (0, default:
-// 2.15-2.16 vs 2.145-2.15 ms at M = 1e6, bw = 1,000, profiles/r04/band2_ab.jsonl)
-static bool band_def() {
-  static const bool v = [] {
-    const char* e = ab_env("SGV_BAND_DEF");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
-// SGV_BAND_PD (A/B, with SGV_AB=1): prefetch depth of band plans' NC <= 8
-// kernel -- 2 (default) or 4 steps in flight per wave (bitwise the same products)
-static int band_pd() {
-  static const int v = [] {
-    const char* e = ab_env("SGV_BAND_PD");
-    return (e && e[0] == '4') ? 4 : 2;
-  }();
-  return v;
-}
-
-// SGV_MF_PAIR_MAP (A/B, with SGV_AB=1): k_sym_mfma_pair's form -- 0 waves 2s,
-// 2s + 1 per segment with a barrier per row group, 1 the pair on one SIMD, 2 / 3
-// those with per-pair LDS counters instead of the barriers; default 3 (best of
-// the four at 4 and 8 columns, profiles/r04/pairsync_ab.jsonl)
-static int mf_pair_map() {
-  static const int v = [] {
-    const char* e = ab_env("SGV_MF_PAIR_MAP");
-    return (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : 3;
-  }();
-  return v;
-}
-
-
-// ragged: some strip item stops short of its strip's widest (band blocks): the
-// RAG kernels (default variant only: the A/B switches do not apply there)
-template <int NG, int NW, int PD>
+// ragged: some strip item stops short of its strip's widest (band blocks):
+// the RAG kernels, without the deferred row MFMAs (even there,
+// profiles/r04/band2_ab.jsonl).  pair: the plan's choice of the wave-pair
+// kernel (capi.hip build_strips; bitwise the same products) -- 1: 3-4 columns
+// only (at 5-8 the pair form runs ~14 % slower per byte and a short launch's
+// tail does not pay it back), 2 (forced, SGV_MF_PAIR=1): every column count
+template <int NG>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
-                      const int* run, int pks, bool ragged, int pair, int cw, hipStream_t st) {
-  // SGV_MF_RAG=1 (A/B, SGV_AB=1): the band plans' kernel for every plan (bitwise
-  // the same products).  It holds 2.2-2.3 GHz on band LD but 1.43-1.47 GHz on the
-  // north star's dense blocks, as the dense kernel does: the clock follows the
-  // data, not the instruction mix (profiles/r04/ragclk_*)
-  static const bool force_rag = [] {
-    const char* e = ab_env("SGV_MF_RAG");
-    return e && e[0] == '1';
-  }();
-  ragged = ragged || force_rag;
-  if (cw == 256)   // band plans' 256-column strips (no item narrower than its strip)
-    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, false, true, 0, 256>), dim3(nstrips),
-                       dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (ragged && band_pd() == 4)
-    hipLaunchKernelGGL((k_sym_mfma<NG, NW, 4, true, true, true>), dim3(nstrips), dim3(NW * 64), 0,
-                       st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (ragged && band_def())
-    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, true, true>), dim3(nstrips),
-                       dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (ragged)
-    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, true>), dim3(nstrips), dim3(NW * 64), 0,
-                       st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (pair >= (NG == 1 ? 1 : 2) && mf_pair_map() == 3)
-    // the plan's choice (capi.hip build_strips; bitwise the same products): 3-4
-    // pair 1: 3-4 columns only -- at 5-8 the pair form runs ~14 % slower per
-    // byte (profiles/r04/pairsync_ab.jsonl) and a short launch's tail does not
-    // pay it back; pair 2 (forced, SGV_MF_PAIR=1): every column count
-    hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0, 1, 1>), dim3(nstrips), dim3(512), 0, st, d_strips,
-                       d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (pair >= (NG == 1 ? 1 : 2) && mf_pair_map() == 2)
-    hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0, 0, 1>), dim3(nstrips), dim3(512), 0, st, d_strips,
-                       d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (pair >= (NG == 1 ? 1 : 2) && mf_pair_map() == 1)
-    hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0, 1>), dim3(nstrips), dim3(512), 0, st, d_strips,
+                      const int* run, int pks, bool ragged, int pair, hipStream_t st) {
+  // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
+  if (ragged)
+    hipLaunchKernelGGL((k_sym_mfma<NG, 2, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else if (pair >= (NG == 1 ? 1 : 2))
-    hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, 0>), dim3(nstrips), dim3(512), 0, st, d_strips,
+    hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_pw() && mf_skip() && mf_defer() && mf_xpose() == 1)
-    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, false, true, 1>), dim3(nstrips),
-                       dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_pw() && mf_skip() && mf_defer() && mf_xpose() == 2)
-    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, false, true, 2>), dim3(nstrips),
-                       dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_pw() && mf_skip() && mf_defer())
-    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true, false, true>), dim3(nstrips),
-                       dim3(NW * 64), 0, st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_pw() && mf_skip())
-    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, true>), dim3(nstrips), dim3(NW * 64), 0, st,
-                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_pw())
-    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, true, false>), dim3(nstrips), dim3(NW * 64), 0, st,
-                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else
-    hipLaunchKernelGGL((k_sym_mfma<NG, NW, PD, false, false>), dim3(nstrips), dim3(NW * 64), 0, st,
+    hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true>), dim3(nstrips), dim3(256), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
 }
 
-hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
-                           const PassArgs& pa, int64_t mpad, double* d_pk, double* rowpart,
-                           double* colpart, bool ragged, int pair, int cw, hipStream_t st) {
+hipError_t launch_pk(const PassArgs& pa, int nc, int64_t mpad, double* d_pk, hipStream_t st) {
   if (nc < 1 || nc > 16) return hipErrorInvalidValue;
-  static const hipError_t band_skip_set = [] {   // SGV_BAND_SKIP=0: the A/B's old band steps
-    const char* e = ab_env("SGV_BAND_SKIP");
-    if (!(e && e[0] == '0')) return hipSuccess;
-    const int zero = 0;
-    return hipMemcpyToSymbol(HIP_SYMBOL(c_band_rag_skip), &zero, sizeof zero);
-  }();
-  if (band_skip_set != hipSuccess) return band_skip_set;
-  // SGV_PK16=1 (A/B, SGV_AB=1): the round-2 16-column Pk rows for every NC
-  static const bool pk16 = [] {
-    const char* e = ab_env("SGV_PK16");
-    return e && e[0] == '1';
-  }();
-  const int pks = (nc > 8 || pk16) ? 16 : nc <= 4 ? 4 : 8;
+  const int pks = nc > 8 ? 16 : nc <= 4 ? 4 : 8;
   const int64_t npk = mpad * pks;
   const dim3 pg((unsigned)((npk + 255) / 256));
   if (pks == 4)
@@ -1179,36 +961,31 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
     hipLaunchKernelGGL(k_pack<8>, pg, dim3(256), 0, st, pa, nc, mpad, d_pk);
   else
     hipLaunchKernelGGL(k_pack<16>, pg, dim3(256), 0, st, pa, nc, mpad, d_pk);
+  return hipGetLastError();
+}
+
+hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
+                           const PassArgs& pa, const double* d_pk, double* rowpart,
+                           double* colpart, bool ragged, int pair, hipStream_t st) {
+  if (nc < 1 || nc > 16) return hipErrorInvalidValue;
+  if (nstrips <= 0) return hipSuccess;
+  const int pks = nc > 8 ? 16 : nc <= 4 ? 4 : 8;
   // 9..16 columns: one 16x16x4 group beats three/four 4x4x4 groups (register
   // pressure) and two 8-column wave sets of the 4x4x4 kernel in one 8-wave
   // workgroup re-reading the same R with the default cache policy (+33 %,
   // profiles/r03/s4/mf_sets_ab.jsonl) and three / four 4x4x4 groups at one wave
   // per SIMD with the deferred row MFMAs (+13 % / +28 %, ng4_ab.jsonl):
-  // measured in DESIGN.md
+  // measured in DESIGN.md.  Prefetch depth 2 (7 VGPRs spilled on band plans,
+  // still faster: profiles/r03/s4/mf16_pd_ab.jsonl, profiles/r04/band2_ab.jsonl)
   switch ((nc + 3) / 4) {
-    // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
-    case 1: launch_mf<1, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, cw, st); break;
-    case 2: launch_mf<2, 4, 2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, cw, st); break;
+    case 1: launch_mf<1>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
+    case 2: launch_mf<2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
     default:
-      if (cw == 256)
-        hipLaunchKernelGGL((k_sym_mfma16<2, true, false, 256>), dim3(nstrips), dim3(256), 0, st,
-                           d_strips, d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-      else if (ragged && mf16_pd() == 2)   // band plans at the dense plans' prefetch depth
-        // (7 VGPRs spilled, still -2.3 %: 2.58-2.59 vs 2.64-2.65 ms at M = 1e6, bw =
-        // 1,000, bitwise the same products, profiles/r04/band2_ab.jsonl)
-        hipLaunchKernelGGL((k_sym_mfma16<2, true, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-      else if (ragged)
-        hipLaunchKernelGGL((k_sym_mfma16<1, true, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-      else if (mf16_pd() == 2)
+      if (ragged)
         hipLaunchKernelGGL((k_sym_mfma16<2, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
                            d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-      else if (mf_skip())
-        hipLaunchKernelGGL((k_sym_mfma16<1, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       else
-        hipLaunchKernelGGL((k_sym_mfma16<1, false>), dim3(nstrips), dim3(256), 0, st, d_strips,
+        hipLaunchKernelGGL((k_sym_mfma16<2>), dim3(nstrips), dim3(256), 0, st, d_strips,
                            d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       break;
   }
@@ -1241,6 +1018,7 @@ hipError_t launch_sym_finalize_strip(int nc, const SymPanel* d_panels, int npane
                                      hipStream_t st) {
   // the partials with the default cache policy: nontemporal loads measured
   // 0.5-3 % slower (profiles/r03/s4/fin_nt_ab.jsonl; they were just written)
+  if (npanels <= 0) return hipSuccess;   // a block group without packed panels
   const bool one = fin_form(ragged, nc) == 1;
 #define FIN_CASE(N)                                                                        \
   case N:                                                                                  \

@@ -204,27 +204,14 @@ __global__ __launch_bounds__(256 * FIN_Q) void k_sym_finalize(const SymPanel* __
   fin_epilogue<NC>(pn, pa, y, partials, pre);
 }
 
-// SGV_SYM_SKIP (A/B, with SGV_AB=1): default 1 = sweep only the stored segments of a
-// chunk (bitwise the same; north-star blocks NC = 2 -2.5 %, profiles/r03/sym_skip_ab.jsonl);
-// 0 = every segment
-static bool sym_skip() {
-  static const bool v = [] {
-    const char* e = ab_env("SGV_SYM_SKIP");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
+// the stored segments of a chunk only (bitwise the same; north-star blocks NC = 2
+// -2.5 %, profiles/r03/sym_skip_ab.jsonl)
 template <int NC, int NSEG>
 static hipError_t launch_sym_nc(const SymItem* d_items, int nitems, const PassArgs& pa,
                                 double* rowpart, double* colpart, hipStream_t st) {
   constexpr int RWI = (NC <= 2) ? 8 : (NC <= 4) ? 4 : (NC <= 8) ? 2 : 1;   // RWI*NC <= 16
-  if (sym_skip())
-    hipLaunchKernelGGL((k_sym_pass<NC, RWI, NSEG, true>), dim3(nitems), dim3(256), 0, st, d_items,
-                       pa, rowpart, colpart);
-  else
-    hipLaunchKernelGGL((k_sym_pass<NC, RWI, NSEG, false>), dim3(nitems), dim3(256), 0, st, d_items,
-                       pa, rowpart, colpart);
+  hipLaunchKernelGGL((k_sym_pass<NC, RWI, NSEG, true>), dim3(nitems), dim3(256), 0, st, d_items,
+                     pa, rowpart, colpart);
   return hipGetLastError();
 }
 

@@ -54,17 +54,18 @@ __device__ __forceinline__ void zero_unowned(double* __restrict__ base, int nv, 
 // denoiser_meta + der_denoiser_meta, src/sgvamp.py:93-114, per marker (:273,285)
 // ---------------------------------------------------------------------------
 // KM: cohort bound of the instantiation (registers: vr holds MPT x KM values);
-// partials [k] at stride K
+// partials [k] at stride K (+ 4 with the metrics: [K .. K + 3])
 template <int KM>
 __global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restrict__ chs,
                                                       DenoiseArgs a,
                                                       double* __restrict__ part) {
   const ChunkDesc ch = chs[blockIdx.x];
-  double acc[KM];
+  const bool met = a.x0 != nullptr;   // uniform
+  double acc[KM + 4];
 #pragma unroll
-  for (int k = 0; k < KM; ++k) acc[k] = 0.0;
+  for (int k = 0; k < KM + 4; ++k) acc[k] = 0.0;
   // loads of the thread's MPT markers first (see MPT), then the markers in order
-  double vr[MPT][KM], vxo[MPT];
+  double vr[MPT][KM], vxo[MPT], vx0[MPT];
 #pragma unroll
   for (int j = 0; j < MPT; ++j) {
     const int t = threadIdx.x + j * VTHREADS;
@@ -78,6 +79,7 @@ __global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restric
           if (k < a.K) vr[j][k] = a.r1[k][i];
       }
       if (a.damp && a.write_x) vxo[j] = a.xhat1[i];
+      if (met) vx0[j] = a.x0[i];
     }
   }
 #pragma unroll
@@ -132,6 +134,13 @@ __global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restric
       double x = Num / Den;
       if (a.damp) x = a.rho * x + (1 - a.rho) * vxo[j];   // :275-276
       a.xhat1[i] = x;
+      if (met) {   // k_metrics' sums of this marker, same order (:381-382)
+        const double b = vx0[j], d = x - b;
+        acc[KM + 0] += x * b;
+        acc[KM + 1] += x * x;
+        acc[KM + 2] += d * d;
+        acc[KM + 3] += b * b;
+      }
     }
     // der_denoiser_meta for every cohort k (:112-114 with a[k]*gam1s[k])
 #pragma unroll
@@ -152,7 +161,26 @@ __global__ __launch_bounds__(VTHREADS) void k_denoise(const ChunkDesc* __restric
         acc[k] += (DerNum * Den - DerDen * Num) / (Den * Den);
       }
   }
-  block_reduce_store<KM>(acc, part + (int64_t)blockIdx.x * a.K, a.K);
+  // the workgroup's sums as block_reduce_store (wave butterfly, waves in order):
+  // derivative sum k -> slot k, metric j -> slot K + j
+  {
+    __shared__ double sm[VTHREADS / WAVE][KM + 4];
+    const int lane = threadIdx.x & (WAVE - 1), wid = threadIdx.x / WAVE;
+#pragma unroll
+    for (int k = 0; k < KM + 4; ++k) {
+      if (k >= KM ? !met : k >= a.K) continue;   // uniform
+      const double s = wave_sum(acc[k]);
+      if (lane == 0) sm[wid][k] = s;
+    }
+    __syncthreads();
+    const int nv = a.K + (met ? 4 : 0);
+    double* out = part + (int64_t)blockIdx.x * nv;
+    const int t = threadIdx.x;
+    if (t < nv) {
+      const int k = t < a.K ? t : KM + (t - a.K);
+      out[t] = ((sm[0][k] + sm[1][k]) + sm[2][k]) + sm[3][k];
+    }
+  }
 }
 
 hipError_t launch_denoise(const ChunkDesc* d_ch, int nch, const DenoiseArgs& a, double* d_part,
@@ -1024,30 +1052,32 @@ hipError_t launch_pack(const ChunkDesc* d_ch, int nch, const int64_t* d_doff, co
 // ---------------------------------------------------------------------------
 // ordered reductions
 // ---------------------------------------------------------------------------
-// grid (nblk, nv), one wave: bsum[b * nv + v] = sum (op 0) or min (op 1) of parts
-// [begin[b], begin[b+1])
+// grid (nblk, nv), one wave: bsum[b * ostride + ooff + v] = sum (op 0) or min
+// (op 1) of parts [begin[b], begin[b+1])
 __global__ __launch_bounds__(WAVE) void k_reduce_blocks(const double* __restrict__ part, int nv,
                                                         const int* __restrict__ begin,
-                                                        double* __restrict__ bsum, int op) {
+                                                        double* __restrict__ bsum, int op,
+                                                        int ostride, int ooff) {
   const int b = blockIdx.x, v = blockIdx.y, lane = threadIdx.x;
   const int p0 = begin[b], p1 = begin[b + 1];
+  double* out = bsum + (int64_t)b * ostride + ooff + v;
   if (op == 0) {
     double s = 0.0;
     for (int p = p0 + lane; p < p1; p += WAVE) s += part[(int64_t)p * nv + v];
     s = wave_sum(s);
-    if (lane == 0) bsum[(int64_t)b * nv + v] = s;
+    if (lane == 0) *out = s;
   } else {
     double s = __builtin_inf();
     for (int p = p0 + lane; p < p1; p += WAVE) s = fmin(s, part[(int64_t)p * nv + v]);
     for (int o = 32; o > 0; o >>= 1) s = fmin(s, __shfl_xor(s, o, WAVE));
-    if (lane == 0) bsum[(int64_t)b * nv + v] = s;
+    if (lane == 0) *out = s;
   }
 }
 
 hipError_t launch_reduce_blocks(const double* d_part, int nv, const int* d_begin, int nblk,
-                                double* d_bsum, hipStream_t st, int op) {
+                                double* d_bsum, hipStream_t st, int op, int ostride, int ooff) {
   hipLaunchKernelGGL(k_reduce_blocks, dim3(nblk, nv), dim3(WAVE), 0, st, d_part, nv, d_begin,
-                     d_bsum, op);
+                     d_bsum, op, ostride > 0 ? ostride : nv, ooff);
   return hipGetLastError();
 }
 

@@ -90,6 +90,10 @@ class Engine:
                 uid = hb.unique_id() if self.rank == 0 else None
                 uid = self.comm.bcast(uid, root=0)
                 self.ctx.sgv_comm_init(self.nranks, self.rank, uid, hb.iptr(counts))
+            # this job's all-gather latency, the EM loop's cost-model parameter
+            # (the same on every rank; an SGV_XCHG_LAT_US setting is replaced)
+            if os.environ.get("SGV_XCHG_LAT_US") is None:
+                self.exchange_probe(10)
 
     # ---- inputs ----------------------------------------------------------
     def set_ld_block(self, ld, b_global, block):
@@ -365,13 +369,27 @@ class Engine:
 
     def exchange_stats(self, reset=False):
         """Cross-rank exchange counters (sgv_exchange_stats): all-gathers issued,
-        ms in them, bytes contributed, the EM loop mode and its threshold."""
-        t = np.zeros(6)
+        ms in them, bytes contributed, the EM loops' modes and the cost model's
+        last decision, the exact-CG host waits."""
+        t = np.zeros(14)
         self.ctx.sgv_exchange_stats(hb.dptr(t), int(bool(reset)))
         return dict(allgathers=int(t[0]), ms=float(t[1]), bytes=float(t[2]),
                     em_mode={1: "replicated", 0: "per-step", -1: None}[int(t[3])],
-                    em_rep_max_km=float(t[4]),
-                    transport={1: "rccl", 2: "host", 0: None}[int(t[5])])
+                    latency_us=float(t[4]),
+                    latency_source={0: "default", 1: "env SGV_XCHG_LAT_US",
+                                    2: "measured (sgv_exchange_probe)"}[int(t[12])],
+                    transport={1: "rccl", 2: "host", 0: None}[int(t[5])],
+                    em_loops_replicated=int(t[6]), em_loops_per_step=int(t[7]),
+                    em_pred_replicated_us=float(t[8]), em_pred_per_step_us=float(t[9]),
+                    em_pred_steps=float(t[10]), host_wait_ms=float(t[11]),
+                    em_replicated_possible=bool(t[13]))
+
+    def exchange_probe(self, reps=20):
+        """Measure the exchange's per-all-gather latency (collective) and make the
+        maximum over ranks the EM cost model's parameter; returns it in us."""
+        us = np.zeros(1)
+        self.ctx.sgv_exchange_probe(int(reps), hb.dptr(us))
+        return float(us[0])
 
     def set_ld_packing(self, packed):
         """True: symmetric blocks set/generated from now on are stored packed."""
