@@ -49,6 +49,7 @@ sys.path.insert(0, os.path.join(ROOT, "sgvamp-py_amd"))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E, MI355X_MICROARCH.md chip table
+F64_MFMA_PEAK_TFS = 78.6   # MI355X dense f64 matrix peak (AMD spec; not in the guide)
 
 
 def log(*a):
@@ -482,6 +483,9 @@ def main():
         cname = "C4 (BASELINE.json configs[3]) on %d GPU(s)" % world
     elif eng.M == 1000000 and K == 8 and args.ridge == 0.1 and args.lmmse_damp:
         cname = "C5 (BASELINE.json configs[4]) on %d GPU(s)" % world
+        if args.nsamp >= max(eng.block_sizes):   # full-rank LD blocks: the run converges
+            cname += (", N >= LD block size (full-rank blocks: a converging run, unlike the "
+                      "N = 10,000 C5 line)")
     else:
         cname = "custom"
     passes = sum(r["ld_passes"] for r in recs)
@@ -539,6 +543,22 @@ def main():
             "box_stream_GBs": box_bw,
             "frac_of_box_stream": (achieved / box_bw) if (achieved and box_bw) else None,
         },
+        # the 9..16-column passes (C5: 16 CG columns on one LD) are bound by the
+        # f64 matrix core (v_mfma_f64_16x16x4f64), not by HBM: their algorithmic
+        # flops (sgv_timers: 2 per multiply-add, row part of every stored element
+        # + transpose part of the off-diagonal-block ones) over their HIP-event
+        # time, against the dense f64 matrix peak (AMD's MI355X figure; the
+        # guide lists no f64 row)
+        "compute_roofline": ({
+            "bound": "mfma",
+            "achieved": tm["wide_flops"] / (tm["wide_ms"] / 1e3) / 1e12,
+            "peak": F64_MFMA_PEAK_TFS,
+            "unit": "TFLOP/s",
+            "frac": tm["wide_flops"] / (tm["wide_ms"] / 1e3) / 1e12 / F64_MFMA_PEAK_TFS,
+            "passes": tm["wide_launches"],
+            "avg_launch_ms": tm["wide_ms"] / tm["wide_launches"],
+            "hbm_frac_of_these_passes": None,
+        } if tm["wide_launches"] > 0 and tm["wide_ms"] > 0 else None),
         "exchange": {
             # cross-rank all-gathers of the timed steps (sgv_exchange_stats): the
             # ordered CG/EM reductions and r1 gathers that replace the reference's
@@ -562,8 +582,9 @@ def main():
                          "predicted_replicated_us": xs["em_pred_replicated_us"],
                          "predicted_per_step_us": xs["em_pred_per_step_us"],
                          "replicated_possible": xs["em_replicated_possible"]},
-            # exact CG column sets: host wall time waiting for a stop test before
-            # the passes could be enqueued (upper bound of the device bubble)
+            # exact CG column sets: the device's idle time between an iteration's
+            # p update and its passes, which the host enqueues after reading the
+            # stop test (HIP events; the slowest rank's)
             "host_wait_ms_per_step": max(x["host_wait_ms"] for x in xs_all) / steps,
             "K_times_M": K * eng.M,
         },

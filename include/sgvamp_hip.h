@@ -369,8 +369,13 @@ int sgv_cg_solve(sgv_ctx* ctx, int ld, int ncol, const double* c1, const double*
  * t[0] = kernel time (ms), t[1] = passes, t[2] = LD bytes read (the stored
  * bytes: n^2*8 dense, sum over panels H*(n - r0)*8 packed), t[3] = RHS bytes
  * (2 * ncol * M_local * 8), t[4] = dense-equivalent LD bytes (n^2*8),
- * t[5] = packed-pass partial-buffer bytes (written + read).  reset != 0 zeroes. */
-int sgv_timers(sgv_ctx* ctx, double* t6, int reset);
+ * t[5] = packed-pass partial-buffer bytes (written + read), t[6] = the passes'
+ * algorithmic flops (2 per multiply-add: each column's row part over every
+ * stored element, and its transpose part over the packed elements right of
+ * each panel's diagonal block), t[7] / t[8] / t[9] = flops / kernel ms / passes
+ * of the 9..16-column passes (f64 16x16x4 MFMA: their bound is the matrix core).
+ * reset != 0 zeroes. */
+int sgv_timers(sgv_ctx* ctx, double* t10, int reset);
 /* Cross-rank exchange counters since the last reset (the bcast/all-gather of
  * src/sgvamp.py:228-233 and the CG/EM scalar reductions that replace it):
  * out[0] = all-gathers issued, out[1] = ms spent in them (RCCL: HIP events
@@ -382,8 +387,9 @@ int sgv_timers(sgv_ctx* ctx, double* t6, int reset);
  * out[5] = 1 RCCL, 2 host exchange, 0 none, out[6] / out[7] = EM loops run
  * replicated / per step, out[8] / out[9] = the last decision's predicted cost
  * (us) of the replicated / per-step loop, out[10] = the steps it predicted,
- * out[11] = host ms spent waiting for exact-CG stop tests before enqueuing the
- * passes, out[12] = the latency's source (0 default 25 us, 1 env
+ * out[11] = ms the device idled between an exact-CG iteration's p update and
+ * its passes, which the host enqueues once it has read the stop test (HIP
+ * events), out[12] = the latency's source (0 default 25 us, 1 env
  * SGV_XCHG_LAT_US of rank 0, 2 sgv_exchange_probe), out[13] = 1 if the
  * replicated loop can run (K <= 32, <= 128 blocks in all).  reset != 0 zeroes
  * out[0..2], out[6..7] and out[11]. */

@@ -1,0 +1,367 @@
+// Packed band LD pass on the f64 matrix cores: workgroups WALK DOWN the band.
+//
+// A band block (windowed LD: src/main.py:199-200 .npz CSR, :251-257 PLINK .ld)
+// is stored as panels of 256 rows, panel g holding columns [256 g, 256 g + E)
+// (E = the band's stored extent, R = E / 256 column ranges).  The strip kernel
+// (sym_mfma.hip) cuts it into 512-column chunks over the panels of one parity,
+// which in a band meet only ~3 panels: per stored byte it writes and re-reads
+// 2.7x the row and column partials of a dense plan, and a finalize launch adds
+// them up (PMC: 1.097x the stored bytes at M = 1e6, bw = 1,000).
+//
+// Here one workgroup owns a WALK: W consecutive panels of one block, the whole
+// stored width of each.  Panel g's rows are complete after its own items (row
+// part) and the column parts of panels g - R + 1 .. g - 1 (the transposes of
+// their stored elements right of their diagonal blocks) -- all inside the walk
+// but for its first R - 1 panels.  So the walk keeps an LDS ring of R panel
+// accumulators acc[256][NC]: panel g's items add their row sums into slot g mod
+// R and their column sums into the slots of panels g + 1 .. g + R - 1; when
+// panel g is done, its slot is complete and the fused epilogue writes out =
+// c1 y + c2 in, R_s in, and the panel's partial dots -- no partial buffers, no
+// finalize.  Only the walk's first R - 1 panels ("head" panels, unless the walk
+// starts the block) lack the previous walk's column parts: they leave their
+// partial sums in headbuf, the previous walk leaves its open slots in carrybuf,
+// and k_walk_fin adds the two (then the coupling sums) and runs the epilogue.
+// The walk partition is a function of the block alone (capi.hip plan_walks),
+// so the summation order -- and every product -- is the same on 1 and N ranks.
+//
+// 8 waves per workgroup (one per CU: the ring takes R x 16 KiB of LDS), each
+// wave 64 columns of a 512-column item, sweeping its 16-row groups as the strip
+// kernel does (16 x 32 sub-tiles loaded once, 16 B per lane, nontemporal; the
+// row fragment through a per-wave XOR-swizzled LDS tile; v_mfma_f64_4x4x4f64).
+// Per row group the eight waves' row sums are added in wave order into the
+// panel's slot by one of them (wave gg mod 8), synchronised through LDS
+// counters instead of a barrier: a ring of WK_RD hand-off buffers lets a wave
+// run up to WK_RD - 1 row groups ahead of the slowest (bounded waits: every
+// wait is on a write or a combine another wave reaches without waiting on
+// this one).  One barrier per panel (its epilogue).
+//
+// Summation order of row i of panel g (fixed): the column parts of panels
+// g - R + 1, ..., g - 1 in panel order (in a head panel: those inside the walk,
+// then the carry of the earlier ones as one term), then the row parts of the
+// panel's items in item order (per item: the eight waves in order), then the
+// coupling sum of a cut between band pieces.
+#include "common.h"
+
+namespace sgv {
+
+#define MFMA4W(a, b, c) __builtin_amdgcn_mfma_f64_4x4x4f64((a), (b), (c), 0, 0, 0)
+
+constexpr int WK_NW = 8;          // waves per workgroup
+constexpr int WK_WC = 64;         // columns per wave of a 512-column item
+constexpr int WK_NT = WK_WC / 32; // 32-column steps per wave
+constexpr int WK_RD = 4;          // row-sum hand-off buffers (row groups in flight)
+
+__device__ __forceinline__ void wk_lds_order() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int NG>
+__global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
+    const SymWalk* __restrict__ walks, const SymPanel* __restrict__ panels,
+    const SymItem* __restrict__ items, const double* __restrict__ pk, int pks, PassArgs pa,
+    int ncol, double* __restrict__ headbuf, double* __restrict__ carrybuf,
+    double* __restrict__ partials) {
+  constexpr int RW = 4 * NG;                                   // accumulator row stride
+  __shared__ __attribute__((aligned(16))) double ring[WALK_RMAX][SYM_H * RW];
+  __shared__ __attribute__((aligned(16))) double red[WK_RD][WK_NW][16 * RW];
+  __shared__ int hready[WK_RD], hdone[WK_RD];   // writes into / combines of each buffer
+  __shared__ __attribute__((aligned(16))) double stg[WK_NW][16 * 32];
+  __shared__ double s_w[4][RW];
+  const SymWalk wk = walks[blockIdx.x];
+  if (pa.run && !ldg(pa.run)) return;   // no-op pass (pipelined CG past its stop test)
+  const int R = wk.R;
+  const int lane = threadIdx.x & (WAVE - 1);
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
+  const int lo = lane & 15, hi = lane >> 4, bq = (lane >> 2) & 3, n4 = lane & 3;
+  const int pc = hi + 4 * bq;                                  // column pair in a fragment
+  double* sb = stg[wid];
+  for (int e = threadIdx.x; e < R * SYM_H * RW; e += WK_NW * 64) (&ring[0][0])[e] = 0.0;
+  if (threadIdx.x < WK_RD) hready[threadIdx.x] = hdone[threadIdx.x] = 0;
+  __syncthreads();
+  auto lds_wait_ge = [](int* ctr, int v) {
+    while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v)
+      __builtin_amdgcn_s_sleep(1);
+  };
+
+  int gg = 0;                                                  // row groups done (red parity)
+#pragma unroll 1
+  for (int s = 0; s < wk.np; ++s) {
+    const SymPanel pn = panels[wk.p0 + s];
+    const int g = pn.g;
+    double* acc = ring[g % R];
+    const double* pkb = pk + (int64_t)pn.voff * pks;
+    const int ng = (pn.H + 15) / 16;
+#pragma unroll 1
+    for (int itx = pn.item_begin; itx < pn.item_end; ++itx) {
+      const SymItem it = items[itx];
+      const int crel = it.c0 - it.r0;                          // item's first column (panel-relative)
+      const int cw0 = crel + WK_WC * wid;                      // this wave's first column
+      // 32-column steps holding stored columns; the diagonal block (crel + col
+      // < H) feeds the row sums only
+      const int nta = min(WK_NT, max(0, (it.nc - WK_WC * wid + 31) / 32));
+      const bool colz = cw0 < SYM_H;                           // wave inside the diagonal block
+      const uint64_t b0 = (uint64_t)(it.P + crel);             // element (r0, c0)
+      double brow[WK_NT][2][NG];
+#pragma unroll
+      for (int t = 0; t < WK_NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int col = WK_WC * wid + 32 * t + 2 * pc + e;   // item-relative
+          const bool ok = col < it.nc;
+#pragma unroll
+          for (int q = 0; q < NG; ++q) {
+            const double v = ldg(pkb + (int64_t)(it.c0 + (ok ? col : 0)) * pks + 4 * q + n4);
+            brow[t][e][q] = ok ? v : 0.0;
+          }
+        }
+      double dcol[WK_NT][2][NG];
+#pragma unroll
+      for (int t = 0; t < WK_NT; ++t)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+#pragma unroll
+          for (int q = 0; q < NG; ++q) dcol[t][e][q] = 0.0;
+      // fragments of row group g2, step t (16 B per lane, branch-free: rows past
+      // H clamp -- their P is 0 -- and columns past the item load column 0)
+      auto load_cf = [&](int g2, int t, d2* cf) {
+        uint64_t bb = b0;
+        asm volatile("" : "+s"(bb));
+        const int xc = WK_WC * wid + 32 * t + 2 * lo;
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const int rB = 16 * g2 + 4 * a + hi;
+          const double* row = (const double*)bb + (int64_t)(rB < pn.H ? rB : pn.H - 1) * it.w;
+          cf[a] = ldg_nt((const d2*)(row + (xc < it.nc ? xc : 0)));
+        }
+      };
+      auto load_bcol = [&](int g2, double (*bc)[NG]) {
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const int rB = 16 * g2 + 4 * a + hi;
+#pragma unroll
+          for (int q = 0; q < NG; ++q) {
+            const double v = ldg(pkb + (int64_t)(pn.r0 + (rB < pn.H ? rB : 0)) * pks + 4 * q + n4);
+            bc[a][q] = (rB < pn.H && !colz) ? v : 0.0;
+          }
+        }
+      };
+      d2 cfn[WK_NT][4];
+      double bcn[4][NG];
+#pragma unroll
+      for (int t = 0; t < WK_NT; ++t) load_cf(0, t, cfn[t]);
+      load_bcol(0, bcn);
+#pragma unroll 1
+      for (int g2 = 0; g2 < ng; ++g2, ++gg) {
+        d2 cf[WK_NT][4];
+        double bcol[4][NG];
+#pragma unroll
+        for (int t = 0; t < WK_NT; ++t)
+#pragma unroll
+          for (int a = 0; a < 4; ++a) cf[t][a] = cfn[t][a];
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int q = 0; q < NG; ++q) bcol[a][q] = bcn[a][q];
+        // the next row group's loads go out before this one's LDS and MFMA work
+        // (past the last row group: the last one again, cache-resident)
+        const int gn = g2 + 1 < ng ? g2 + 1 : g2;
+#pragma unroll
+        for (int t = 0; t < WK_NT; ++t) load_cf(gn, t, cfn[t]);
+        load_bcol(gn, bcn);
+        double drow[4][NG];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < NG; ++q) drow[r][q] = 0.0;
+#pragma unroll
+        for (int t = 0; t < WK_NT; ++t) {
+          if (t >= nta) continue;                              // wave-uniform: past the item
+          // a step partly past the item's stored end: those columns read as 0
+          const int xc = WK_WC * wid + 32 * t + 2 * lo;
+#pragma unroll
+          for (int a = 0; a < 4; ++a) {
+            cf[t][a].x = xc < it.nc ? cf[t][a].x : 0.0;
+            cf[t][a].y = xc + 1 < it.nc ? cf[t][a].y : 0.0;
+          }
+          d2 rf[4];
+          wk_lds_order();
+#pragma unroll
+          for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[t][a];
+          wk_lds_order();
+#pragma unroll
+          for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
+          __builtin_amdgcn_s_setprio(1);
+          if (!colz) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a)
+#pragma unroll
+              for (int q = 0; q < NG; ++q) {
+                dcol[t][0][q] = MFMA4W(cf[t][a].x, bcol[a][q], dcol[t][0][q]);
+                dcol[t][1][q] = MFMA4W(cf[t][a].y, bcol[a][q], dcol[t][1][q]);
+              }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4W(rf[r].x, brow[t][0][q], drow[r][q]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4W(rf[r].y, brow[t][1][q], drow[r][q]);
+          __builtin_amdgcn_s_setprio(0);
+        }
+        // the row group's row sums: 4 blocks (DPP), handed to the combining wave
+        const int hs = gg % WK_RD, gen = gg / WK_RD;
+        lds_wait_ge(&hdone[hs], gen);                          // buffer hs free (gg - WK_RD combined)
+        double* rb = red[hs][wid];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int q = 0; q < NG; ++q) {
+            double v = drow[r][q];
+            v = v + row_ror<12>(v);
+            v = v + row_ror<8>(v);
+            if (bq == 0) rb[(4 * r + hi) * RW + 4 * q + n4] = v;   // D row 4r + m (m = hi)
+          }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0)
+          __hip_atomic_fetch_add(&hready[hs], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (wid == gg % WK_NW) {   // this wave combines row group gg: the 8 waves in order
+          lds_wait_ge(&hready[hs], WK_NW * (gen + 1));
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#pragma unroll
+          for (int k = 0; k < (16 * RW + WAVE - 1) / WAVE; ++k) {
+            const int e = lane + WAVE * k;
+            if (e < 16 * RW) {
+              const int row = e / RW, cc = e - row * RW;
+              const double* rr = &red[hs][0][0] + e;
+              double v = rr[0];
+#pragma unroll
+              for (int w = 1; w < WK_NW; ++w) v += rr[w * 16 * RW];
+              acc[(16 * g2 + row) * RW + cc] += v;
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          if (lane == 0)
+            __hip_atomic_store(&hdone[hs], gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+      // the item's column sums: this wave's columns of ranges g + 1 .. g + R - 1
+      if (!colz) {
+#pragma unroll
+        for (int t = 0; t < WK_NT; ++t) {
+          if (t >= nta) continue;
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int col = cw0 + 32 * t + 2 * pc + e;         // panel-relative
+            if (col - crel >= it.nc) continue;
+            double* dst = ring[(g + col / SYM_H) % R] + (col % SYM_H) * RW;
+#pragma unroll
+            for (int q = 0; q < NG; ++q) dst[4 * q + n4] += dcol[t][e][q];
+          }
+        }
+      }
+    }
+    __syncthreads();   // panel g's slot is complete (but for a head panel's carry)
+    if (threadIdx.x < SYM_H) {
+      const int t = threadIdx.x;
+      double* row = acc + t * RW;
+      if (s < wk.nhead) {   // partial: k_walk_fin adds the previous walk's carry
+        double* hb = headbuf + ((int64_t)(wk.hslot + s) * SYM_H + t) * ncol;
+        for (int c = 0; c < ncol; ++c) hb[c] = row[c];
+      } else {
+        const bool live = t < pn.H;
+        const int64_t idx = pn.voff + pn.r0 + (live ? t : 0);
+        const int w4 = t / WAVE;
+        for (int c = 0; c < ncol; ++c) {
+          double v = row[c];
+          if (pn.cp >= 0) v += pa.cpbuf[((int64_t)pn.cp * 256 + t) * ncol + c];   // coupled pieces
+          double a = 0.0;
+          if (live) {
+            const double in = pa.in[c][idx];
+            const double o = pa.c1[c] * v + pa.c2[c] * in;
+            pa.out[c][idx] = o;
+            if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * v + pa.ys0 * in;
+            if (pa.dot[c]) a = pa.dot[c][idx] * o;
+          }
+          const double sm = wave_sum(a);
+          if (lane == 0) s_w[w4][c] = sm;
+        }
+      }
+      for (int c = 0; c < RW; ++c) row[c] = 0.0;   // the slot's next panel: g + R
+    }
+    __syncthreads();
+    if (s >= wk.nhead && threadIdx.x < ncol) {
+      const int c = threadIdx.x;
+      partials[(int64_t)pn.part * ncol + c] = ((s_w[0][c] + s_w[1][c]) + s_w[2][c]) + s_w[3][c];
+    }
+  }
+  // the open slots: column parts of the next walk's head panels
+  if (threadIdx.x < SYM_H) {
+    const int t = threadIdx.x;
+    const int gend = panels[wk.p0 + wk.np - 1].g + 1;
+    for (int j = 0; j < wk.ncarry; ++j) {
+      const double* row = ring[(gend + j) % R] + t * RW;
+      double* cb = carrybuf + ((int64_t)(wk.cslot + j) * SYM_H + t) * ncol;
+      for (int c = 0; c < ncol; ++c) cb[c] = row[c];
+    }
+  }
+}
+
+// Head panels of the walks: y = the walk's partial + the previous walk's carry
+// (+ the coupling sum), then the epilogue and the panel's partial dots (wave
+// butterfly, waves 0..3 in order) -- as k_band_walk's own epilogue
+__global__ __launch_bounds__(256) void k_walk_fin(const WalkFin* __restrict__ fins,
+                                                  const SymPanel* __restrict__ panels, PassArgs pa,
+                                                  int ncol, const double* __restrict__ headbuf,
+                                                  const double* __restrict__ carrybuf,
+                                                  double* __restrict__ partials) {
+  __shared__ double s_w[4][MAXC];
+  const WalkFin f = fins[blockIdx.x];
+  if (pa.run && !ldg(pa.run)) return;
+  const SymPanel pn = panels[f.panel];
+  const int t = threadIdx.x, lane = t & (WAVE - 1), w4 = t / WAVE;
+  const bool live = t < pn.H;
+  const int64_t idx = pn.voff + pn.r0 + (live ? t : 0);
+  const double* hb = headbuf + ((int64_t)f.hslot * SYM_H + t) * ncol;
+  const double* cb = carrybuf + ((int64_t)f.cslot * SYM_H + t) * ncol;
+  for (int c = 0; c < ncol; ++c) {
+    double v = hb[c] + cb[c];
+    if (pn.cp >= 0) v += pa.cpbuf[((int64_t)pn.cp * 256 + t) * ncol + c];
+    double a = 0.0;
+    if (live) {
+      const double in = pa.in[c][idx];
+      const double o = pa.c1[c] * v + pa.c2[c] * in;
+      pa.out[c][idx] = o;
+      if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * v + pa.ys0 * in;
+      if (pa.dot[c]) a = pa.dot[c][idx] * o;
+    }
+    const double sm = wave_sum(a);
+    if (lane == 0) s_w[w4][c] = sm;
+  }
+  __syncthreads();
+  if (t < ncol) partials[(int64_t)pn.part * ncol + t] = ((s_w[0][t] + s_w[1][t]) + s_w[2][t]) + s_w[3][t];
+}
+
+hipError_t launch_band_walk(int nc, const SymWalk* d_walks, int nwalks, const SymPanel* d_panels,
+                            const SymItem* d_items, const double* d_pk, const PassArgs& pa,
+                            double* headbuf, double* carrybuf, const WalkFin* d_fins, int nfins,
+                            double* partials, hipStream_t st) {
+  if (nc < 1 || nc > 8) return hipErrorInvalidValue;
+  const int pks = nc <= 4 ? 4 : 8;
+  if (nwalks > 0) {
+    if (nc <= 4)
+      hipLaunchKernelGGL(k_band_walk<1>, dim3(nwalks), dim3(WK_NW * 64), 0, st, d_walks, d_panels,
+                         d_items, d_pk, pks, pa, nc, headbuf, carrybuf, partials);
+    else
+      hipLaunchKernelGGL(k_band_walk<2>, dim3(nwalks), dim3(WK_NW * 64), 0, st, d_walks, d_panels,
+                         d_items, d_pk, pks, pa, nc, headbuf, carrybuf, partials);
+  }
+  if (nfins > 0)
+    hipLaunchKernelGGL(k_walk_fin, dim3(nfins), dim3(256), 0, st, d_fins, d_panels, pa, nc,
+                       headbuf, carrybuf, partials);
+  return hipGetLastError();
+}
+
+}  // namespace sgv

@@ -116,6 +116,21 @@ struct SymStrip {
   int32_t it0, npan, slot, ncmax;
 };
 
+// band walks (band_walk.hip): a workgroup walks panels p0 .. p0 + np - 1 (one
+// block, consecutive; entries of the walk panel table) with a ring of R = the
+// block's stored extent / 256 panel accumulators.  The first nhead panels are
+// head panels (their partial sums -> headbuf slots hslot ..), the ring's ncarry
+// open slots at the end -> carrybuf slots cslot ..
+constexpr int WALK_RMAX = 5;   // ring slots of LDS (extent <= 1,280 columns)
+struct SymWalk {
+  int32_t p0, np, nhead, ncarry;
+  int32_t hslot, cslot, R, pad_;
+};
+// one head panel: walk panel table entry, its partial's slot, the carry slot
+struct WalkFin {
+  int32_t panel, hslot, cslot, pad_;
+};
+
 // element (i, j) of a packed block is stored iff j >= 256 * floor(i / 256)
 __device__ __forceinline__ double* sym_addr(double* base, const int64_t* poff, const int64_t* pw,
                                             int i, int j) {
@@ -337,6 +352,11 @@ hipError_t launch_pk(const PassArgs& pa, int nc, int64_t mpad, double* d_pk, hip
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                            const PassArgs& pa, const double* d_pk, double* rowpart,
                            double* colpart, bool ragged, int pair, hipStream_t st);
+// band walks (NC <= 8, band_walk.hip): the walks, then the head panels' finalize
+hipError_t launch_band_walk(int nc, const SymWalk* d_walks, int nwalks, const SymPanel* d_panels,
+                            const SymItem* d_items, const double* d_pk, const PassArgs& pa,
+                            double* headbuf, double* carrybuf, const WalkFin* d_fins, int nfins,
+                            double* partials, hipStream_t st);
 hipError_t launch_sym_finalize_strip(int nc, const SymPanel* d_panels, int npanels,
                                      const PassArgs& pa, const double* rowpart,
                                      const double* colpart, double* partials, bool ragged,

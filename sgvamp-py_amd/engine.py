@@ -362,10 +362,11 @@ class Engine:
         return X, it, info
 
     def timers(self, reset=False):
-        t = np.zeros(6)
+        t = np.zeros(10)
         self.ctx.sgv_timers(hb.dptr(t), int(bool(reset)))
         return dict(ld_ms=t[0], ld_launches=int(t[1]), ld_bytes=t[2], rhs_bytes=t[3],
-                    dense_bytes=t[4], aux_bytes=t[5])
+                    dense_bytes=t[4], aux_bytes=t[5], ld_flops=t[6], wide_flops=t[7],
+                    wide_ms=t[8], wide_launches=int(t[9]))
 
     def exchange_stats(self, reset=False):
         """Cross-rank exchange counters (sgv_exchange_stats): all-gathers issued,

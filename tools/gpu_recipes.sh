@@ -1,0 +1,59 @@
+#!/bin/bash
+# One driver for the GPU-box measurements (per-step limits: tools/gpu_steps.sh;
+# logs and profiler output under gpurun_out/).  Run through gpurun:
+#   /usr/local/graft/bin/gpurun -- 'bash tools/gpu_recipes.sh <recipe> <tag> [args]'
+# Recipes:
+#   suite   TAG [pytest paths]   the driver's GPU suite, smoke(), the default bench line
+#   trace   TAG [bench args]     kernel trace + --stats of a bench workload (trace_pass_summary.py)
+#   pmc     TAG [bench args]     FETCH_SIZE and WRITE_SIZE in separate --pmc passes (pmc_summary.py)
+#   clock   TAG [bench args]     effective clock, MFMA busy, SQ stall mix per dispatch (clock_summary.py)
+#   configs TAG                  one bench line per BASELINE.json configuration, the band line,
+#                                the N = 8 share and the 8-rank rehearsal
+#   ab      TAG VAR "v0 v1 .." SHAPES NCOLS [bench args]   an SGV_AB switch (gpu_ab_multi.sh)
+#   gate50  TAG [K]              the north star's own 50-iteration gate (SGV_FULL_GATE=1)
+cd "$(dirname "$0")/.." || exit 2
+R=$(pwd)
+export TMPDIR=/tmp
+recipe=$1; T=${2:-x}; shift 2
+B="--steps 5 --warmup 2 --cpu-baseline off --read-bw 0"
+case $recipe in
+  suite)
+    SEL=${*:-tests}
+    exec_steps=("gputests_$T:1000:python -u -m pytest $SEL -m gpu -x -q -p no:cacheprovider --timeout 600 --timeout-method thread -rs"
+                "smoke_$T:300:python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'"
+                "bench_$T:300:python bench.py")
+    tools/gpu_steps.sh "${exec_steps[@]}" ;;
+  trace)
+    tools/gpu_steps.sh "trace_$T:400:cd /tmp && rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$T -o bench --output-format csv -- python3 $R/bench.py $B $*" ;;
+  pmc)
+    tools/gpu_steps.sh \
+      "pmc_fetch_$T:300:cd /tmp && timeout -s KILL 280 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch_$T -o pmc --output-format csv -- python3 $R/bench.py $B --no-files $*" \
+      "pmc_write_$T:300:cd /tmp && timeout -s KILL 280 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write_$T -o pmc --output-format csv -- python3 $R/bench.py $B --no-files $*" ;;
+  clock)
+    P="GRBM_GUI_ACTIVE GRBM_COUNT SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"
+    tools/gpu_steps.sh "clock_$T:300:cd /tmp && timeout -s KILL 280 rocprofv3 --pmc $P -d $R/gpurun_out/clock_$T -o pmc --output-format csv -- python3 $R/bench.py $B --no-files $*" ;;
+  configs)
+    o=gpurun_out/cfg_$T
+    run() {   # name, timeout, args...
+      local name=$1 to=$2; shift 2
+      timeout -k 10 $to python -u bench.py "$@" > ${o}_$name.json 2> ${o}_$name.err || {
+        echo "$name FAILED"; tail -20 ${o}_$name.err; exit 1; }
+      python -c "import json; d=json.load(open('${o}_$name.json')); r=d['roofline']; c=d.get('compute_roofline'); print(json.dumps(dict(config='$name', value=round(d['value'],3), ms_per_step=round(d['ms_per_step'],3), ms_pass=round(r['avg_launch_ms'],4), frac=round(r['frac'],4), passes=round(d['ld_passes_per_step'],2), stream=r.get('box_stream_GBs'), mfma_frac=(round(c['frac'],4) if c else None), xchg=d['exchange']['allgathers_per_step'])))" | tee -a ${o}.jsonl
+    }
+    Q="--cpu-baseline off --read-bw 0"
+    run ns 600 --cpu-baseline off
+    run c2 400 --blocks 8 --block-size 25000 --K 1 $Q
+    run c3 400 --blocks 8 --block-size 25000 --K 4 $Q
+    run c4 400 --K 1 $Q
+    run c5 400 --K 8 --ridge 0.1 --lmmse-damp 1 --steps 3 --warmup 1 $Q
+    run c5conv 500 --K 8 --ridge 0.1 --lmmse-damp 1 --nsamp 20000 --steps 5 --warmup 2 $Q
+    run band 400 --band 1000000,1000 --steps 10 --warmup 2 --no-files $Q
+    run ns8blk 400 --blocks 8 --block-size 15625 --K 4 $Q
+    run share8 600 --gpus 8 --share-device --steps 3 --warmup 1 $Q ;;
+  ab)
+    bash tools/gpu_ab_multi.sh gpurun_out/ab_$T "$@" ;;
+  gate50)
+    tools/gpu_steps.sh "gate50_$T:2400:SGV_FULL_GATE=1 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -q -s -p no:cacheprovider -k 'north_star_50 and ${1:-4}' --timeout 2300" ;;
+  *)
+    echo "unknown recipe $recipe"; exit 2 ;;
+esac
