@@ -378,7 +378,7 @@ def launch_from_env(environ=None):
         # launches that set no LOCAL_WORLD_SIZE -- the ranks meet on this host
         one_node = (local_size == size or size == 1 or
                     (source == "env" and local_size is None and
-                     env.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost", "::1")))
+                     _is_local_addr(env.get("MASTER_ADDR", "127.0.0.1"))))
         local_rank = rank if one_node else None
     if local_rank is None:
         raise RuntimeError("launcher environment (%s) gives no node-local rank: set LOCAL_RANK "
@@ -402,6 +402,25 @@ def launch_from_env(environ=None):
     token = env.get("SGV_COMM_TOKEN") or ("%s|%s" % (source, job) if job else None)
     return dict(rank=int(rank), size=int(size), local_rank=int(local_rank),
                 local_size=local_size, addr=addr, port=int(port), token=token, source=source)
+
+
+def _is_local_addr(addr):
+    """True if `addr` (a name or a literal) is this host: a loopback name, or an
+    address some local interface holds (a socket can be bound to it)."""
+    if addr in ("127.0.0.1", "localhost", "::1"):
+        return True
+    try:
+        infos = socket.getaddrinfo(addr, None)
+    except OSError:
+        return False
+    for fam, _, _, _, sa in infos:
+        try:
+            with socket.socket(fam, socket.SOCK_DGRAM) as s:
+                s.bind((sa[0], 0))
+            return True
+        except OSError:
+            continue
+    return False
 
 
 def world_from_env(environ=None):

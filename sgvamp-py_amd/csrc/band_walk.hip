@@ -56,6 +56,67 @@ __device__ __forceinline__ void wk_lds_order() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// A workgroup barrier over LDS only: the wave's DS operations complete
+// (lgkmcnt(0)), then s_barrier -- without the vmcnt(0) of __syncthreads, which
+// would drain the prefetched HBM fragments at every barrier.  The wavefront-
+// scope fences only keep the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void wk_lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_s_waitcnt(0xC07F);   // gfx9 encoding: lgkmcnt(0), vmcnt / expcnt at max
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// the fused epilogue of one panel (the walk's, or k_walk_fin's for a head
+// panel): y = acc (+ the coupling sum), out = c1 y + c2 in, R_s in, and the
+// panel's partial dots -- the 64-row wave butterflies added in row-quarter
+// order.  `nthr` threads: thread t takes row t & 255 and, with 512 threads,
+// half (t >> 8) of the columns; every load of a thread is issued before its
+// first store.
+template <int RW, int NH>
+__device__ __forceinline__ void walk_epilogue(const SymPanel& pn, const PassArgs& pa, int ncol,
+                                              const double* __restrict__ yrow, double* s_w) {
+  constexpr int CPT = RW / NH;   // columns per thread
+  const int t = threadIdx.x & 255, h = threadIdx.x >> 8;
+  const int lane = threadIdx.x & (WAVE - 1), q4 = t / WAVE;
+  const bool live = t < pn.H;
+  const int64_t idx = pn.voff + pn.r0 + (live ? t : 0);
+  double y[CPT], in[CPT], dt[CPT], cp[CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const int c = h * CPT + j;
+    y[j] = yrow[j];
+    in[j] = dt[j] = cp[j] = 0.0;
+    if (c < ncol) {
+      in[j] = pa.in[c][idx];
+      if (pa.dot[c]) dt[j] = pa.dot[c][idx];
+      if (pn.cp >= 0) cp[j] = pa.cpbuf[((int64_t)pn.cp * 256 + t) * ncol + c];   // coupled pieces
+    }
+  }
+  double a[CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const int c = h * CPT + j;
+    a[j] = 0.0;
+    if (c < ncol) {
+      double v = y[j];
+      if (pn.cp >= 0) v += cp[j];
+      if (live) {
+        const double o = pa.c1[c] * v + pa.c2[c] * in[j];
+        pa.out[c][idx] = o;
+        if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * v + pa.ys0 * in[j];
+        if (pa.dot[c]) a[j] = dt[j] * o;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const int c = h * CPT + j;
+    const double sm = wave_sum(a[j]);
+    if (lane == 0 && c < ncol) s_w[q4 * RW + c] = sm;
+  }
+}
+
 template <int NG>
 __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
     const SymWalk* __restrict__ walks, const SymPanel* __restrict__ panels,
@@ -63,11 +124,12 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
     int ncol, double* __restrict__ headbuf, double* __restrict__ carrybuf,
     double* __restrict__ partials) {
   constexpr int RW = 4 * NG;                                   // accumulator row stride
+  constexpr int CPT = RW / 2;                                  // epilogue columns per thread
   __shared__ __attribute__((aligned(16))) double ring[WALK_RMAX][SYM_H * RW];
   __shared__ __attribute__((aligned(16))) double red[WK_RD][WK_NW][16 * RW];
   __shared__ int hready[WK_RD], hdone[WK_RD];   // writes into / combines of each buffer
   __shared__ __attribute__((aligned(16))) double stg[WK_NW][16 * 32];
-  __shared__ double s_w[4][RW];
+  __shared__ double s_w[4 * RW];
   const SymWalk wk = walks[blockIdx.x];
   if (pa.run && !ldg(pa.run)) return;   // no-op pass (pipelined CG past its stop test)
   const int R = wk.R;
@@ -80,41 +142,112 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
   if (threadIdx.x < WK_RD) hready[threadIdx.x] = hdone[threadIdx.x] = 0;
   __syncthreads();
   auto lds_wait_ge = [](int* ctr, int v) {
-    while (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < v)
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v)
       __builtin_amdgcn_s_sleep(1);
   };
 
-  int gg = 0;                                                  // row groups done (red parity)
+  // an item of the walk as this wave sees it
+  struct Cur {
+    uint64_t b0;        // element (r0, c0)
+    int64_t w;          // row stride
+    const double* pkb;  // Pk of the block
+    int nc, c0, r0, H;
+    bool colz;          // this wave's columns lie in the diagonal block
+  };
+  auto make = [&](const SymItem& it, const SymPanel& p) {
+    Cur u;
+    const int crel = it.c0 - it.r0;
+    u.b0 = (uint64_t)(it.P + crel);
+    u.w = it.w;
+    u.pkb = pk + (int64_t)p.voff * pks;
+    u.nc = it.nc;
+    u.c0 = it.c0;
+    u.r0 = p.r0;
+    u.H = p.H;
+    u.colz = crel + WK_WC * wid < SYM_H;
+    return u;
+  };
+  // fragments of row group g2, step t (16 B per lane, branch-free: rows past
+  // H clamp -- their P is 0 -- and columns past the item load column 0)
+  auto load_cf = [&](const Cur& u, int g2, int t, d2* cf) {
+    uint64_t bb = u.b0;
+    asm volatile("" : "+s"(bb));
+    const int xc = WK_WC * wid + 32 * t + 2 * lo;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int rB = 16 * g2 + 4 * a + hi;
+      const double* row = (const double*)bb + (int64_t)(rB < u.H ? rB : u.H - 1) * u.w;
+      cf[a] = ldg_nt((const d2*)(row + (xc < u.nc ? xc : 0)));
+    }
+  };
+  // P operands are loaded raw (clamped addresses) and masked when they are
+  // used: a select right behind its load would make the compiler wait for each
+  // load in turn.  The masks: bit a (bcol: row valid, not the diagonal block),
+  // bit 2 t + e (brow: column inside the item)
+  auto load_bcol = [&](const Cur& u, int g2, double (*bc)[NG]) {
+    int m = 0;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int rB = 16 * g2 + 4 * a + hi;
+      m |= (rB < u.H && !u.colz) ? 1 << a : 0;
+#pragma unroll
+      for (int q = 0; q < NG; ++q)
+        bc[a][q] = ldg(u.pkb + (int64_t)(u.r0 + (rB < u.H ? rB : 0)) * pks + 4 * q + n4);
+    }
+    return m;
+  };
+  auto load_brow = [&](const Cur& u, double (*br)[2][NG]) {
+    int m = 0;
+#pragma unroll
+    for (int t = 0; t < WK_NT; ++t)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int col = WK_WC * wid + 32 * t + 2 * pc + e;     // item-relative
+        const bool ok = col < u.nc;
+        m |= ok ? 1 << (2 * t + e) : 0;
+#pragma unroll
+        for (int q = 0; q < NG; ++q)
+          br[t][e][q] = ldg(u.pkb + (int64_t)(u.c0 + (ok ? col : 0)) * pks + 4 * q + n4);
+      }
+    return m;
+  };
+
+  // the walk's first item: its first row group and P operands in flight
+  SymPanel pn = panels[wk.p0];
+  Cur cu = make(items[pn.item_begin], pn);
+  d2 cfn[WK_NT][4];
+  double bcn[4][NG], brn[WK_NT][2][NG];
+#pragma unroll
+  for (int t = 0; t < WK_NT; ++t) load_cf(cu, 0, t, cfn[t]);
+  int bcm = load_bcol(cu, 0, bcn);
+  int brm = load_brow(cu, brn);
+
+  int gg = 0;                                                  // row groups done
 #pragma unroll 1
   for (int s = 0; s < wk.np; ++s) {
-    const SymPanel pn = panels[wk.p0 + s];
     const int g = pn.g;
     double* acc = ring[g % R];
-    const double* pkb = pk + (int64_t)pn.voff * pks;
     const int ng = (pn.H + 15) / 16;
+    const bool more_panels = s + 1 < wk.np;
+    const SymPanel pnx = panels[wk.p0 + (more_panels ? s + 1 : s)];
 #pragma unroll 1
     for (int itx = pn.item_begin; itx < pn.item_end; ++itx) {
-      const SymItem it = items[itx];
-      const int crel = it.c0 - it.r0;                          // item's first column (panel-relative)
+      // the next item of the walk (this panel's, or the next panel's first)
+      const bool nx_here = itx + 1 < pn.item_end;
+      const bool has_nx = nx_here || more_panels;
+      const Cur cn = has_nx ? make(items[nx_here ? itx + 1 : pnx.item_begin], nx_here ? pn : pnx) : cu;
+      const int crel = cu.c0 - pn.r0;                          // item's first column (panel-relative)
       const int cw0 = crel + WK_WC * wid;                      // this wave's first column
-      // 32-column steps holding stored columns; the diagonal block (crel + col
-      // < H) feeds the row sums only
-      const int nta = min(WK_NT, max(0, (it.nc - WK_WC * wid + 31) / 32));
-      const bool colz = cw0 < SYM_H;                           // wave inside the diagonal block
-      const uint64_t b0 = (uint64_t)(it.P + crel);             // element (r0, c0)
+      // 32-column steps holding stored columns; the diagonal block feeds the row sums only
+      const int nta = min(WK_NT, max(0, (cu.nc - WK_WC * wid + 31) / 32));
+      const bool colz = cu.colz;
       double brow[WK_NT][2][NG];
 #pragma unroll
       for (int t = 0; t < WK_NT; ++t)
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int col = WK_WC * wid + 32 * t + 2 * pc + e;   // item-relative
-          const bool ok = col < it.nc;
+        for (int e = 0; e < 2; ++e)
 #pragma unroll
-          for (int q = 0; q < NG; ++q) {
-            const double v = ldg(pkb + (int64_t)(it.c0 + (ok ? col : 0)) * pks + 4 * q + n4);
-            brow[t][e][q] = ok ? v : 0.0;
-          }
-        }
+          for (int q = 0; q < NG; ++q) brow[t][e][q] = (brm >> (2 * t + e) & 1) ? brn[t][e][q] : 0.0;
       double dcol[WK_NT][2][NG];
 #pragma unroll
       for (int t = 0; t < WK_NT; ++t)
@@ -122,53 +255,29 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
         for (int e = 0; e < 2; ++e)
 #pragma unroll
           for (int q = 0; q < NG; ++q) dcol[t][e][q] = 0.0;
-      // fragments of row group g2, step t (16 B per lane, branch-free: rows past
-      // H clamp -- their P is 0 -- and columns past the item load column 0)
-      auto load_cf = [&](int g2, int t, d2* cf) {
-        uint64_t bb = b0;
-        asm volatile("" : "+s"(bb));
-        const int xc = WK_WC * wid + 32 * t + 2 * lo;
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          const int rB = 16 * g2 + 4 * a + hi;
-          const double* row = (const double*)bb + (int64_t)(rB < pn.H ? rB : pn.H - 1) * it.w;
-          cf[a] = ldg_nt((const d2*)(row + (xc < it.nc ? xc : 0)));
-        }
-      };
-      auto load_bcol = [&](int g2, double (*bc)[NG]) {
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          const int rB = 16 * g2 + 4 * a + hi;
-#pragma unroll
-          for (int q = 0; q < NG; ++q) {
-            const double v = ldg(pkb + (int64_t)(pn.r0 + (rB < pn.H ? rB : 0)) * pks + 4 * q + n4);
-            bc[a][q] = (rB < pn.H && !colz) ? v : 0.0;
-          }
-        }
-      };
-      d2 cfn[WK_NT][4];
-      double bcn[4][NG];
-#pragma unroll
-      for (int t = 0; t < WK_NT; ++t) load_cf(0, t, cfn[t]);
-      load_bcol(0, bcn);
 #pragma unroll 1
       for (int g2 = 0; g2 < ng; ++g2, ++gg) {
-        d2 cf[WK_NT][4];
         double bcol[4][NG];
-#pragma unroll
-        for (int t = 0; t < WK_NT; ++t)
-#pragma unroll
-          for (int a = 0; a < 4; ++a) cf[t][a] = cfn[t][a];
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
-          for (int q = 0; q < NG; ++q) bcol[a][q] = bcn[a][q];
-        // the next row group's loads go out before this one's LDS and MFMA work
-        // (past the last row group: the last one again, cache-resident)
-        const int gn = g2 + 1 < ng ? g2 + 1 : g2;
-#pragma unroll
-        for (int t = 0; t < WK_NT; ++t) load_cf(gn, t, cfn[t]);
-        load_bcol(gn, bcn);
+          for (int q = 0; q < NG; ++q) bcol[a][q] = (bcm >> a & 1) ? bcn[a][q] : 0.0;
+        // where the next row group's loads come from: this item's next, or the
+        // next item's first (then also its row operands).  Branch-free, the same
+        // loads on every path (a branch join with different load counts makes
+        // the compiler drain every load in flight): the row operands are re-read
+        // for the current item until its last row group (cache hits)
+        const bool last = g2 + 1 >= ng;
+        Cur src;
+        src.b0 = last ? cn.b0 : cu.b0;
+        src.w = last ? cn.w : cu.w;
+        src.pkb = last ? cn.pkb : cu.pkb;
+        src.nc = last ? cn.nc : cu.nc;
+        src.c0 = last ? cn.c0 : cu.c0;
+        src.r0 = last ? cn.r0 : cu.r0;
+        src.H = last ? cn.H : cu.H;
+        src.colz = last ? cn.colz : cu.colz;
+        const int gn = last ? 0 : g2 + 1;
         double drow[4][NG];
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -176,40 +285,52 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
           for (int q = 0; q < NG; ++q) drow[r][q] = 0.0;
 #pragma unroll
         for (int t = 0; t < WK_NT; ++t) {
-          if (t >= nta) continue;                              // wave-uniform: past the item
-          // a step partly past the item's stored end: those columns read as 0
-          const int xc = WK_WC * wid + 32 * t + 2 * lo;
+          // a ring of one row group per wave: step t's fragments came in with
+          // the previous row group's step t and are used in place; the same step
+          // of the next row group goes into their registers right after, so two
+          // steps of loads stay in flight (no copy: a loop-carried copy of
+          // loaded registers makes the compiler wait for the loads at the back edge)
+          d2* cf = cfn[t];
+          if (t < nta) {                                       // wave-uniform: inside the item
+            // a step partly past the item's stored end: those columns read as 0
+            const int xc = WK_WC * wid + 32 * t + 2 * lo;
 #pragma unroll
-          for (int a = 0; a < 4; ++a) {
-            cf[t][a].x = xc < it.nc ? cf[t][a].x : 0.0;
-            cf[t][a].y = xc + 1 < it.nc ? cf[t][a].y : 0.0;
+            for (int a = 0; a < 4; ++a) {
+              cf[a].x = xc < cu.nc ? cf[a].x : 0.0;
+              cf[a].y = xc + 1 < cu.nc ? cf[a].y : 0.0;
+            }
+            d2 rf[4];
+            wk_lds_order();
+#pragma unroll
+            for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[a];
+            wk_lds_order();
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
+            __builtin_amdgcn_s_setprio(1);
+            if (!colz) {
+#pragma unroll
+              for (int a = 0; a < 4; ++a)
+#pragma unroll
+                for (int q = 0; q < NG; ++q) {
+                  dcol[t][0][q] = MFMA4W(cf[a].x, bcol[a][q], dcol[t][0][q]);
+                  dcol[t][1][q] = MFMA4W(cf[a].y, bcol[a][q], dcol[t][1][q]);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4W(rf[r].x, brow[t][0][q], drow[r][q]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4W(rf[r].y, brow[t][1][q], drow[r][q]);
+            __builtin_amdgcn_s_setprio(0);
           }
-          d2 rf[4];
-          wk_lds_order();
-#pragma unroll
-          for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[t][a];
-          wk_lds_order();
-#pragma unroll
-          for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
-          __builtin_amdgcn_s_setprio(1);
-          if (!colz) {
-#pragma unroll
-            for (int a = 0; a < 4; ++a)
-#pragma unroll
-              for (int q = 0; q < NG; ++q) {
-                dcol[t][0][q] = MFMA4W(cf[t][a].x, bcol[a][q], dcol[t][0][q]);
-                dcol[t][1][q] = MFMA4W(cf[t][a].y, bcol[a][q], dcol[t][1][q]);
-              }
+          load_cf(src, gn, t, cfn[t]);
+          if (t == 0) {
+            bcm = load_bcol(src, gn, bcn);
+            brm = load_brow(src, brn);
           }
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4W(rf[r].x, brow[t][0][q], drow[r][q]);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4W(rf[r].y, brow[t][1][q], drow[r][q]);
-          __builtin_amdgcn_s_setprio(0);
         }
         // the row group's row sums: 4 blocks (DPP), handed to the combining wave
         const int hs = gg % WK_RD, gen = gg / WK_RD;
@@ -224,12 +345,15 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
             v = v + row_ror<8>(v);
             if (bq == 0) rb[(4 * r + hi) * RW + 4 * q + n4] = v;   // D row 4r + m (m = hi)
           }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        // LDS executes a wave's DS operations in order, so the counter's add
+        // lands after the row sums; the wavefront-scope fences keep the
+        // compiler's order and wait for nothing (the fragments stay in flight)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         if (lane == 0)
           __hip_atomic_fetch_add(&hready[hs], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (wid == gg % WK_NW) {   // this wave combines row group gg: the 8 waves in order
           lds_wait_ge(&hready[hs], WK_NW * (gen + 1));
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
           for (int k = 0; k < (16 * RW + WAVE - 1) / WAVE; ++k) {
             const int e = lane + WAVE * k;
@@ -242,7 +366,7 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
               acc[(16 * g2 + row) * RW + cc] += v;
             }
           }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           if (lane == 0)
             __hip_atomic_store(&hdone[hs], gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -255,93 +379,76 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             const int col = cw0 + 32 * t + 2 * pc + e;         // panel-relative
-            if (col - crel >= it.nc) continue;
+            if (col - crel >= cu.nc) continue;
             double* dst = ring[(g + col / SYM_H) % R] + (col % SYM_H) * RW;
 #pragma unroll
             for (int q = 0; q < NG; ++q) dst[4 * q + n4] += dcol[t][e][q];
           }
         }
       }
+      cu = cn;
     }
-    __syncthreads();   // panel g's slot is complete (but for a head panel's carry)
-    if (threadIdx.x < SYM_H) {
-      const int t = threadIdx.x;
-      double* row = acc + t * RW;
+    wk_lds_barrier();   // panel g's slot is complete (but for a head panel's carry)
+    {
+      const int t = threadIdx.x & 255, h = threadIdx.x >> 8;
+      double* row = acc + t * RW + h * CPT;
       if (s < wk.nhead) {   // partial: k_walk_fin adds the previous walk's carry
-        double* hb = headbuf + ((int64_t)(wk.hslot + s) * SYM_H + t) * ncol;
-        for (int c = 0; c < ncol; ++c) hb[c] = row[c];
+        double* hb = headbuf + ((int64_t)(wk.hslot + s) * SYM_H + t) * ncol + h * CPT;
+#pragma unroll
+        for (int j = 0; j < CPT; ++j)
+          if (h * CPT + j < ncol) hb[j] = row[j];
       } else {
-        const bool live = t < pn.H;
-        const int64_t idx = pn.voff + pn.r0 + (live ? t : 0);
-        const int w4 = t / WAVE;
-        for (int c = 0; c < ncol; ++c) {
-          double v = row[c];
-          if (pn.cp >= 0) v += pa.cpbuf[((int64_t)pn.cp * 256 + t) * ncol + c];   // coupled pieces
-          double a = 0.0;
-          if (live) {
-            const double in = pa.in[c][idx];
-            const double o = pa.c1[c] * v + pa.c2[c] * in;
-            pa.out[c][idx] = o;
-            if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * v + pa.ys0 * in;
-            if (pa.dot[c]) a = pa.dot[c][idx] * o;
-          }
-          const double sm = wave_sum(a);
-          if (lane == 0) s_w[w4][c] = sm;
-        }
+        walk_epilogue<RW, 2>(pn, pa, ncol, row, s_w);
       }
-      for (int c = 0; c < RW; ++c) row[c] = 0.0;   // the slot's next panel: g + R
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) row[j] = 0.0;             // the slot's next panel: g + R
     }
-    __syncthreads();
+    wk_lds_barrier();
     if (s >= wk.nhead && threadIdx.x < ncol) {
       const int c = threadIdx.x;
-      partials[(int64_t)pn.part * ncol + c] = ((s_w[0][c] + s_w[1][c]) + s_w[2][c]) + s_w[3][c];
+      partials[(int64_t)pn.part * ncol + c] =
+          ((s_w[0 * RW + c] + s_w[1 * RW + c]) + s_w[2 * RW + c]) + s_w[3 * RW + c];
     }
+    pn = pnx;
   }
   // the open slots: column parts of the next walk's head panels
-  if (threadIdx.x < SYM_H) {
-    const int t = threadIdx.x;
+  {
+    const int t = threadIdx.x & 255, h = threadIdx.x >> 8;
     const int gend = panels[wk.p0 + wk.np - 1].g + 1;
     for (int j = 0; j < wk.ncarry; ++j) {
-      const double* row = ring[(gend + j) % R] + t * RW;
-      double* cb = carrybuf + ((int64_t)(wk.cslot + j) * SYM_H + t) * ncol;
-      for (int c = 0; c < ncol; ++c) cb[c] = row[c];
+      const double* row = ring[(gend + j) % R] + t * RW + h * CPT;
+      double* cb = carrybuf + ((int64_t)(wk.cslot + j) * SYM_H + t) * ncol + h * CPT;
+#pragma unroll
+      for (int i = 0; i < CPT; ++i)
+        if (h * CPT + i < ncol) cb[i] = row[i];
     }
   }
 }
 
 // Head panels of the walks: y = the walk's partial + the previous walk's carry
-// (+ the coupling sum), then the epilogue and the panel's partial dots (wave
-// butterfly, waves 0..3 in order) -- as k_band_walk's own epilogue
+// (+ the coupling sum), then the epilogue and the panel's partial dots -- as
+// k_band_walk's own epilogue
+template <int RW>
 __global__ __launch_bounds__(256) void k_walk_fin(const WalkFin* __restrict__ fins,
                                                   const SymPanel* __restrict__ panels, PassArgs pa,
                                                   int ncol, const double* __restrict__ headbuf,
                                                   const double* __restrict__ carrybuf,
                                                   double* __restrict__ partials) {
-  __shared__ double s_w[4][MAXC];
+  __shared__ double s_w[4 * RW];
   const WalkFin f = fins[blockIdx.x];
   if (pa.run && !ldg(pa.run)) return;
   const SymPanel pn = panels[f.panel];
-  const int t = threadIdx.x, lane = t & (WAVE - 1), w4 = t / WAVE;
-  const bool live = t < pn.H;
-  const int64_t idx = pn.voff + pn.r0 + (live ? t : 0);
+  const int t = threadIdx.x;
   const double* hb = headbuf + ((int64_t)f.hslot * SYM_H + t) * ncol;
   const double* cb = carrybuf + ((int64_t)f.cslot * SYM_H + t) * ncol;
-  for (int c = 0; c < ncol; ++c) {
-    double v = hb[c] + cb[c];
-    if (pn.cp >= 0) v += pa.cpbuf[((int64_t)pn.cp * 256 + t) * ncol + c];
-    double a = 0.0;
-    if (live) {
-      const double in = pa.in[c][idx];
-      const double o = pa.c1[c] * v + pa.c2[c] * in;
-      pa.out[c][idx] = o;
-      if (pa.yout[c]) pa.yout[c][idx] = pa.ys1 * v + pa.ys0 * in;
-      if (pa.dot[c]) a = pa.dot[c][idx] * o;
-    }
-    const double sm = wave_sum(a);
-    if (lane == 0) s_w[w4][c] = sm;
-  }
+  double y[RW];
+#pragma unroll
+  for (int c = 0; c < RW; ++c) y[c] = c < ncol ? hb[c] + cb[c] : 0.0;
+  walk_epilogue<RW, 1>(pn, pa, ncol, y, s_w);
   __syncthreads();
-  if (t < ncol) partials[(int64_t)pn.part * ncol + t] = ((s_w[0][t] + s_w[1][t]) + s_w[2][t]) + s_w[3][t];
+  if (t < ncol)
+    partials[(int64_t)pn.part * ncol + t] =
+        ((s_w[0 * RW + t] + s_w[1 * RW + t]) + s_w[2 * RW + t]) + s_w[3 * RW + t];
 }
 
 hipError_t launch_band_walk(int nc, const SymWalk* d_walks, int nwalks, const SymPanel* d_panels,
@@ -358,9 +465,14 @@ hipError_t launch_band_walk(int nc, const SymWalk* d_walks, int nwalks, const Sy
       hipLaunchKernelGGL(k_band_walk<2>, dim3(nwalks), dim3(WK_NW * 64), 0, st, d_walks, d_panels,
                          d_items, d_pk, pks, pa, nc, headbuf, carrybuf, partials);
   }
-  if (nfins > 0)
-    hipLaunchKernelGGL(k_walk_fin, dim3(nfins), dim3(256), 0, st, d_fins, d_panels, pa, nc,
-                       headbuf, carrybuf, partials);
+  if (nfins > 0) {
+    if (nc <= 4)
+      hipLaunchKernelGGL(k_walk_fin<4>, dim3(nfins), dim3(256), 0, st, d_fins, d_panels, pa, nc,
+                         headbuf, carrybuf, partials);
+    else
+      hipLaunchKernelGGL(k_walk_fin<8>, dim3(nfins), dim3(256), 0, st, d_fins, d_panels, pa, nc,
+                         headbuf, carrybuf, partials);
+  }
   return hipGetLastError();
 }
 

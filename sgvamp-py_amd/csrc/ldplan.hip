@@ -313,12 +313,21 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
 // summation order is the same for every rank count; W >= R - 1 keeps every
 // column part inside the walk or the one before it.  A walk that does not start
 // its block has min(R - 1, np) head panels; one that does not end it leaves
-// min(R - 1, panels after it) carry slots.  SGV_BAND_WALK=0 (with SGV_AB=1):
-// the strip kernels for every band plan.
+// min(R - 1, panels after it) carry slots.
+// The walks run the passes of up to 4 columns (one 4x4x4 column group): 1-3 %
+// faster than the strips at M = 1e6, bw = 1,000 (3 / 4 columns: 1.82 / 1.86
+// vs 1.87 / 1.92 ms); at 5-8 columns they are 14 % slower (2.43 vs 2.14 ms,
+// profiles/r05/walk_v5_ab.jsonl), so those stay on the strips.
+// SGV_BAND_WALK (with SGV_AB=1): 0 = the strips for every band pass, 8 = walks
+// up to 8 columns (A/B).
+static int band_walk_max_nc() {
+  const char* e = ab_env("SGV_BAND_WALK");
+  return e ? (e[0] == '0' ? 0 : e[0] == '8' ? 8 : 4) : 4;
+}
+
 static int plan_walks(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
                       const std::vector<SymPanel>& panels, LdPlan* pl) {
-  const char* e = ab_env("SGV_BAND_WALK");
-  if (e && e[0] == '0') return SGV_OK;
+  if (band_walk_max_nc() == 0) return SGV_OK;
   bool any = false;
   for (int b = 0; b < c->nblk; ++b) {
     const LdBlock& lb = c->ldb[ld][b];
@@ -402,6 +411,16 @@ static int plan_couplings(sgv_ctx* c, int ld, LdPlan& pl, std::vector<int>& slot
   };
   pl.hmax = 0;
   for (const LdCoupling& q : cv) pl.hmax = std::max<int64_t>(pl.hmax, std::max(q.nr, q.nc));
+  // a piece's head rows (coupling gb - 1: nc) and tail rows (coupling gb: nr)
+  // must not overlap: both couplings store their sums into the same panel slots
+  for (size_t i = 1; i < cv.size(); ++i) {
+    if (cv[i].gb != cv[i - 1].gb + 1) continue;
+    const int b = cv[i].gb - c->blk0;
+    if (b >= 0 && b < c->nblk && (int64_t)cv[i - 1].nc + cv[i].nr > c->bn[b])
+      return fail(c, SGV_ERR_ARG,
+                  "couplings %d and %d overlap in piece %d: %d head + %d tail rows > %lld markers",
+                  cv[i - 1].gb, cv[i].gb, cv[i].gb, cv[i - 1].nc, cv[i].nr, (long long)c->bn[b]);
+  }
   pl.halo = false;
   pl.h_len0 = pl.h_len1 = 0;
   for (const LdCoupling& q : cv) {
@@ -633,7 +652,8 @@ int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa_in){
     const int cls = mf ? 1 : sym_class(nc);
     if (mf) {
       HIPCHK(launch_pk(pa, nc, c->Mpad, c->d_pk, c->st));
-      if (pl.nwalks && nc <= 8) {   // band plan: the walks, then the head panels
+      const bool walk = pl.nwalks && nc <= band_walk_max_nc();
+      if (walk) {   // band plan: the walks, then the head panels
         HIPCHK(launch_band_walk(nc, pl.d_walks, pl.nwalks, pl.d_wpanels, pl.d_witems, c->d_pk, pa,
                                 c->d_whead, c->d_wcarry, pl.d_wfins, pl.nwfins, c->d_part, c->st));
       } else if (pl.ngrp <= 1) {
@@ -659,7 +679,7 @@ int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa_in){
         HIPCHK(hipEventRecord(c->ev_fin, c->st_fin));
         HIPCHK(hipStreamWaitEvent(c->st, c->ev_fin, 0));
       }
-      if (pl.nwalks && nc <= 8)   // head partials and carries, written and read
+      if (walk)   // head partials and carries, written and read
         c->aux_bytes += 2.0 * 8.0 * nc * SYM_H * (double)(pl.nhslots + pl.ncslots);
       else
         c->aux_bytes += 2.0 * 8.0 * nc * ((double)pl.nitems[cls] * SYM_H +

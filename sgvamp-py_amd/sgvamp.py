@@ -100,6 +100,10 @@ class BlockLD:
             self.block_sizes = [int(b) for b in block_sizes]
             self._loader = loader
         self._csr_loader = csr_loader
+        # from_csr: the whole matrix and the block offsets, so pieces and
+        # couplings are sliced from it directly (no per-block copies)
+        self._csr_src = None
+        self._sym = {}
         self.s = float(s)
 
     @property
@@ -119,11 +123,18 @@ class BlockLD:
         """Block b as scipy CSR, or None for a dense source."""
         return None if self._csr_loader is None else self._csr_loader(b).tocsr()
 
+    def symmetric(self, b, A=None):
+        """Whether CSR block b is exactly symmetric (cached: one transpose per block)."""
+        if b not in self._sym:
+            A = self.block_csr(b) if A is None else A
+            self._sym[b] = A is not None and (A != A.T).nnz == 0
+        return self._sym[b]
+
     def upload(self, eng, ld, b, packed=True):
         """Put block b of this matrix into LD slot `ld` of the engine."""
         A = self.block_csr(b) if packed else None
         if A is not None:
-            if (A != A.T).nnz == 0:
+            if self.symmetric(b, A):
                 import scipy.sparse
 
                 U = scipy.sparse.triu(A, format="csr")
@@ -142,12 +153,9 @@ class BlockLD:
         cache = self.__dict__.setdefault("_bw", {})
         if b not in cache:
             A = self.block_csr(b)
-            if A is None or (A != A.T).nnz != 0:
-                cache[b] = None
-            else:
-                import scipy.sparse
-
-                cache[b] = csr_bandwidth(scipy.sparse.triu(A, format="csr"))
+            # symmetric: the upper bandwidth is max(j - i) over all entries
+            # (straight from indptr / indices: no transpose, no triangle copy)
+            cache[b] = csr_bandwidth(A) if A is not None and self.symmetric(b, A) else None
         return cache[b]
 
     def pieces(self, cuts):
@@ -169,27 +177,38 @@ class BlockLD:
         if len(sizes) == len(self.block_sizes):
             return self, {}
         src = self
-        last = {}   # the original block last sliced (pieces are loaded in order)
+        if self._csr_src is not None:
+            # slices of the whole matrix: a rank loads only the pieces it owns
+            # and no block is copied whole
+            Afull, boffs = self._csr_src
+
+            def region(b, r0, r1, c0, c1):
+                g = int(boffs[b])
+                return Afull[g + r0:g + r1, g + c0:g + c1]
+        else:
+            last = {}   # the original block last sliced (pieces are loaded in order)
+
+            def region(b, r0, r1, c0, c1):
+                if last.get("b") != b:
+                    last.clear()
+                    last.update(b=b, A=src.block_csr(b))
+                return last["A"][r0:r1, c0:c1]
 
         def loader(k):
             b, o = origin[k]
-            if last.get("b") != b:
-                last.clear()
-                last.update(b=b, A=src.block_csr(b))
-            return last["A"][o:o + sizes[k], o:o + sizes[k]]
+            return region(b, o, o + sizes[k], o, o + sizes[k])
 
         L = BlockLD(block_sizes=sizes, s=self.s, csr_loader=loader)
         couplings = {}
         k = 0
         for b, ps in enumerate(cuts):
             if len(ps) > 1:
-                A = src.block_csr(b)
                 bw = max(1, src.band_width(b) or 1)
                 o = 0
                 for i in range(len(ps) - 1):
                     cut = o + ps[i]
                     nr, nc = min(bw, ps[i]), min(bw, ps[i + 1])
-                    C = A[cut - nr:cut, cut:cut + nc]
+                    C = region(b, cut - nr, cut, cut, cut + nc)
                     couplings[k + i] = (nr, nc, C)   # sparse; densified on upload
                     o = cut
             k += len(ps)
@@ -214,8 +233,13 @@ class BlockLD:
         M = A.shape[0]
         sizes = block_sizes or coarsen_blocks(detect_blocks_csr(A.indptr, A.indices, M))
         offs = np.concatenate([[0], np.cumsum(sizes)])
-        return cls(block_sizes=sizes,
-                   csr_loader=lambda b: A[offs[b]:offs[b + 1], offs[b]:offs[b + 1]], s=s)
+        if len(sizes) == 1:   # one block: the matrix itself, not a copy
+            L = cls(block_sizes=sizes, csr_loader=lambda b: A, s=s)
+        else:
+            L = cls(block_sizes=sizes,
+                    csr_loader=lambda b: A[offs[b]:offs[b + 1], offs[b]:offs[b + 1]], s=s)
+        L._csr_src = (A, offs)
+        return L
 
     def regroup(self, sizes):
         """The same matrix on a coarser partition (every boundary of ``sizes`` must

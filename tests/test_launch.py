@@ -277,3 +277,14 @@ def test_env_launch_requires_rank_and_local_rank():
         cm.launch_from_env(dict(RANK="5", WORLD_SIZE="8", LOCAL_WORLD_SIZE="4", MASTER_ADDR="10.0.0.5"))
     with pytest.raises(RuntimeError, match="LOCAL_RANK"):     # remote rendezvous, node size unknown
         cm.launch_from_env(dict(RANK="5", WORLD_SIZE="8", MASTER_ADDR="10.0.0.5"))
+    # a MASTER_ADDR naming this host (its name, or an address one of its
+    # interfaces holds) is a one-node launch
+    import socket
+    host = socket.gethostname()
+    try:
+        socket.getaddrinfo(host, None)
+        resolvable = True
+    except OSError:
+        resolvable = False
+    if resolvable:
+        assert cm.launch_from_env(dict(RANK="1", WORLD_SIZE="2", MASTER_ADDR=host))["local_rank"] == 1

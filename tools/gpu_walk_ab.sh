@@ -14,14 +14,14 @@ timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_mu
 tail -2 $o.parity.log
 export SGV_AB=1
 for rep in 1 2; do
-  for v in 1 0; do
+  for v in 8 0; do
     SGV_BAND_WALK=$v timeout -k 10 300 python -u tools/ldpass_band.py --M 1000000 --bw 1000 \
         --ncols 3,4,8 --tag walk=$v >> $o.ab.jsonl 2>> $o.ab.err || exit 1
   done
 done
 cat $o.ab.jsonl
 for rep in 1 2; do
-  for v in 1 0; do
+  for v in 4 0; do
     SGV_BAND_WALK=$v timeout -k 10 300 python -u bench.py --band 1000000,1000 --steps 10 --warmup 2 \
         --no-files --read-bw 0 > $o.bench_$v.json 2>> $o.bench.err || exit 1
     python -c "import json; d=json.load(open('$o.bench_$v.json')); print(json.dumps(dict(walk=$v, value=round(d['value'],2), ms_pass=round(d['roofline']['avg_launch_ms'],4), frac=round(d['roofline']['frac'],4), cg=d['cg_iters_per_step'][-1])))" | tee -a $o.bench.jsonl
