@@ -43,8 +43,13 @@ def per_dispatch(path, counter, kernel):
             if row.get("Counter_Name") != counter:
                 continue
             d = row.get("Dispatch_Id") or row.get("Correlation_Id")
-            vals[d] = vals.get(d, 0.0) + float(row["Counter_Value"])
-    return list(vals.values())
+            vals[int(d)] = vals.get(int(d), 0.0) + float(row["Counter_Value"])
+    return [vals[d] for d in sorted(vals)]
+
+
+def grouped(vals, n):
+    """sums of n consecutive dispatches: one pass launched as n block groups"""
+    return [sum(vals[i:i + n]) for i in range(0, len(vals) - n + 1, n)]
 
 
 def main():
@@ -56,9 +61,11 @@ def main():
     ap.add_argument("--algorithmic-bytes", type=float, default=None)
     ap.add_argument("--K", type=int, default=None, help="cohorts of the profiled bench run")
     ap.add_argument("--M", type=int, default=None, help="markers of the profiled bench run")
+    ap.add_argument("--group", type=int, default=1,
+                    help="launches per pass (block groups, round 5): traffic is summed per pass")
     a = ap.parse_args()
-    fetch = per_dispatch(a.fetch, "FETCH_SIZE", a.kernel)
-    write = per_dispatch(a.write, "WRITE_SIZE", a.kernel)
+    fetch = grouped(per_dispatch(a.fetch, "FETCH_SIZE", a.kernel), a.group)
+    write = grouped(per_dispatch(a.write, "WRITE_SIZE", a.kernel), a.group)
     if not fetch:
         sys.exit("no FETCH_SIZE rows for kernel %s" % a.kernel)
     f_kib = statistics.median(fetch)
@@ -70,6 +77,7 @@ def main():
         "label": a.label,
         "K": a.K,
         "M": a.M,
+        "launches_per_pass": a.group,
         "dispatches_fetch": len(fetch),
         "dispatches_write": len(write),
         "FETCH_SIZE_kib_median": f_kib,
