@@ -403,6 +403,15 @@ int sgv_exchange_stats(sgv_ctx* ctx, double* out14, int reset);
  * all-gathers are not counted in sgv_exchange_stats. */
 int sgv_exchange_probe(sgv_ctx* ctx, int reps, double* us_out);
 
+/* The EM exchange cost model alone (host arithmetic, no device): predicted us
+ * of one EM loop of `steps` enqueued steps over `cohort_markers` = K x M on
+ * `nranks` ranks with a per-all-gather latency of `latency_us`; out2[0] =
+ * replicated (one r1 all-gather, the loop over all markers on every rank;
+ * src/sgvamp.py:228-259), out2[1] = one exchange per EM step.  The library
+ * runs the cheaper (sgv_exchange_stats out[3], out[8..10]). */
+int sgv_em_cost_model(double cohort_markers, int nranks, double latency_us, double steps,
+                      double* out2);
+
 /* Synchronise the ctx stream. */
 int sgv_sync(sgv_ctx* ctx);
 

@@ -184,15 +184,25 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
   // used: a select right behind its load would make the compiler wait for each
   // load in turn.  The masks: bit a (bcol: row valid, not the diagonal block),
   // bit 2 t + e (brow: column inside the item)
+  // Pk row layout (k_pack): NG = 1 columns 0..3; NG = 2 PAIRED, column
+  // 4 q + n4 at 2 n4 + q, so a lane's two groups are one 16-B load
+  auto ld_p = [&](const double* rowp, double* v) {
+    if constexpr (NG == 2) {
+      const d2 x = ldg((const d2*)(rowp + 2 * n4));
+      v[0] = x.x;
+      v[1] = x.y;
+    } else {
+#pragma unroll
+      for (int q = 0; q < NG; ++q) v[q] = ldg(rowp + 4 * q + n4);
+    }
+  };
   auto load_bcol = [&](const Cur& u, int g2, double (*bc)[NG]) {
     int m = 0;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int rB = 16 * g2 + 4 * a + hi;
       m |= (rB < u.H && !u.colz) ? 1 << a : 0;
-#pragma unroll
-      for (int q = 0; q < NG; ++q)
-        bc[a][q] = ldg(u.pkb + (int64_t)(u.r0 + (rB < u.H ? rB : 0)) * pks + 4 * q + n4);
+      ld_p(u.pkb + (int64_t)(u.r0 + (rB < u.H ? rB : 0)) * pks, bc[a]);
     }
     return m;
   };
@@ -205,9 +215,7 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
         const int col = WK_WC * wid + 32 * t + 2 * pc + e;     // item-relative
         const bool ok = col < u.nc;
         m |= ok ? 1 << (2 * t + e) : 0;
-#pragma unroll
-        for (int q = 0; q < NG; ++q)
-          br[t][e][q] = ldg(u.pkb + (int64_t)(u.c0 + (ok ? col : 0)) * pks + 4 * q + n4);
+        ld_p(u.pkb + (int64_t)(u.c0 + (ok ? col : 0)) * pks, br[t][e]);
       }
     return m;
   };

@@ -170,11 +170,14 @@ int gather_f64(sgv_ctx* c, const double* d_send, double* d_recv, size_t cnt,
 // SGV_EM_REP=0/1 (with SGV_AB=1) forces either mode.
 constexpr double EM_K_FIX_US = 5.0, EM_K_PER_CM_US = 1.1e-5, EM_T_REP_US = 35.0,
                  EM_T_PS_US = 15.0, EM_AG_GBS = 100.0;
-static void em_costs(const sgv_ctx* c, double steps, double* rep_us, double* ps_us) {
-  const double km = (double)c->K * (double)c->Mtot, n = (double)c->nranks, L = c->xlat_us;
+static void em_costs_raw(double km, double n, double L, double steps, double* rep_us,
+                         double* ps_us) {
   *rep_us = L + 8.0 * km * (n - 1.0) / n / (EM_AG_GBS * 1e3) +
             steps * (EM_K_FIX_US + EM_K_PER_CM_US * km + EM_T_REP_US);
   *ps_us = steps * (EM_K_FIX_US + EM_K_PER_CM_US * km / n + EM_T_PS_US + L);
+}
+static void em_costs(const sgv_ctx* c, double steps, double* rep_us, double* ps_us) {
+  em_costs_raw((double)c->K * (double)c->Mtot, (double)c->nranks, c->xlat_us, steps, rep_us, ps_us);
 }
 // the mode of the next EM loop (maxit steps at most); records the prediction
 bool em_mode_pick(sgv_ctx* c, int maxit){
@@ -388,5 +391,13 @@ extern "C" int sgv_exchange_probe(sgv_ctx* c, int reps, double* us_out) {
   c->xchg_ms = ms0;
   c->xchg_bytes = b0;
   *us_out = agreed;
+  return SGV_OK;
+}
+
+extern "C" int sgv_em_cost_model(double cohort_markers, int nranks, double latency_us,
+                                 double steps, double* out2) {
+  if (!out2 || nranks < 1 || !(cohort_markers >= 0.0) || !(latency_us >= 0.0) || !(steps >= 0.0))
+    return SGV_ERR_ARG;
+  em_costs_raw(cohort_markers, (double)nranks, latency_us, steps, &out2[0], &out2[1]);
   return SGV_OK;
 }

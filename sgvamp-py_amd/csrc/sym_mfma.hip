@@ -917,14 +917,18 @@ __global__ __launch_bounds__(256) void k_sym_finalize_strip1(
 // vector).  PKS = the columns the pass kernel's groups read: 4 (NC <= 4), 8
 // (NC <= 8), 16 -- a row is one cache line's worth of what is read, so the
 // pass's Pk reads (L2 misses on M = 1e6) carry no unused columns
-template <int PKS>
+// PAIRED (PKS = 8, the 5-8-column band walks): slot p holds column
+// 4 (p & 1) + (p >> 1), so the walk's lane n4 reads its columns n4 and 4 + n4
+// as one 16-B load
+template <int PKS, bool PAIRED = false>
 __global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpad,
                                               double* __restrict__ pk) {
   if (pa.run && !ldg(pa.run)) return;
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (t >= mpad * PKS) return;
   const int64_t i = t / PKS;
-  const int c = (int)(t % PKS);
+  const int p = (int)(t % PKS);
+  const int c = PAIRED ? 4 * (p & 1) + (p >> 1) : p;
   pk[t] = c < ncol ? pa.in[c][i] : 0.0;
 }
 
@@ -950,13 +954,16 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
 }
 
-hipError_t launch_pk(const PassArgs& pa, int nc, int64_t mpad, double* d_pk, hipStream_t st) {
+hipError_t launch_pk(const PassArgs& pa, int nc, int64_t mpad, double* d_pk, hipStream_t st,
+                     bool paired) {
   if (nc < 1 || nc > 16) return hipErrorInvalidValue;
   const int pks = nc > 8 ? 16 : nc <= 4 ? 4 : 8;
   const int64_t npk = mpad * pks;
   const dim3 pg((unsigned)((npk + 255) / 256));
   if (pks == 4)
     hipLaunchKernelGGL(k_pack<4>, pg, dim3(256), 0, st, pa, nc, mpad, d_pk);
+  else if (pks == 8 && paired)
+    hipLaunchKernelGGL((k_pack<8, true>), pg, dim3(256), 0, st, pa, nc, mpad, d_pk);
   else if (pks == 8)
     hipLaunchKernelGGL(k_pack<8>, pg, dim3(256), 0, st, pa, nc, mpad, d_pk);
   else

@@ -82,6 +82,8 @@ _SIGS = {
     "sgv_timers": [_vp, _c_dbl_p, ctypes.c_int],
     "sgv_exchange_stats": [_vp, _c_dbl_p, ctypes.c_int],
     "sgv_exchange_probe": [_vp, ctypes.c_int, _c_dbl_p],
+    "sgv_em_cost_model": [ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_double,
+                          _c_dbl_p],
     "sgv_step": [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_dbl_p, _c_dbl_p,
                  _c_dbl_p, _c_dbl_p, _c_dbl_p, ctypes.c_double, _c_dbl_p, _c_dbl_p, _c_dbl_p,
                  _c_i8_p, ctypes.c_int, ctypes.c_double, ctypes.c_int, _c_dbl_p, _c_int_p,

@@ -144,3 +144,48 @@ def test_probe_stream_odd_position():
     for n in (5000, 1248, 3):
         ref = (rs.binomial(p=1 / 2, n=1, size=n) * 2 - 1).astype(np.int8)
         np.testing.assert_array_equal(ps.draw(n, 0, n), ref)
+
+
+def _em_costs(km, n, lat, steps):
+    import numpy as np
+    import hip_backend as hb
+
+    out = np.zeros(2)
+    assert hb.load().sgv_em_cost_model(km, n, lat, steps, hb.dptr(out)) == hb.SGV_OK
+    return out
+
+
+def test_em_cost_model_host_only():
+    """The EM exchange cost model (sgv_em_cost_model, host arithmetic): the
+    replicated loop's cost is one latency
+    plus the r1 bytes plus the steps over all markers, the per-step loop's one
+    latency per step; raising the latency moves the choice to replicated at a
+    crossover the formula predicts; bad arguments are refused."""
+    import hip_backend as hb
+
+    km = 4e6   # the north star: K = 4, M = 1e6
+    rep1, ps1 = _em_costs(km, 1, 25.0, 10)
+    assert rep1 == pytest.approx(ps1 + 25.0 + 10 * (35.0 - 15.0 - 25.0))
+    # per-step cost grows with L once per step, replicated once per loop
+    rep_a, ps_a = _em_costs(km, 8, 10.0, 10)
+    rep_b, ps_b = _em_costs(km, 8, 110.0, 10)
+    assert rep_b - rep_a == pytest.approx(100.0)
+    assert ps_b - ps_a == pytest.approx(10 * 100.0)
+    # the crossover latency: rep(L*) == ps(L*), with L per step vs once
+    lo, hi = 0.0, 1e4
+    for _ in range(60):
+        mid = 0.5 * (lo + hi)
+        r, p = _em_costs(km, 8, mid, 10)
+        lo, hi = (mid, hi) if p < r else (lo, mid)
+    r, p = _em_costs(km, 8, hi * 1.01, 10)
+    assert r < p
+    r, p = _em_costs(km, 8, lo * 0.99, 10)
+    assert p < r
+    # replicated bytes: 8 K M (N-1)/N at 100 GB/s
+    r2, _ = _em_costs(km, 2, 0.0, 0)
+    assert r2 == pytest.approx(8 * km * 0.5 / 1e5)
+    out = (ctypes.c_double * 2)()
+    lib = hb.load()
+    assert lib.sgv_em_cost_model(km, 0, 25.0, 10, out) != hb.SGV_OK
+    assert lib.sgv_em_cost_model(-1.0, 8, 25.0, 10, out) != hb.SGV_OK
+    assert lib.sgv_em_cost_model(km, 8, 25.0, 10, None) != hb.SGV_OK

@@ -10,6 +10,7 @@ d = collections.defaultdict(list)
 sha = collections.defaultdict(set)
 for line in open(sys.argv[1]):
     r = json.loads(line)
+    r.setdefault("shape", "M=%s,bw=%s" % (r.get("M"), r.get("bw")))   # ldpass_band.py lines
     d[(r["shape"], r["ncol"], r["tag"])].append(r["ms_per_pass"])
     sha[(r["shape"], r["ncol"])].add(r["sha"])
 for k in sorted(d):

@@ -10,6 +10,8 @@
 #   configs TAG                  one bench line per BASELINE.json configuration, the band line,
 #                                the N = 8 share and the 8-rank rehearsal
 #   ab      TAG VAR "v0 v1 .." SHAPES NCOLS [bench args]   an SGV_AB switch (gpu_ab_multi.sh)
+#   walkpmc TAG                  band walks vs strips (SGV_BAND_WALK 8 / 0) at M = 1e6, bw = 1,000,
+#                                4 and 8 columns: clock/stall, LDS and HBM-byte --pmc passes
 #   gate50  TAG [K]              the north star's own 50-iteration gate (SGV_FULL_GATE=1)
 cd "$(dirname "$0")/.." || exit 2
 R=$(pwd)
@@ -32,6 +34,19 @@ case $recipe in
   clock)
     P="GRBM_GUI_ACTIVE GRBM_COUNT SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"
     tools/gpu_steps.sh "clock_$T:300:cd /tmp && timeout -s KILL 280 rocprofv3 --pmc $P -d $R/gpurun_out/clock_$T -o pmc --output-format csv -- python3 $R/bench.py $B --no-files $*" ;;
+  walkpmc)
+    P1="GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS"
+    P2="GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU"
+    L="python3 $R/tools/ldpass_band.py --M 1000000 --bw 1000 --ncols 4,8 --reps 3"
+    steps=()
+    for v in 8 0; do
+      i=0
+      for p in "$P1" "$P2" FETCH_SIZE WRITE_SIZE; do
+        i=$((i + 1))
+        steps+=("wpmc_${T}_w${v}_$i:200:cd /tmp && SGV_AB=1 SGV_BAND_WALK=$v timeout -s KILL 180 rocprofv3 --pmc $p -d $R/gpurun_out/wpmc_${T}_w${v}_$i -o pmc --output-format csv -- $L --tag walk=$v")
+      done
+    done
+    tools/gpu_steps.sh "${steps[@]}" ;;
   configs)
     o=gpurun_out/cfg_$T
     run() {   # name, timeout, args...
