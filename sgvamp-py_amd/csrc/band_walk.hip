@@ -50,6 +50,11 @@ constexpr int WK_NW = 8;          // waves per workgroup
 constexpr int WK_WC = 64;         // columns per wave of a 512-column item
 constexpr int WK_NT = WK_WC / 32; // 32-column steps per wave
 constexpr int WK_RD = 4;          // row-sum hand-off buffers (row groups in flight)
+// operand loads: buffer loads (true) or flat global loads with clamped 64-bit
+// addresses (false), for 5-8 columns (NG = 2; 3-4 columns keep the global
+// loads: 6 % faster there, profiles/r05/walk_bufld_ab.jsonl); A/B builds flip these
+constexpr bool WK_CF_BUF = true;  // R fragments
+constexpr bool WK_P_BUF = true;   // P operands
 
 __device__ __forceinline__ void wk_lds_order() {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -120,8 +125,8 @@ __device__ __forceinline__ void walk_epilogue(const SymPanel& pn, const PassArgs
 template <int NG>
 __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
     const SymWalk* __restrict__ walks, const SymPanel* __restrict__ panels,
-    const SymItem* __restrict__ items, const double* __restrict__ pk, int pks, PassArgs pa,
-    int ncol, double* __restrict__ headbuf, double* __restrict__ carrybuf,
+    const SymItem* __restrict__ items, const double* __restrict__ pk, int pks, int64_t pk_rows,
+    PassArgs pa, int ncol, double* __restrict__ headbuf, double* __restrict__ carrybuf,
     double* __restrict__ partials) {
   constexpr int RW = 4 * NG;                                   // accumulator row stride
   constexpr int CPT = RW / 2;                                  // epilogue columns per thread
@@ -146,76 +151,128 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
       __builtin_amdgcn_s_sleep(1);
   };
 
+  // Every operand load is a buffer load: a wave-uniform descriptor, a 32-bit
+  // lane offset and the row group's step in the scalar offset, so the loop
+  // computes no 64-bit addresses and clamps nothing; a read past a
+  // descriptor's range returns 0 without touching memory (rows past a ragged
+  // panel's H, Pk rows past the vector, the row operands' re-reads in row
+  // groups other than an item's last).
   // an item of the walk as this wave sees it
   struct Cur {
-    uint64_t b0;        // element (r0, c0)
-    int64_t w;          // row stride
-    const double* pkb;  // Pk of the block
+    const double* b0;   // element (r0, c0)
+    int w;              // row stride
     int nc, c0, r0, H;
+    uint32_t rec;       // bytes from b0 to the end of the panel's H rows
     bool colz;          // this wave's columns lie in the diagonal block
   };
   auto make = [&](const SymItem& it, const SymPanel& p) {
     Cur u;
     const int crel = it.c0 - it.r0;
-    u.b0 = (uint64_t)(it.P + crel);
-    u.w = it.w;
-    u.pkb = pk + (int64_t)p.voff * pks;
+    u.b0 = it.P + crel;
+    u.w = (int)it.w;
     u.nc = it.nc;
     u.c0 = it.c0;
     u.r0 = p.r0;
     u.H = p.H;
+    u.rec = (uint32_t)(((int64_t)p.H * it.w - crel) * 8);
     u.colz = crel + WK_WC * wid < SYM_H;
     return u;
   };
-  // fragments of row group g2, step t (16 B per lane, branch-free: rows past
-  // H clamp -- their P is 0 -- and columns past the item load column 0)
+  // descriptors from wave-uniform words (readfirstlane: provably uniform, so
+  // no waterfall loop around each load)
+  auto rsrc = [](const double* p, uint32_t bytes) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t l32 = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t h32 = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)h32 << 32) | l32), 0,
+                                             (int)__builtin_amdgcn_readfirstlane(bytes),
+                                             0x00020000);
+  };
+  // the walk's block in Pk (the panels of a walk are one block's)
+  const int64_t pvoff = panels[wk.p0].voff;
+  const int p_rng = (int)min<int64_t>((pk_rows - pvoff) * pks * 8, 0x7FFF0000);
+  const auto prs = rsrc(pk + pvoff * pks, (uint32_t)p_rng);
+  const int pbyte = 8 * pks;                                   // one Pk row
+  // fragments of row group g2, step t (16 B per lane, nontemporal); columns
+  // past the item are masked where they are used
   auto load_cf = [&](const Cur& u, int g2, int t, d2* cf) {
-    uint64_t bb = u.b0;
-    asm volatile("" : "+s"(bb));
     const int xc = WK_WC * wid + 32 * t + 2 * lo;
+    if constexpr (WK_CF_BUF && NG == 2) {
+      const auto r = rsrc(u.b0, u.rec);
+      const int so = __builtin_amdgcn_readfirstlane(16 * g2 * u.w * 8);
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int rB = 16 * g2 + 4 * a + hi;
-      const double* row = (const double*)bb + (int64_t)(rB < u.H ? rB : u.H - 1) * u.w;
-      cf[a] = ldg_nt((const d2*)(row + (xc < u.nc ? xc : 0)));
+      for (int a = 0; a < 4; ++a)
+        cf[a] = __builtin_bit_cast(
+            d2, __builtin_amdgcn_raw_buffer_load_b128(r, ((4 * a + hi) * u.w + xc) * 8, so, 2));
+    } else {
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int rB = 16 * g2 + 4 * a + hi;
+        const double* row = u.b0 + (int64_t)(rB < u.H ? rB : u.H - 1) * u.w;
+        cf[a] = ldg_nt((const d2*)(row + (xc < u.nc ? xc : 0)));
+      }
     }
   };
-  // P operands are loaded raw (clamped addresses) and masked when they are
-  // used: a select right behind its load would make the compiler wait for each
-  // load in turn.  The masks: bit a (bcol: row valid, not the diagonal block),
-  // bit 2 t + e (brow: column inside the item)
   // Pk row layout (k_pack): NG = 1 columns 0..3; NG = 2 PAIRED, column
   // 4 q + n4 at 2 n4 + q, so a lane's two groups are one 16-B load
-  auto ld_p = [&](const double* rowp, double* v) {
-    if constexpr (NG == 2) {
-      const d2 x = ldg((const d2*)(rowp + 2 * n4));
+  auto ld_p = [&](int vo, int so, double* v) {
+    if constexpr (!WK_P_BUF || NG == 1) {
+      const char* pb = (const char*)(pk + pvoff * pks) + min(so + vo, p_rng - 64);
+      if constexpr (NG == 2) {
+        const d2 x = ldg((const d2*)(pb + 16 * n4));
+        v[0] = x.x;
+        v[1] = x.y;
+      } else {
+#pragma unroll
+        for (int q = 0; q < NG; ++q) v[q] = ldg((const double*)(pb + 8 * (4 * q + n4)));
+      }
+    } else if constexpr (NG == 2) {
+      const d2 x =
+          __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(prs, vo + 16 * n4, so, 0));
       v[0] = x.x;
       v[1] = x.y;
     } else {
 #pragma unroll
-      for (int q = 0; q < NG; ++q) v[q] = ldg(rowp + 4 * q + n4);
+      for (int q = 0; q < NG; ++q)
+        v[q] = __builtin_bit_cast(
+            double, __builtin_amdgcn_raw_buffer_load_b64(prs, vo + 8 * (4 * q + n4), so, 0));
     }
   };
+  // P operands, raw, masked when they are used (a select right behind its
+  // load would make the compiler wait for each load in turn).  The masks:
+  // bit a (bcol: row valid, not the diagonal block), bit 2 t + e (brow: column
+  // inside the item)
   auto load_bcol = [&](const Cur& u, int g2, double (*bc)[NG]) {
     int m = 0;
+    const int so = __builtin_amdgcn_readfirstlane((u.r0 + 16 * g2) * pbyte);
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int rB = 16 * g2 + 4 * a + hi;
       m |= (rB < u.H && !u.colz) ? 1 << a : 0;
-      ld_p(u.pkb + (int64_t)(u.r0 + (rB < u.H ? rB : 0)) * pks, bc[a]);
+      ld_p((4 * a + hi) * pbyte, so, bc[a]);
     }
     return m;
   };
-  auto load_brow = [&](const Cur& u, double (*br)[2][NG]) {
+  // live = false (not the item's last row group: the next item's row operands
+  // are not due yet) reads past the range -- the same loads on every path, no
+  // bytes moved.  The offset is chosen by a scalar select (a vector select's
+  // temporary landed in a register a load was still filling: a wait for it)
+  auto load_brow = [&](const Cur& u, bool live, double (*br)[2][NG]) {
     int m = 0;
+    int so;
+    asm volatile("s_cmp_lg_u32 %1, 0\n\ts_cselect_b32 %0, %2, %3"
+                 : "=s"(so)
+                 : "s"(__builtin_amdgcn_readfirstlane((int)live)),
+                   "s"(__builtin_amdgcn_readfirstlane(u.c0 * pbyte)),
+                   "s"(__builtin_amdgcn_readfirstlane(p_rng))
+                 : "scc");
 #pragma unroll
     for (int t = 0; t < WK_NT; ++t)
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int col = WK_WC * wid + 32 * t + 2 * pc + e;     // item-relative
-        const bool ok = col < u.nc;
-        m |= ok ? 1 << (2 * t + e) : 0;
-        ld_p(u.pkb + (int64_t)(u.c0 + (ok ? col : 0)) * pks, br[t][e]);
+        m |= col < u.nc ? 1 << (2 * t + e) : 0;
+        ld_p(col * pbyte, so, br[t][e]);
       }
     return m;
   };
@@ -228,7 +285,7 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
 #pragma unroll
   for (int t = 0; t < WK_NT; ++t) load_cf(cu, 0, t, cfn[t]);
   int bcm = load_bcol(cu, 0, bcn);
-  int brm = load_brow(cu, brn);
+  int brm = load_brow(cu, true, brn);
 
   int gg = 0;                                                  // row groups done
 #pragma unroll 1
@@ -279,11 +336,11 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
         Cur src;
         src.b0 = last ? cn.b0 : cu.b0;
         src.w = last ? cn.w : cu.w;
-        src.pkb = last ? cn.pkb : cu.pkb;
         src.nc = last ? cn.nc : cu.nc;
         src.c0 = last ? cn.c0 : cu.c0;
         src.r0 = last ? cn.r0 : cu.r0;
         src.H = last ? cn.H : cu.H;
+        src.rec = last ? cn.rec : cu.rec;
         src.colz = last ? cn.colz : cu.colz;
         const int gn = last ? 0 : g2 + 1;
         double drow[4][NG];
@@ -337,7 +394,7 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
           load_cf(src, gn, t, cfn[t]);
           if (t == 0) {
             bcm = load_bcol(src, gn, bcn);
-            brm = load_brow(src, brn);
+            brm = load_brow(src, last, brn);
           }
         }
         // the row group's row sums: 4 blocks (DPP), handed to the combining wave
@@ -460,7 +517,8 @@ __global__ __launch_bounds__(256) void k_walk_fin(const WalkFin* __restrict__ fi
 }
 
 hipError_t launch_band_walk(int nc, const SymWalk* d_walks, int nwalks, const SymPanel* d_panels,
-                            const SymItem* d_items, const double* d_pk, const PassArgs& pa,
+                            const SymItem* d_items, const double* d_pk, int64_t pk_rows,
+                            const PassArgs& pa,
                             double* headbuf, double* carrybuf, const WalkFin* d_fins, int nfins,
                             double* partials, hipStream_t st) {
   if (nc < 1 || nc > 8) return hipErrorInvalidValue;
@@ -468,10 +526,10 @@ hipError_t launch_band_walk(int nc, const SymWalk* d_walks, int nwalks, const Sy
   if (nwalks > 0) {
     if (nc <= 4)
       hipLaunchKernelGGL(k_band_walk<1>, dim3(nwalks), dim3(WK_NW * 64), 0, st, d_walks, d_panels,
-                         d_items, d_pk, pks, pa, nc, headbuf, carrybuf, partials);
+                         d_items, d_pk, pks, pk_rows, pa, nc, headbuf, carrybuf, partials);
     else
       hipLaunchKernelGGL(k_band_walk<2>, dim3(nwalks), dim3(WK_NW * 64), 0, st, d_walks, d_panels,
-                         d_items, d_pk, pks, pa, nc, headbuf, carrybuf, partials);
+                         d_items, d_pk, pks, pk_rows, pa, nc, headbuf, carrybuf, partials);
   }
   if (nfins > 0) {
     if (nc <= 4)

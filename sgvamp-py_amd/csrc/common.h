@@ -37,8 +37,10 @@ __device__ __forceinline__ T ldg_nt(const T* p) {   // streaming (read-once) dat
 template <int N>
 __device__ __forceinline__ double row_ror(double v) {
   const long long b = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0x120 + N, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x120 + N, 0xF, 0xF, false);
+  // every row and bank enabled and row_ror reads inside the row: each lane is
+  // written, so no "old" value (mov_dpp: no v_mov of a zero per half first)
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, 0x120 + N, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x120 + N, 0xF, 0xF, true);
   return __builtin_bit_cast(double, (long long)(((unsigned long long)(unsigned)hi << 32) |
                                                 (unsigned)lo));
 }
@@ -356,8 +358,9 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
                            double* colpart, bool ragged, int pair, hipStream_t st);
 // band walks (NC <= 8, band_walk.hip): the walks, then the head panels' finalize
 hipError_t launch_band_walk(int nc, const SymWalk* d_walks, int nwalks, const SymPanel* d_panels,
-                            const SymItem* d_items, const double* d_pk, const PassArgs& pa,
-                            double* headbuf, double* carrybuf, const WalkFin* d_fins, int nfins,
+                            const SymItem* d_items, const double* d_pk, int64_t pk_rows,
+                            const PassArgs& pa, double* headbuf, double* carrybuf,
+                            const WalkFin* d_fins, int nfins,
                             double* partials, hipStream_t st);
 hipError_t launch_sym_finalize_strip(int nc, const SymPanel* d_panels, int npanels,
                                      const PassArgs& pa, const double* rowpart,

@@ -654,7 +654,8 @@ int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa_in){
       const bool walk = pl.nwalks && nc <= band_walk_max_nc();
       HIPCHK(launch_pk(pa, nc, c->Mpad, c->d_pk, c->st, walk && nc > 4));
       if (walk) {   // band plan: the walks, then the head panels
-        HIPCHK(launch_band_walk(nc, pl.d_walks, pl.nwalks, pl.d_wpanels, pl.d_witems, c->d_pk, pa,
+        HIPCHK(launch_band_walk(nc, pl.d_walks, pl.nwalks, pl.d_wpanels, pl.d_witems, c->d_pk,
+                                c->Mpad, pa,
                                 c->d_whead, c->d_wcarry, pl.d_wfins, pl.nwfins, c->d_part, c->st));
       } else if (pl.ngrp <= 1) {
         HIPCHK(launch_sym_mfma(nc, pl.d_strips, pl.nstrips, pl.d_sitems, pa, c->d_pk,
