@@ -21,7 +21,7 @@
 // starts the block) lack the previous walk's column parts: they leave their
 // partial sums in headbuf, the previous walk leaves its open slots in carrybuf,
 // and k_walk_fin adds the two (then the coupling sums) and runs the epilogue.
-// The walk partition is a function of the block alone (capi.hip plan_walks),
+// The walk partition is a function of the block alone (ldplan.hip plan_walks),
 // so the summation order -- and every product -- is the same on 1 and N ranks.
 //
 // 8 waves per workgroup (one per CU: the ring takes R x 16 KiB of LDS), each
@@ -34,6 +34,16 @@
 // run up to WK_RD - 1 row groups ahead of the slowest (bounded waits: every
 // wait is on a write or a combine another wave reaches without waiting on
 // this one).  One barrier per panel (its epilogue).
+//
+// The loop's addressing is what set its speed (profiles/r05/walk_ab/): the
+// first forms spent ~190 VALU per 4-KiB sub-tile (1.9x the strips), most of
+// it 64-bit address arithmetic and clamps for the P operands, and re-read the
+// row operands every row group.  Now the P operands of a walk come from one
+// base with 32-bit offsets (16-B paired loads at 5-8 columns, k_pack's PAIRED
+// layout), and the row operands are read only in an item's last row group
+// (the others read one cached row): 1.68 / 1.71 / 1.99 ms at 3 / 4 / 8
+// columns against 1.82 / 1.85 / 2.23 before (M = 1e6, bw = 1,000).  Buffer
+// loads for the R fragments were slower (+5-8 %) and are not used.
 //
 // Summation order of row i of panel g (fixed): the column parts of panels
 // g - R + 1, ..., g - 1 in panel order (in a head panel: those inside the walk,
@@ -50,11 +60,6 @@ constexpr int WK_NW = 8;          // waves per workgroup
 constexpr int WK_WC = 64;         // columns per wave of a 512-column item
 constexpr int WK_NT = WK_WC / 32; // 32-column steps per wave
 constexpr int WK_RD = 4;          // row-sum hand-off buffers (row groups in flight)
-// operand loads: buffer loads (true) or flat global loads with clamped 64-bit
-// addresses (false), for 5-8 columns (NG = 2; 3-4 columns keep the global
-// loads: 6 % faster there, profiles/r05/walk_bufld_ab.jsonl); A/B builds flip these
-constexpr bool WK_CF_BUF = true;  // R fragments
-constexpr bool WK_P_BUF = true;   // P operands
 
 __device__ __forceinline__ void wk_lds_order() {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -151,18 +156,11 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
       __builtin_amdgcn_s_sleep(1);
   };
 
-  // Every operand load is a buffer load: a wave-uniform descriptor, a 32-bit
-  // lane offset and the row group's step in the scalar offset, so the loop
-  // computes no 64-bit addresses and clamps nothing; a read past a
-  // descriptor's range returns 0 without touching memory (rows past a ragged
-  // panel's H, Pk rows past the vector, the row operands' re-reads in row
-  // groups other than an item's last).
   // an item of the walk as this wave sees it
   struct Cur {
     const double* b0;   // element (r0, c0)
     int w;              // row stride
     int nc, c0, r0, H;
-    uint32_t rec;       // bytes from b0 to the end of the panel's H rows
     bool colz;          // this wave's columns lie in the diagonal block
   };
   auto make = [&](const SymItem& it, const SymPanel& p) {
@@ -174,89 +172,58 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
     u.c0 = it.c0;
     u.r0 = p.r0;
     u.H = p.H;
-    u.rec = (uint32_t)(((int64_t)p.H * it.w - crel) * 8);
     u.colz = crel + WK_WC * wid < SYM_H;
     return u;
   };
-  // descriptors from wave-uniform words (readfirstlane: provably uniform, so
-  // no waterfall loop around each load)
-  auto rsrc = [](const double* p, uint32_t bytes) {
-    const uint64_t a = (uint64_t)p;
-    const uint32_t l32 = __builtin_amdgcn_readfirstlane((uint32_t)a);
-    const uint32_t h32 = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)h32 << 32) | l32), 0,
-                                             (int)__builtin_amdgcn_readfirstlane(bytes),
-                                             0x00020000);
-  };
-  // the walk's block in Pk (the panels of a walk are one block's)
-  const int64_t pvoff = panels[wk.p0].voff;
-  const int p_rng = (int)min<int64_t>((pk_rows - pvoff) * pks * 8, 0x7FFF0000);
-  const auto prs = rsrc(pk + pvoff * pks, (uint32_t)p_rng);
-  const int pbyte = 8 * pks;                                   // one Pk row
-  // fragments of row group g2, step t (16 B per lane, nontemporal); columns
-  // past the item are masked where they are used
+  // fragments of row group g2, step t (16 B per lane, nontemporal; rows past
+  // H clamp -- their P is 0 -- and columns past the item load column 0)
   auto load_cf = [&](const Cur& u, int g2, int t, d2* cf) {
     const int xc = WK_WC * wid + 32 * t + 2 * lo;
-    if constexpr (WK_CF_BUF && NG == 2) {
-      const auto r = rsrc(u.b0, u.rec);
-      const int so = __builtin_amdgcn_readfirstlane(16 * g2 * u.w * 8);
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
-        cf[a] = __builtin_bit_cast(
-            d2, __builtin_amdgcn_raw_buffer_load_b128(r, ((4 * a + hi) * u.w + xc) * 8, so, 2));
-    } else {
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const int rB = 16 * g2 + 4 * a + hi;
-        const double* row = u.b0 + (int64_t)(rB < u.H ? rB : u.H - 1) * u.w;
-        cf[a] = ldg_nt((const d2*)(row + (xc < u.nc ? xc : 0)));
-      }
+    for (int a = 0; a < 4; ++a) {
+      const int rB = 16 * g2 + 4 * a + hi;
+      cf[a] = ldg_nt((const d2*)(u.b0 + (rB < u.H ? rB : u.H - 1) * u.w + (xc < u.nc ? xc : 0)));
     }
   };
-  // Pk row layout (k_pack): NG = 1 columns 0..3; NG = 2 PAIRED, column
-  // 4 q + n4 at 2 n4 + q, so a lane's two groups are one 16-B load
-  auto ld_p = [&](int vo, int so, double* v) {
-    if constexpr (!WK_P_BUF || NG == 1) {
-      const char* pb = (const char*)(pk + pvoff * pks) + min(so + vo, p_rng - 64);
-      if constexpr (NG == 2) {
-        const d2 x = ldg((const d2*)(pb + 16 * n4));
-        v[0] = x.x;
-        v[1] = x.y;
-      } else {
-#pragma unroll
-        for (int q = 0; q < NG; ++q) v[q] = ldg((const double*)(pb + 8 * (4 * q + n4)));
-      }
-    } else if constexpr (NG == 2) {
-      const d2 x =
-          __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(prs, vo + 16 * n4, so, 0));
+  // P operands: one base per walk (its block's Pk rows; the panels of a walk
+  // are one block's) and 32-bit byte offsets clamped to the Pk vector -- rows
+  // or columns past the item read whatever lies there and are masked where
+  // they are used (a select right behind its load would make the compiler
+  // wait for each load in turn).  Pk row layout (k_pack): NG = 1 columns
+  // 0..3; NG = 2 PAIRED, column 4 q + n4 at 2 n4 + q, so a lane's two groups
+  // are one 16-B load
+  const int64_t pvoff = panels[wk.p0].voff;
+  const char* pbase = (const char*)(pk + pvoff * pks);
+  const int p_rng = (int)min<int64_t>((pk_rows - pvoff) * pks * 8, 0x7FFF0000);
+  const int pbyte = 8 * pks;                                   // one Pk row
+  auto ld_p = [&](int off, double* v) {
+    const char* pb = pbase + min(off, p_rng - pbyte);   // the last row is read whole
+    if constexpr (NG == 2) {
+      const d2 x = ldg((const d2*)(pb + 16 * n4));
       v[0] = x.x;
       v[1] = x.y;
     } else {
 #pragma unroll
-      for (int q = 0; q < NG; ++q)
-        v[q] = __builtin_bit_cast(
-            double, __builtin_amdgcn_raw_buffer_load_b64(prs, vo + 8 * (4 * q + n4), so, 0));
+      for (int q = 0; q < NG; ++q) v[q] = ldg((const double*)(pb + 8 * (4 * q + n4)));
     }
   };
-  // P operands, raw, masked when they are used (a select right behind its
-  // load would make the compiler wait for each load in turn).  The masks:
-  // bit a (bcol: row valid, not the diagonal block), bit 2 t + e (brow: column
-  // inside the item)
+  // the masks: bit a (bcol: row valid, not the diagonal block), bit 2 t + e
+  // (brow: column inside the item)
   auto load_bcol = [&](const Cur& u, int g2, double (*bc)[NG]) {
     int m = 0;
-    const int so = __builtin_amdgcn_readfirstlane((u.r0 + 16 * g2) * pbyte);
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int rB = 16 * g2 + 4 * a + hi;
       m |= (rB < u.H && !u.colz) ? 1 << a : 0;
-      ld_p((4 * a + hi) * pbyte, so, bc[a]);
+      ld_p((u.r0 + rB) * pbyte, bc[a]);
     }
     return m;
   };
   // live = false (not the item's last row group: the next item's row operands
-  // are not due yet) reads past the range -- the same loads on every path, no
-  // bytes moved.  The offset is chosen by a scalar select (a vector select's
-  // temporary landed in a register a load was still filling: a wait for it)
+  // are not due yet) reads the range's last row instead -- the
+  // same loads on every path, L2 hits.  The offset is chosen by a scalar select
+  // (a vector select's temporary landed in a register a load was still
+  // filling: a wait for it)
   auto load_brow = [&](const Cur& u, bool live, double (*br)[2][NG]) {
     int m = 0;
     int so;
@@ -272,7 +239,7 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
       for (int e = 0; e < 2; ++e) {
         const int col = WK_WC * wid + 32 * t + 2 * pc + e;     // item-relative
         m |= col < u.nc ? 1 << (2 * t + e) : 0;
-        ld_p(col * pbyte, so, br[t][e]);
+        ld_p(so + col * pbyte, br[t][e]);
       }
     return m;
   };
@@ -340,7 +307,6 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
         src.c0 = last ? cn.c0 : cu.c0;
         src.r0 = last ? cn.r0 : cu.r0;
         src.H = last ? cn.H : cu.H;
-        src.rec = last ? cn.rec : cu.rec;
         src.colz = last ? cn.colz : cu.colz;
         const int gn = last ? 0 : g2 + 1;
         double drow[4][NG];

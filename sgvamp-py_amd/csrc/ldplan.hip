@@ -314,15 +314,15 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
 // column part inside the walk or the one before it.  A walk that does not start
 // its block has min(R - 1, np) head panels; one that does not end it leaves
 // min(R - 1, panels after it) carry slots.
-// The walks run the passes of up to 4 columns (one 4x4x4 column group): 1-3 %
-// faster than the strips at M = 1e6, bw = 1,000 (3 / 4 columns: 1.82 / 1.86
-// vs 1.87 / 1.92 ms); at 5-8 columns they are 14 % slower (2.43 vs 2.14 ms,
-// profiles/r05/walk_v5_ab.jsonl), so those stay on the strips.
-// SGV_BAND_WALK (with SGV_AB=1): 0 = the strips for every band pass, 8 = walks
-// up to 8 columns (A/B).
+// The walks run the band passes of up to 8 columns (two 4x4x4 column groups;
+// 9-16 columns stay on the strips' 16x16x4 kernel): at M = 1e6, bw = 1,000
+// 1.68 / 1.71 / 1.99 ms at 3 / 4 / 8 columns against the strips' 1.87 / 1.92
+// / 2.12 (profiles/r05/walk_ab/wvs_a_ab.jsonl).
+// SGV_BAND_WALK (with SGV_AB=1): 0 = the strips for every band pass, 4 = walks
+// up to 4 columns (A/B).
 static int band_walk_max_nc() {
   const char* e = ab_env("SGV_BAND_WALK");
-  return e ? (e[0] == '0' ? 0 : e[0] == '8' ? 8 : 4) : 4;
+  return e ? (e[0] == '0' ? 0 : e[0] == '4' ? 4 : 8) : 8;
 }
 
 static int plan_walks(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
