@@ -43,7 +43,7 @@
 // layout), and the row operands are read only in an item's last row group
 // (the others read one cached row): 1.68 / 1.71 / 1.99 ms at 3 / 4 / 8
 // columns against 1.82 / 1.85 / 2.23 before (M = 1e6, bw = 1,000).  Buffer
-// loads for the R fragments were slower (+5-8 %) and are not used.
+// loads (of the R fragments or of the P operands) were 4-13 % slower.
 //
 // Summation order of row i of panel g (fixed): the column parts of panels
 // g - R + 1, ..., g - 1 in panel order (in a head panel: those inside the walk,
