@@ -68,7 +68,7 @@ case $recipe in
   ab)
     bash tools/gpu_ab_multi.sh gpurun_out/ab_$T "$@" ;;
   gate50)
-    tools/gpu_steps.sh "gate50_$T:2400:SGV_FULL_GATE=1 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -q -s -p no:cacheprovider -k 'north_star_50 and ${1:-4}' --timeout 2300" ;;
+    tools/gpu_steps.sh "gate50_$T:1100:SGV_FULL_GATE=1 python -u -m pytest tests/test_gpu_configs.py -m gpu -x -q -s -p no:cacheprovider -k 'north_star_50 and ${1:-4}' --timeout 1050" ;;
   *)
     echo "unknown recipe $recipe"; exit 2 ;;
 esac
