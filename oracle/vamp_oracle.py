@@ -561,7 +561,7 @@ def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-
           prior_vars=(0.0, 1.0), prior_probs=(0.99, 0.01), x0=None, cg_maxit=500,
           em_prior_maxit=100, learn_gamw=True, lmmse_damp=False, prior_update="em",
           update_prior_from=1, seed=0, reducer=None, M_total=None, probe=None,
-          rs_recurrence=False, batched=False):
+          rs_recurrence=False, batched=False, progress=None):
     """All K cohorts of src/sgvamp.py:196-389 in one process.
 
     batched: run the 2K CG solves of an iteration in lockstep (cg_track_batch:
@@ -608,6 +608,8 @@ def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-
     gam_mle = None                                                       # :31 self.gam
 
     for it in range(iterations):
+        if progress is not None:   # test harness heartbeat (long full-size runs)
+            progress(it)
         gam1s = np.array(gam1_k, dtype=np.float64)                      # :228-233
         r1s = np.stack(r1)
         if it >= update_prior_from and prior_update == "em":            # :242-259

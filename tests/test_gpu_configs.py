@@ -230,7 +230,8 @@ def _gate_50(nblk, size, K, tmp_path, its=50, ref_algebra=False):
     else:
         t = vo.infer([L], [0] * K, r_list, [N] * K, its, rho=0.5, gamw=5.0, gam1=1e-6, x0=x0,
                      seed=SEED, reducer=vo.Reducer("blocked", bounds=L.bounds), rs_recurrence=True,
-                     batched=True, **prior, **run)
+                     batched=True, progress=lambda it: _log("oracle iteration %d" % it),
+                     **prior, **run)
     errs = []
     for it in range(its):
         got = xh[it].ravel() / np.sqrt(N * K)
