@@ -233,72 +233,31 @@ hipError_t launch_sym_pass(int nc, int cls, const SymItem* d_items, int nitems,
 }
 
 // ---- coupled band pieces --------------------------------------------------
-// One workgroup per (CouplingTask, 64-row quarter): thread (q, r) sums the
-// inner index range [q L, (q + 1) L) (L = ceil(inner / 4), in order) for output
-// row 64 y + r, and the 4 parts are added in order 0..3 -- a fixed order on
-// every rank, so the coupling sums are the same whichever rank holds the
-// source rows.  Remote sources sit in the gathered halo [rank][2][nc][hstride]:
-// task.src = 2 rank + slot.  Rows of a slot no task writes stay as cleared.
-template <int NC>
-__global__ __launch_bounds__(256) void k_coupling(const CouplingTask* __restrict__ tasks,
-                                                  PassArgs pa, const double* __restrict__ halo,
-                                                  int64_t hstride, double* __restrict__ cpbuf) {
-  __shared__ double part[3][64][NC];
-  const CouplingTask tk = tasks[blockIdx.x];
-  if (pa.run && !ldg(pa.run)) return;
-  const int r = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int row = 64 * blockIdx.y + r;                 // within the task
-  const bool live = row < tk.nrows;
-  const int L = (tk.inner + 3) / 4;
-  const int k0 = q * L, k1 = min(tk.inner, k0 + L);
-  double y[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) y[c] = 0.0;
-  if (live) {
-    const double* src[NC];
-#pragma unroll
-    for (int c = 0; c < NC; ++c)
-      src[c] = tk.local ? pa.in[c] + tk.src : halo + (tk.src * NC + c) * hstride;
-    const double* m = tk.m + tk.row0 + row;
-#pragma unroll 4
-    for (int k = k0; k < k1; ++k) {
-      const double a = m[(int64_t)k * tk.ldm];
-#pragma unroll
-      for (int c = 0; c < NC; ++c) y[c] += a * ldg(src[c] + k);
-    }
-  }
-  if (q > 0) {
-#pragma unroll
-    for (int c = 0; c < NC; ++c) part[q - 1][r][c] = y[c];
-  }
-  __syncthreads();
-  if (q == 0 && live) {
-    double* out = cpbuf + ((int64_t)tk.cp * 256 + tk.prow0 + row) * NC;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) out[c] = ((y[c] + part[0][r][c]) + part[1][r][c]) + part[2][r][c];
-  }
-}
-
-// The same sums with the source values staged through LDS: per chunk of CPL_CH
-// steps the workgroup loads each part's next CPL_CH source values (all NC
-// columns) once, and every row thread reads them from LDS (one broadcast per
+// One workgroup per (CouplingTask, 64-row quarter), CPL_NP waves: thread (q, r)
+// sums the inner index range [q L, (q + 1) L) (L = ceil(inner / CPL_NP), in
+// increasing k) for output row 64 y + r, and the CPL_NP parts are added in
+// order 0, 1, ... -- a fixed order on every rank, so the coupling sums are the
+// same whichever rank holds the source rows.  Per chunk of CPL_CH steps the
+// workgroup stages each part's next CPL_CH source values (all NC columns) in
+// LDS once, and every row thread reads them from there (one broadcast per
 // column) instead of issuing NC global loads per inner index; the C loads of
-// CPL_U consecutive steps go out before their FMAs.  Every y[c] still adds its
-// terms in increasing k, parts combined in order 0..3: bitwise k_coupling.
+// CPL_U consecutive steps go out before their FMAs.  Remote sources sit in
+// the gathered halo [rank][2][nc][hstride]: task.src = 2 rank + slot.  Rows of
+// a slot no task writes stay as cleared.
 constexpr int CPL_CH = 32;
 constexpr int CPL_U = 8;
-template <int NC>
-__global__ __launch_bounds__(256) void k_coupling_lds(const CouplingTask* __restrict__ tasks,
-                                                      PassArgs pa, const double* __restrict__ halo,
-                                                      int64_t hstride, double* __restrict__ cpbuf) {
-  __shared__ double part[3][64][NC];
-  __shared__ double s_src[4][CPL_CH][NC];
+template <int NC, int CPL_NP>   // CPL_NP: parts (waves) per workgroup
+__global__ __launch_bounds__(64 * CPL_NP) void k_coupling_lds(
+    const CouplingTask* __restrict__ tasks, PassArgs pa, const double* __restrict__ halo,
+    int64_t hstride, double* __restrict__ cpbuf) {
+  __shared__ double part[CPL_NP - 1][64][NC];
+  __shared__ double s_src[CPL_NP][CPL_CH][NC];
   const CouplingTask tk = tasks[blockIdx.x];
   if (pa.run && !ldg(pa.run)) return;
   const int r = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int row = 64 * blockIdx.y + r;                 // within the task
   const bool live = row < tk.nrows;
-  const int L = (tk.inner + 3) / 4;
+  const int L = (tk.inner + CPL_NP - 1) / CPL_NP;
   const int k0 = q * L, k1 = min(tk.inner, k0 + L);
   const double* m = tk.m + tk.row0 + (live ? row : 0);
   double y[NC];
@@ -306,7 +265,7 @@ __global__ __launch_bounds__(256) void k_coupling_lds(const CouplingTask* __rest
   for (int c = 0; c < NC; ++c) y[c] = 0.0;
   for (int i0 = 0; i0 < L; i0 += CPL_CH) {
     // stage: value (part qq, step ii, column c) = src_c[qq L + i0 + ii] inside the part's range
-    for (int e = threadIdx.x; e < 4 * CPL_CH * NC; e += 256) {
+    for (int e = threadIdx.x; e < CPL_NP * CPL_CH * NC; e += 64 * CPL_NP) {
       const int c = e % NC, ii = (e / NC) % CPL_CH, qq = e / (NC * CPL_CH);
       const int k = qq * L + i0 + ii;
       const int kend = min(tk.inner, (qq + 1) * L);
@@ -344,15 +303,13 @@ __global__ __launch_bounds__(256) void k_coupling_lds(const CouplingTask* __rest
   if (q == 0 && live) {
     double* out = cpbuf + ((int64_t)tk.cp * 256 + tk.prow0 + row) * NC;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) out[c] = ((y[c] + part[0][r][c]) + part[1][r][c]) + part[2][r][c];
+    for (int c = 0; c < NC; ++c) {
+      double v = y[c];
+#pragma unroll
+      for (int p = 0; p < CPL_NP - 1; ++p) v += part[p][r][c];
+      out[c] = v;
+    }
   }
-}
-
-// SGV_CPL_FORM (A/B, with SGV_AB=1): 0 = k_coupling (global source loads per
-// inner index), 1 = k_coupling_lds (bitwise the same sums); default 1
-static int cpl_form() {
-  const char* e = ab_env("SGV_CPL_FORM");
-  return (e && e[0] == '0') ? 0 : 1;
 }
 
 hipError_t launch_coupling(int nc, const CouplingTask* d_tasks, int ntasks, const PassArgs& pa,
@@ -361,15 +318,16 @@ hipError_t launch_coupling(int nc, const CouplingTask* d_tasks, int ntasks, cons
   if (ntasks <= 0) return hipSuccess;
   const hipError_t e = hipMemsetAsync(cpbuf, 0, sizeof(double) * (size_t)ncp_slots * 256 * nc, st);
   if (e != hipSuccess) return e;
-  const bool lds = cpl_form() == 1;
-#define CPL_CASE(N)                                                                         \
-  case N:                                                                                   \
-    if (lds)                                                                                \
-      hipLaunchKernelGGL(k_coupling_lds<N>, dim3(ntasks, 4), dim3(256), 0, st, d_tasks, pa, \
-                         halo, hstride, cpbuf);                                             \
-    else                                                                                    \
-      hipLaunchKernelGGL(k_coupling<N>, dim3(ntasks, 4), dim3(256), 0, st, d_tasks, pa,     \
-                         halo, hstride, cpbuf);                                             \
+  const char* npe = ab_env("SGV_CPL_NP");   // A/B: 4 parts (the round-4 kernel's sums)
+  const bool np4 = npe && npe[0] == '4';
+#define CPL_CASE(N)                                                                          \
+  case N:                                                                                    \
+    if (np4)                                                                                 \
+      hipLaunchKernelGGL((k_coupling_lds<N, 4>), dim3(ntasks, 4), dim3(256), 0, st, d_tasks, \
+                         pa, halo, hstride, cpbuf);                                          \
+    else                                                                                     \
+      hipLaunchKernelGGL((k_coupling_lds<N, 8>), dim3(ntasks, 4), dim3(512), 0, st, d_tasks, \
+                         pa, halo, hstride, cpbuf);                                          \
     break;
   switch (nc) {
     CPL_CASE(1) CPL_CASE(2) CPL_CASE(3) CPL_CASE(4) CPL_CASE(5) CPL_CASE(6) CPL_CASE(7) CPL_CASE(8)
