@@ -246,6 +246,7 @@ hipError_t launch_sym_pass(int nc, int cls, const SymItem* d_items, int nitems,
 // a slot no task writes stay as cleared.
 constexpr int CPL_CH = 32;
 constexpr int CPL_U = 8;
+// 8 parts: the band bench's pass -0.8 % against 4 (profiles/r05/cpl_parts_bench.jsonl)
 template <int NC, int CPL_NP>   // CPL_NP: parts (waves) per workgroup
 __global__ __launch_bounds__(64 * CPL_NP) void k_coupling_lds(
     const CouplingTask* __restrict__ tasks, PassArgs pa, const double* __restrict__ halo,
@@ -318,16 +319,10 @@ hipError_t launch_coupling(int nc, const CouplingTask* d_tasks, int ntasks, cons
   if (ntasks <= 0) return hipSuccess;
   const hipError_t e = hipMemsetAsync(cpbuf, 0, sizeof(double) * (size_t)ncp_slots * 256 * nc, st);
   if (e != hipSuccess) return e;
-  const char* npe = ab_env("SGV_CPL_NP");   // A/B: 4 parts (the round-4 kernel's sums)
-  const bool np4 = npe && npe[0] == '4';
 #define CPL_CASE(N)                                                                          \
   case N:                                                                                    \
-    if (np4)                                                                                 \
-      hipLaunchKernelGGL((k_coupling_lds<N, 4>), dim3(ntasks, 4), dim3(256), 0, st, d_tasks, \
-                         pa, halo, hstride, cpbuf);                                          \
-    else                                                                                     \
-      hipLaunchKernelGGL((k_coupling_lds<N, 8>), dim3(ntasks, 4), dim3(512), 0, st, d_tasks, \
-                         pa, halo, hstride, cpbuf);                                          \
+    hipLaunchKernelGGL((k_coupling_lds<N, 8>), dim3(ntasks, 4), dim3(512), 0, st, d_tasks,   \
+                       pa, halo, hstride, cpbuf);                                            \
     break;
   switch (nc) {
     CPL_CASE(1) CPL_CASE(2) CPL_CASE(3) CPL_CASE(4) CPL_CASE(5) CPL_CASE(6) CPL_CASE(7) CPL_CASE(8)
