@@ -920,16 +920,23 @@ __global__ __launch_bounds__(256) void k_sym_finalize_strip1(
 // PAIRED (PKS = 8, the 5-8-column band walks): slot p holds column
 // 4 (p & 1) + (p >> 1), so the walk's lane n4 reads its columns n4 and 4 + n4
 // as one 16-B load
+// One thread per row: the column reads are coalesced over the threads, the
+// row is written as 16-B stores.
 template <int PKS, bool PAIRED = false>
 __global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpad,
                                               double* __restrict__ pk) {
   if (pa.run && !ldg(pa.run)) return;
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= mpad * PKS) return;
-  const int64_t i = t / PKS;
-  const int p = (int)(t % PKS);
-  const int c = PAIRED ? 4 * (p & 1) + (p >> 1) : p;
-  pk[t] = c < ncol ? pa.in[c][i] : 0.0;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= mpad) return;
+  double v[PKS];
+#pragma unroll
+  for (int p = 0; p < PKS; ++p) {
+    const int c = PAIRED ? 4 * (p & 1) + (p >> 1) : p;
+    v[p] = c < ncol ? pa.in[c][i] : 0.0;
+  }
+  d2* row = (d2*)(pk + i * PKS);
+#pragma unroll
+  for (int p = 0; p < PKS; p += 2) row[p / 2] = d2{v[p], v[p + 1]};
 }
 
 // ragged: some strip item stops short of its strip's widest (band blocks):
@@ -958,8 +965,7 @@ hipError_t launch_pk(const PassArgs& pa, int nc, int64_t mpad, double* d_pk, hip
                      bool paired) {
   if (nc < 1 || nc > 16) return hipErrorInvalidValue;
   const int pks = nc > 8 ? 16 : nc <= 4 ? 4 : 8;
-  const int64_t npk = mpad * pks;
-  const dim3 pg((unsigned)((npk + 255) / 256));
+  const dim3 pg((unsigned)((mpad + 255) / 256));
   if (pks == 4)
     hipLaunchKernelGGL(k_pack<4>, pg, dim3(256), 0, st, pa, nc, mpad, d_pk);
   else if (pks == 8 && paired)
