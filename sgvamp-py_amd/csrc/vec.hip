@@ -263,7 +263,7 @@ __device__ __forceinline__ bool em_partials(const ChunkDesc* __restrict__ chs, c
 #pragma unroll
         for (int l = 0; l < LM; ++l)
           if (l < a.nslab) {
-            tl[l] = -r2 * tb[2 + l];                         // :127 (tb: 1 / (2 (s_l + 1/g1)))
+            tl[l] = -r2 / 2 / tb[2 + l];                     // :127
             emax = (l == 0 || tl[l] > emax) ? tl[l] : emax;
           }
         double xi[LM];
@@ -271,12 +271,11 @@ __device__ __forceinline__ bool em_partials(const ChunkDesc* __restrict__ chs, c
 #pragma unroll
         for (int l = 0; l < LM; ++l)
           if (l < a.nslab) {
-            xi[l] = lam * om[l] * exp(tl[l] - emax) * tb[2 + MAXL + l];                 // :128
+            xi[l] = lam * om[l] * exp(tl[l] - emax) / tb[2 + MAXL + l];                 // :128
             sum_xi = (l == 0) ? xi[l] : sum_xi + xi[l];                                   // :129
           }
-        const double inv_xi = 1.0 / sum_xi;
         const double pi =
-            1.0 / (1.0 + (1 - lam) * exp(-r2 / 2 * a.gam1[k] - emax) * tb[1] * inv_xi);   // :131
+            1.0 / (1.0 + (1 - lam) * exp(-r2 / 2 * a.gam1[k] - emax) / tb[1] / sum_xi);   // :131
         const double pa = pi * a.a[k];
         avg = (k == 0) ? pa : avg + pa;
         // compile-time accumulator indices (a runtime acc[1 + nslab] puts the
@@ -285,7 +284,7 @@ __device__ __forceinline__ bool em_partials(const ChunkDesc* __restrict__ chs, c
         for (int v = 1; v < LM + 2; ++v) {
           const int l = v - 1;
           if (l < a.nslab)
-            acc[v] += pi * (xi[l] * inv_xi) * a.a[k];   // :136 numerator
+            acc[v] += pi * (xi[l] / sum_xi) * a.a[k];   // :136 numerator
           else if (l == a.nslab)
             acc[v] += pa;                               // :136 denominator
         }
@@ -334,15 +333,12 @@ __global__ __launch_bounds__(EM_THREADS) void k_em(const ChunkDesc* __restrict__
 __global__ __launch_bounds__(WAVE) void k_em_prep(EmArgs a, double* __restrict__ tab) {
   for (int k = threadIdx.x; k < a.K; k += WAVE) {
     double* tb = tab + k * EM_TAB;
-    // the per-cohort divisors of the step as reciprocals: the step multiplies
-    // (one reciprocal per cohort and loop instead of 2 L + 1 divisions per
-    // marker and cohort and step; within an ulp of the quotients)
     const double ginv = 1.0 / a.gam1[k];      // gam1invs (:125)
     tb[0] = ginv;
-    tb[1] = 1.0 / sqrt(ginv);                 // 1 / np.sqrt(gam1invs) (:131)
+    tb[1] = sqrt(ginv);                       // np.sqrt(gam1invs) (:131)
     for (int l = 0; l < MAXL; ++l) {
-      tb[2 + l] = l < a.nslab ? 0.5 / (a.sigmas[l] + ginv) : 1.0;               // (:127)
-      tb[2 + MAXL + l] = l < a.nslab ? 1.0 / sqrt(ginv + a.sigmas[l]) : 1.0;    // (:128)
+      tb[2 + l] = l < a.nslab ? a.sigmas[l] + ginv : 1.0;               // (:127)
+      tb[2 + MAXL + l] = l < a.nslab ? sqrt(ginv + a.sigmas[l]) : 1.0;   // (:128)
     }
   }
 }
