@@ -159,11 +159,11 @@ struct PassArgs {
   // next to its first descriptor load
   const int* run;
   // coupling sums of the panels next to a cut between coupled band pieces
-  // ([slot][256][ncol], SymPanel::cp), written by k_coupling before the finalize
+  // ([slot][256][ncol], SymPanel::cp), written by k_coupling_lds before the finalize
   const double* cpbuf;
 };
 
-// One task of k_coupling: up to 256 rows of one side of the coupling between
+// One task of k_coupling_lds: up to 256 rows of one side of the coupling between
 // band pieces gb and gb + 1 (C = R[tail nr rows of gb][head nc columns of gb + 1]):
 //   side 0 (rows = gb's tail):   y[i] = sum_j C[i][j] p_{gb+1}[j]   (m = C^T, nc x nr)
 //   side 1 (rows = gb+1's head): y[j] = sum_i C[i][j] p_{gb}[n - nr + i] (m = C, nr x nc)

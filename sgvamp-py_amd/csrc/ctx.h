@@ -90,7 +90,7 @@ struct LdPlan {
   // multiply-adds per column of a pass: every stored element (row part) plus the
   // packed off-diagonal-block ones again (their transposes)
   double mac_elems = 0.0;
-  // coupled band pieces: k_coupling tasks, panel slots of PassArgs::cpbuf, and
+  // coupled band pieces: k_coupling_lds tasks, panel slots of PassArgs::cpbuf, and
   // the halo this rank sends (head of its first block, tail of its last) when a
   // coupling spans two ranks -- the same decision on every rank (all ranks know
   // every coupling and the block partition)
