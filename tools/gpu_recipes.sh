@@ -10,6 +10,8 @@
 #   configs TAG                  one bench line per BASELINE.json configuration, the band line,
 #                                the N = 8 share and the 8-rank rehearsal
 #   ab      TAG VAR "v0 v1 .." SHAPES NCOLS [bench args]   an SGV_AB switch (gpu_ab_multi.sh)
+#   stall   TAG [bench args]     VMEM latency (INST_LEVEL / INSTS), active-instruction mix, LDS and
+#                                TA back-pressure counters, two --pmc passes (kernel_pmc_table.py)
 #   walkpmc TAG                  band walks vs strips (SGV_BAND_WALK 8 / 0) at M = 1e6, bw = 1,000,
 #                                4 and 8 columns: clock/stall, LDS and HBM-byte --pmc passes
 #   gate50  TAG [K]              the north star's own 50-iteration gate (SGV_FULL_GATE=1)
@@ -34,6 +36,12 @@ case $recipe in
   clock)
     P="GRBM_GUI_ACTIVE GRBM_COUNT SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY"
     tools/gpu_steps.sh "clock_$T:300:cd /tmp && timeout -s KILL 280 rocprofv3 --pmc $P -d $R/gpurun_out/clock_$T -o pmc --output-format csv -- python3 $R/bench.py $B --no-files $*" ;;
+  stall)
+    P1="GRBM_GUI_ACTIVE SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
+    P2="GRBM_GUI_ACTIVE GRBM_TA_BUSY TA_ADDR_STALLED_BY_TC_CYCLES TA_DATA_STALLED_BY_TC_CYCLES SQ_VMEM_TA_ADDR_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL SQ_LDS_DATA_FIFO_FULL SQ_INST_LEVEL_LDS SQ_INSTS_LDS SQ_WAVE_CYCLES"
+    tools/gpu_steps.sh \
+      "stall1_$T:120:cd /tmp && timeout -s KILL 100 rocprofv3 --pmc $P1 -d $R/gpurun_out/stall1_$T -o pmc --output-format csv -- python3 $R/bench.py $B --no-files $*" \
+      "stall2_$T:120:cd /tmp && timeout -s KILL 100 rocprofv3 --pmc $P2 -d $R/gpurun_out/stall2_$T -o pmc --output-format csv -- python3 $R/bench.py $B --no-files $*" ;;
   walkpmc)
     P1="GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS"
     P2="GRBM_GUI_ACTIVE SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VALU"
