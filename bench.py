@@ -334,6 +334,25 @@ def cpu_baseline(eng, args, ref_flags, recs, x0):
     return out
 
 
+def flags_label(args, prior):
+    """The reference CLI flags (src/main.py:27-50) this run uses, naming every
+    one that differs from the CLI's default."""
+    diff = []
+    if args.band or args.prior != "cli":
+        diff.append("--prior-vars %s --prior-probs %s (%s; the CLI default 0,1 / 0.99,0.01 "
+                    "collapses the reference algorithm on this data, DESIGN.md section 6)" % (
+                        ",".join("%.6g" % x for x in prior["prior_vars"]),
+                        ",".join("%.6g" % x for x in prior["prior_probs"]),
+                        "the simulated mixture" if not args.band else "the band problem's mixture"))
+    if args.ridge:
+        diff.append("--s %g" % args.ridge)
+    if args.lmmse_damp:
+        diff.append("--lmmse-damp 1")
+    if not diff:
+        return "reference CLI default flags (src/main.py:27-50)"
+    return ("reference CLI flags (src/main.py:27-50) at their defaults except " + ", ".join(diff))
+
+
 def main():
     args = parse()
     from launch import relaunch
@@ -437,6 +456,12 @@ def main():
     tm = eng.timers()
     xs = eng.exchange_stats()
     xs_all = comm.allgather(xs) if world > 1 else [xs]
+    # each rank's view of the exchange (sgv_comm_info: RCCL's own rank count and
+    # this rank in it, the HIP device and its PCI bus id) and its exact-CG host
+    # wait, so an N-GPU line proves which devices and which communicator ran
+    ci = eng.comm_info()
+    ci.update(rank=rank, host_wait_ms_per_step=xs["host_wait_ms"] / args.steps)
+    ci_all = comm.allgather(ci) if world > 1 else [ci]
     # this box's own streaming-read rate (after the timed region; context only:
     # the roofline peak stays the guide's 8 TB/s); the slowest rank's
     box_bw = None
@@ -508,12 +533,10 @@ def main():
                  "(Bin(2,0.4) genotypes, 50%% causal, h2=0.8), seed %d" % args.seed),
         "config": {
             "workload": "%s: K=%d cohort(s) %s, M=%d markers in %d LD blocks "
-                        "of %d, N=%d per cohort, reference CLI default flags, output files written "
-                        "each iteration, prior %s %s" % (cname, K, "with one LD matrix each"
-                                                         if args.distinct_ld else "sharing one LD",
-                                                         eng.M, len(eng.block_sizes),
-                                                         max(eng.block_sizes), args.nsamp,
-                                                         prior["prior_vars"], prior["prior_probs"]),
+                        "of %d, N=%d per cohort, output files written each iteration, %s"
+                        % (cname, K, "with one LD matrix each" if args.distinct_ld
+                           else "sharing one LD", eng.M, len(eng.block_sizes),
+                           max(eng.block_sizes), args.nsamp, flags_label(args, prior)),
             "K": K, "M": eng.M, "ld_blocks": len(eng.block_sizes),
             "block_size": args.block_size if not args.band else max(eng.block_sizes),
             "band": args.band,
@@ -587,6 +610,17 @@ def main():
             # stop test (HIP events; the slowest rank's)
             "host_wait_ms_per_step": max(x["host_wait_ms"] for x in xs_all) / steps,
             "K_times_M": K * eng.M,
+            # who ran: RCCL's own count of ranks in the communicator (None unless
+            # the transport is RCCL), and per rank its place in the communicator,
+            # HIP device, PCI bus id and exact-CG host wait
+            "transport_note": {"rccl": "RCCL all-gathers (ncclAllGather) on each rank's device",
+                               "host": "host exchange: per-block partials all-gathered by the "
+                                       "host communicator (a rehearsal when --share-device puts "
+                                       "every rank on one device; not RCCL)",
+                               None: "one rank, no communicator"}[xs["transport"]],
+            "rccl_ranks": ci_all[0]["comm_ranks"] if xs["transport"] == "rccl" else None,
+            "ranks": ci_all,
+            "distinct_devices": len({c["pci_bus_id"] for c in ci_all}),
         },
         "ld_passes_per_step": passes / steps,
         "effective_ld_gbps_end_to_end": passes * ld_bytes_total / dt / 1e9,

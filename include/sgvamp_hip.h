@@ -36,6 +36,12 @@ extern "C" {
 #define SGV_ERR_RCCL (-3)
 #define SGV_ERR_STATE (-4)
 
+/* ABI revision of this header.  2: sgv_timers / sgv_exchange_stats take the
+ * caller's buffer length (cap), sgv_comm_info added.  An integrator checks
+ * sgv_abi_version() == SGV_ABI_VERSION before binding the rest. */
+#define SGV_ABI_VERSION 2
+int sgv_abi_version(void);
+
 #define SGV_MAX_COHORTS 1024 /* cohorts per context (the reference's K is its MPI
                                 world size); the LMMSE batches them 8 at a time
                                 (16 CG right-hand sides per LD pass), the marker
@@ -374,8 +380,11 @@ int sgv_cg_solve(sgv_ctx* ctx, int ld, int ncol, const double* c1, const double*
  * stored element, and its transpose part over the packed elements right of
  * each panel's diagonal block), t[7] / t[8] / t[9] = flops / kernel ms / passes
  * of the 9..16-column passes (f64 16x16x4 MFMA: their bound is the matrix core).
+ * Writes min(cap, SGV_TIMERS_N) values (a caller built against a shorter list
+ * passes its own length and gets that prefix); cap < 0 is an error.
  * reset != 0 zeroes. */
-int sgv_timers(sgv_ctx* ctx, double* t10, int reset);
+#define SGV_TIMERS_N 10
+int sgv_timers(sgv_ctx* ctx, double* t, int cap, int reset);
 /* Cross-rank exchange counters since the last reset (the bcast/all-gather of
  * src/sgvamp.py:228-233 and the CG/EM scalar reductions that replace it):
  * out[0] = all-gathers issued, out[1] = ms spent in them (RCCL: HIP events
@@ -391,9 +400,22 @@ int sgv_timers(sgv_ctx* ctx, double* t10, int reset);
  * its passes, which the host enqueues once it has read the stop test (HIP
  * events), out[12] = the latency's source (0 default 25 us, 1 env
  * SGV_XCHG_LAT_US of rank 0, 2 sgv_exchange_probe), out[13] = 1 if the
- * replicated loop can run (K <= 32, <= 128 blocks in all).  reset != 0 zeroes
- * out[0..2], out[6..7] and out[11]. */
-int sgv_exchange_stats(sgv_ctx* ctx, double* out14, int reset);
+ * replicated loop can run (K <= 32, <= 128 blocks in all).  Writes
+ * min(cap, SGV_EXCHANGE_STATS_N) values; cap < 0 is an error.  reset != 0
+ * zeroes out[0..2], out[6..7] and out[11]. */
+#define SGV_EXCHANGE_STATS_N 14
+int sgv_exchange_stats(sgv_ctx* ctx, double* out, int cap, int reset);
+
+/* Who this context's exchange talks to, for a launch to prove its topology:
+ * out[0] = transport (0 none, 1 RCCL, 2 host exchange), out[1] = ranks in the
+ * communicator (RCCL: ncclCommCount; host: the nranks given), out[2] = this
+ * rank in it (RCCL: ncclCommUserRank), out[3] = the HIP device the context runs
+ * on (RCCL: ncclCommCuDevice), out[4] = the nranks the context was given.
+ * Writes min(cap, SGV_COMM_INFO_N) values; pci_bus_id (if not null) receives
+ * the device's PCI bus id ("0000:xx:00.0", NUL-terminated, at most pci_len
+ * bytes). */
+#define SGV_COMM_INFO_N 5
+int sgv_comm_info(sgv_ctx* ctx, int* out, int cap, char* pci_bus_id, int pci_len);
 
 /* Measure the per-all-gather latency of this job's exchange (the CG's ordered
  * reduction of 16 values: per-block sums, all-gather, ordered total; `reps`

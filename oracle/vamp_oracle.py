@@ -306,6 +306,40 @@ class CoupledLD:
         return (1 - self.s) * self.matvec_R(v) + self.s * v
 
 
+def _oracle_workers():
+    """Threads for the host panel products: the job's CPU share
+    (OMP_NUM_THREADS: 16 on the MI355X pool, where os.cpu_count() shows the
+    whole machine), at most 16; SGV_ORACLE_THREADS overrides."""
+    import os
+
+    v = os.environ.get("SGV_ORACLE_THREADS") or os.environ.get("OMP_NUM_THREADS")
+    try:
+        n = int(v) if v else (os.cpu_count() or 1)
+    except ValueError:
+        n = 1
+    return max(1, min(16, n))
+
+
+class _blas_single_thread:
+    """One BLAS thread per call while the pool runs (threadpoolctl when present;
+    otherwise BLAS keeps its own setting -- the sums are the same, only slower)."""
+
+    def __enter__(self):
+        try:
+            from threadpoolctl import threadpool_limits
+
+            self._cm = threadpool_limits(limits=1, user_api="blas")
+            self._cm.__enter__()
+        except Exception:
+            self._cm = None
+        return self
+
+    def __exit__(self, *exc):
+        if self._cm is not None:
+            self._cm.__exit__(*exc)
+        return False
+
+
 class PanelLD:
     """Block-diagonal LD held as the upper triangle of each block in panels of
     ``H`` rows -- panel g of a block stores rows r0 = H*g .. r0+h-1 over columns
@@ -335,17 +369,34 @@ class PanelLD:
         self.blocks.append((off, n, panels))
         self.sizes.append(n)
 
+    def _block_product(self, blk, V, Y):
+        off, n, panels = blk
+        Vb, Yb = V[off:off + n], Y[off:off + n]
+        for g, P in enumerate(panels):
+            r0 = g * self.H
+            h = P.shape[0]
+            Yb[r0:r0 + h] += P @ Vb[r0:]                     # rows of the panel
+            if P.shape[1] > h:
+                Yb[r0 + h:] += P[:, h:].T @ Vb[r0:r0 + h]    # their transposes
+
     def matmat_R(self, V):
+        """Blocks are independent (each writes only its own rows), so they run
+        on a thread pool (numpy releases the GIL in BLAS), one BLAS thread per
+        call: the order of the additions inside a block does not depend on the
+        worker count.  A full-size pass over 63.5 GB then streams at the host's
+        memory rate instead of one core's (the north-star gate in the driver's
+        GPU suite)."""
         V = np.asarray(V, dtype=np.float64)
         Y = np.zeros_like(V)
-        for off, n, panels in self.blocks:
-            Vb, Yb = V[off:off + n], Y[off:off + n]
-            for g, P in enumerate(panels):
-                r0 = g * self.H
-                h = P.shape[0]
-                Yb[r0:r0 + h] += P @ Vb[r0:]                     # rows of the panel
-                if P.shape[1] > h:
-                    Yb[r0 + h:] += P[:, h:].T @ Vb[r0:r0 + h]    # their transposes
+        nw = _oracle_workers()
+        if nw <= 1 or len(self.blocks) < 2:
+            for blk in self.blocks:
+                self._block_product(blk, V, Y)
+            return Y
+        from concurrent.futures import ThreadPoolExecutor
+
+        with _blas_single_thread(), ThreadPoolExecutor(nw) as ex:
+            list(ex.map(lambda blk: self._block_product(blk, V, Y), self.blocks))
         return Y
 
     def matvec_R(self, v):

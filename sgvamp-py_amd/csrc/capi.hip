@@ -706,11 +706,15 @@ extern "C" int sgv_outputs_wait(sgv_ctx* c, int slot, double** data) {
   return SGV_OK;
 }
 
-extern "C" int sgv_timers(sgv_ctx* c, double* t6, int reset) {
+extern "C" int sgv_abi_version(void) { return SGV_ABI_VERSION; }
+
+extern "C" int sgv_timers(sgv_ctx* c, double* dst, int cap, int reset) {
   ENTER(c);
+  if (cap < 0 || (cap > 0 && !dst)) return fail(c, SGV_ERR_ARG, "sgv_timers: bad buffer");
   CHK(stream_wait(c));
   resolve_timers(c);
-  if (t6) {
+  {
+    double t6[SGV_TIMERS_N];
     t6[0] = c->ld_ms;
     t6[1] = c->ld_launches;
     t6[2] = c->ld_bytes;
@@ -721,6 +725,7 @@ extern "C" int sgv_timers(sgv_ctx* c, double* t6, int reset) {
     t6[7] = c->ld_flops_wide;
     t6[8] = c->ld_ms_wide;
     t6[9] = c->ld_launches_wide;
+    for (int i = 0; i < std::min(cap, SGV_TIMERS_N); ++i) dst[i] = t6[i];
   }
   if (reset) {
     c->ld_ms = c->ld_launches = c->rhs_bytes = c->ld_bytes = c->dense_bytes = c->aux_bytes = 0.0;

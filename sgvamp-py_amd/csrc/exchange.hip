@@ -314,12 +314,13 @@ extern "C" int sgv_comm_init_host(sgv_ctx* c, int nranks, int rank, const int* n
   return em_rep_setup(c, nblk_per_rank);
 }
 
-extern "C" int sgv_exchange_stats(sgv_ctx* c, double* out, int reset) {
+extern "C" int sgv_exchange_stats(sgv_ctx* c, double* dst, int cap, int reset) {
   ENTER(c);
-  if (!out) return fail(c, SGV_ERR_ARG, "sgv_exchange_stats: out is null");
+  if (cap < 0 || (cap > 0 && !dst)) return fail(c, SGV_ERR_ARG, "sgv_exchange_stats: bad buffer");
   CHK(stream_wait(c));
   resolve_timers(c);
   const bool cm = c->comm || c->host_ag;
+  double out[SGV_EXCHANGE_STATS_N];
   out[0] = c->xchg_n;
   out[1] = c->xchg_ms;
   out[2] = c->xchg_bytes;
@@ -334,11 +335,31 @@ extern "C" int sgv_exchange_stats(sgv_ctx* c, double* out, int reset) {
   out[11] = c->host_wait_ms;
   out[12] = (double)c->xlat_src;
   out[13] = c->em_rep ? 1.0 : 0.0;
+  for (int i = 0; i < std::min(cap, SGV_EXCHANGE_STATS_N); ++i) dst[i] = out[i];
   if (reset) {
     c->xchg_n = c->xchg_ms = c->xchg_bytes = 0.0;
     c->em_loops_rep = c->em_loops_ps = 0.0;
     c->host_wait_ms = 0.0;
   }
+  return SGV_OK;
+}
+
+extern "C" int sgv_comm_info(sgv_ctx* c, int* dst, int cap, char* pci_bus_id, int pci_len) {
+  ENTER(c);
+  if (cap < 0 || (cap > 0 && !dst) || (pci_bus_id && pci_len < 1))
+    return fail(c, SGV_ERR_ARG, "sgv_comm_info: bad buffer");
+  int out[SGV_COMM_INFO_N] = {c->comm ? 1 : c->host_ag ? 2 : 0, c->nranks, c->rank, c->dev,
+                              c->nranks};
+  if (c->comm) {
+    NCCLCHK(ncclCommCount(c->comm, &out[1]));
+    NCCLCHK(ncclCommUserRank(c->comm, &out[2]));
+    NCCLCHK(ncclCommCuDevice(c->comm, &out[3]));
+  } else if (!c->host_ag) {
+    out[1] = 1;
+    out[2] = 0;
+  }
+  for (int i = 0; i < std::min(cap, SGV_COMM_INFO_N); ++i) dst[i] = out[i];
+  if (pci_bus_id) HIPCHK(hipDeviceGetPCIBusId(pci_bus_id, pci_len, out[3]));
   return SGV_OK;
 }
 

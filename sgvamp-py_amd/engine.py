@@ -90,9 +90,14 @@ class Engine:
                 uid = hb.unique_id() if self.rank == 0 else None
                 uid = self.comm.bcast(uid, root=0)
                 self.ctx.sgv_comm_init(self.nranks, self.rank, uid, hb.iptr(counts))
-            # this job's all-gather latency, the EM loop's cost-model parameter
-            # (the same on every rank; an SGV_XCHG_LAT_US setting is replaced)
-            if os.environ.get("SGV_XCHG_LAT_US") is None:
+            # this job's all-gather latency, the EM loop's cost-model parameter.
+            # The probe is collective, so the decision must be the same on every
+            # rank: the library took rank 0's SGV_XCHG_LAT_US (if any) at
+            # communicator set-up, and its latency source -- rank 0's, identical
+            # on every rank -- says whether to probe ("default": rank 0 set no
+            # value) or keep rank 0's setting.  A rank's own environment decides
+            # nothing here.
+            if self.exchange_stats()["latency_source"] == "default":
                 self.exchange_probe(10)
 
     # ---- inputs ----------------------------------------------------------
@@ -362,8 +367,8 @@ class Engine:
         return X, it, info
 
     def timers(self, reset=False):
-        t = np.zeros(10)
-        self.ctx.sgv_timers(hb.dptr(t), int(bool(reset)))
+        t = np.zeros(hb.TIMERS_N)
+        self.ctx.sgv_timers(hb.dptr(t), len(t), int(bool(reset)))
         return dict(ld_ms=t[0], ld_launches=int(t[1]), ld_bytes=t[2], rhs_bytes=t[3],
                     dense_bytes=t[4], aux_bytes=t[5], ld_flops=t[6], wide_flops=t[7],
                     wide_ms=t[8], wide_launches=int(t[9]))
@@ -372,8 +377,8 @@ class Engine:
         """Cross-rank exchange counters (sgv_exchange_stats): all-gathers issued,
         ms in them, bytes contributed, the EM loops' modes and the cost model's
         last decision, the exact-CG host waits."""
-        t = np.zeros(14)
-        self.ctx.sgv_exchange_stats(hb.dptr(t), int(bool(reset)))
+        t = np.zeros(hb.EXCHANGE_STATS_N)
+        self.ctx.sgv_exchange_stats(hb.dptr(t), len(t), int(bool(reset)))
         return dict(allgathers=int(t[0]), ms=float(t[1]), bytes=float(t[2]),
                     em_mode={1: "replicated", 0: "per-step", -1: None}[int(t[3])],
                     latency_us=float(t[4]),
@@ -384,6 +389,17 @@ class Engine:
                     em_pred_replicated_us=float(t[8]), em_pred_per_step_us=float(t[9]),
                     em_pred_steps=float(t[10]), host_wait_ms=float(t[11]),
                     em_replicated_possible=bool(t[13]))
+
+    def comm_info(self):
+        """Who the exchange talks to (sgv_comm_info): transport, ranks in the
+        communicator and this rank in it (RCCL's own ncclCommCount /
+        ncclCommUserRank), the HIP device and its PCI bus id."""
+        t = np.zeros(hb.COMM_INFO_N, dtype=np.int32)
+        pci = ctypes.create_string_buffer(64)
+        self.ctx.sgv_comm_info(hb.iptr(t), len(t), pci, len(pci))
+        return dict(transport={1: "rccl", 2: "host", 0: None}[int(t[0])], comm_ranks=int(t[1]),
+                    comm_rank=int(t[2]), device=int(t[3]), nranks=int(t[4]),
+                    pci_bus_id=pci.value.decode(errors="replace"))
 
     def exchange_probe(self, reps=20):
         """Measure the exchange's per-all-gather latency (collective) and make the

@@ -22,6 +22,8 @@ MLE_NOT_CONVERGED, MLE_NEGATIVE = 1, 2
 OUT_SLOTS = 3
 MAX_COHORTS = 1024
 MAX_SLABS = 8
+ABI_VERSION = 2          # the header's SGV_ABI_VERSION this binding is typed against
+TIMERS_N, EXCHANGE_STATS_N, COMM_INFO_N = 10, 14, 5
 
 _c_int_p = ctypes.POINTER(ctypes.c_int)
 _c_i64_p = ctypes.POINTER(ctypes.c_int64)
@@ -79,8 +81,10 @@ _SIGS = {
     "sgv_ld_matvec": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, _c_dbl_p],
     "sgv_cg_solve": [_vp, ctypes.c_int, ctypes.c_int, _c_dbl_p, _c_dbl_p, _c_dbl_p, _c_dbl_p,
                      ctypes.c_int, ctypes.c_double, _c_int_p, _c_int_p],
-    "sgv_timers": [_vp, _c_dbl_p, ctypes.c_int],
-    "sgv_exchange_stats": [_vp, _c_dbl_p, ctypes.c_int],
+    "sgv_abi_version": [],
+    "sgv_timers": [_vp, _c_dbl_p, ctypes.c_int, ctypes.c_int],
+    "sgv_exchange_stats": [_vp, _c_dbl_p, ctypes.c_int, ctypes.c_int],
+    "sgv_comm_info": [_vp, _c_int_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int],
     "sgv_exchange_probe": [_vp, ctypes.c_int, _c_dbl_p],
     "sgv_em_cost_model": [ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_double,
                           _c_dbl_p],
@@ -141,6 +145,9 @@ def load(path=LIB_PATH, strict=True):
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    if strict and lib.sgv_abi_version() != ABI_VERSION:
+        raise HipError("%s has ABI version %d, this binding expects %d: rebuild with "
+                       "`make -C sgvamp-py_amd/csrc`" % (path, lib.sgv_abi_version(), ABI_VERSION))
     _lib = lib
     return lib
 

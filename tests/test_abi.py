@@ -50,7 +50,9 @@ def test_binding_constants_match_header():
     defs = {m.group(1): int(m.group(2))
             for m in re.finditer(r"^#define (SGV_\w+)\s+\(?(-?\d+)\)?", text, flags=re.M)}
     pairs = {"SGV_OK": hb.SGV_OK, "SGV_MAX_COHORTS": hb.MAX_COHORTS,
-             "SGV_MAX_SLABS": hb.MAX_SLABS, "SGV_LMMSE_NOUT": hb.LMMSE_NOUT}
+             "SGV_MAX_SLABS": hb.MAX_SLABS, "SGV_LMMSE_NOUT": hb.LMMSE_NOUT,
+             "SGV_ABI_VERSION": hb.ABI_VERSION, "SGV_TIMERS_N": hb.TIMERS_N,
+             "SGV_EXCHANGE_STATS_N": hb.EXCHANGE_STATS_N, "SGV_COMM_INFO_N": hb.COMM_INFO_N}
     for n in ("R", "R1", "XHAT1", "XHAT2", "SIG2U", "X0"):
         pairs["SGV_VEC_" + n] = getattr(hb, "VEC_" + n)
     for n in ("TRSIGMA2", "ALPHA2", "GAM1", "Z", "TRRSIGMA2", "GAMW", "XR", "XRX"):
@@ -62,6 +64,13 @@ def test_binding_constants_match_header():
         pairs["SGV_MLE_" + n] = getattr(hb, "MLE_" + n)
     for name, value in pairs.items():
         assert defs[name] == value, (name, defs[name], value)
+
+
+def test_abi_version():
+    """The library reports the header's ABI revision (no device needed)."""
+    import hip_backend as hb
+
+    assert hb.load().sgv_abi_version() == hb.ABI_VERSION
 
 
 def test_library_is_gfx950_only():

@@ -159,6 +159,13 @@ def test_sharded_bench_equals_one_rank(name, flags, tmp_path):
                              else "per-step")
     assert x8["em_loops"]["replicated"] + x8["em_loops"]["per_step"] >= 2
     assert x8["host_wait_ms_per_step"] >= 0
+    # the line says who ran: the host transport labelled
+    # as such, no RCCL rank count, every rank on the one device with its own wait
+    assert x8["rccl_ranks"] is None and "not RCCL" in x8["transport_note"]
+    assert [r["rank"] for r in x8["ranks"]] == list(range(8))
+    assert all(r["transport"] == "host" and r["comm_ranks"] == 8 and r["comm_rank"] == r["rank"]
+               and r["device"] == 0 and r["host_wait_ms_per_step"] >= 0 for r in x8["ranks"])
+    assert x8["distinct_devices"] == 1 and x1["ranks"][0]["comm_ranks"] == 1
     _log(name, "eight-rank exchange", x8)
     files = sorted(f for f in os.listdir(tmp_path / "one") if f.endswith(".bin"))
     K = one["config"]["K"]

@@ -85,9 +85,30 @@ def _run_case_files(name, out, exchange):
             em_prior_maxit=f["em_prior_maxit"], learn_gamw=f["learn_gamw"],
             lmmse_damp=f["lmmse_damp"], prior_update=f["prior_update"],
             update_prior_from=f["update_prior_from"])
+    info = v.engine.comm_info()
+    _short_buffers(v.engine)
     v.engine.close()
-    return {fn: open(os.path.join(out, fn), "rb").read() for fn in sorted(os.listdir(out))
-            if fn.endswith(".bin")}
+    files = {fn: open(os.path.join(out, fn), "rb").read() for fn in sorted(os.listdir(out))
+             if fn.endswith(".bin")}
+    return files, info
+
+
+def _short_buffers(eng):
+    """ABI revision 2: a caller built against a shorter list
+    passes its own length and the library writes that prefix only."""
+    import numpy as np
+
+    import hip_backend as hb
+
+    for fn, n in (("sgv_exchange_stats", hb.EXCHANGE_STATS_N), ("sgv_timers", hb.TIMERS_N)):
+        full = np.zeros(n)
+        getattr(eng.ctx, fn)(hb.dptr(full), n, 0)
+        buf = np.full(n + 4, -7.25)
+        getattr(eng.ctx, fn)(hb.dptr(buf), 6, 0)          # round 5's 6-double buffer
+        assert (buf[6:] == -7.25).all(), fn
+        np.testing.assert_array_equal(buf[:6], full[:6])
+    with pytest.raises(hb.HipError):
+        eng.ctx.sgv_timers(hb.dptr(np.zeros(1)), -1, 0)
 
 
 @pytest.mark.gpu
@@ -98,14 +119,19 @@ def test_one_rank_exchange_rehearsal_bitwise(name, tmp_path):
     the host exchange likewise.  Both must leave every output file bitwise
     identical to the run without a communicator."""
     (tmp_path / "none").mkdir()
-    base = _run_case_files(name, tmp_path / "none", None)
+    base, info = _run_case_files(name, tmp_path / "none", None)
+    assert info["transport"] is None and info["comm_ranks"] == 1
     for ex in ("rccl", "host"):
         d = tmp_path / ex
         d.mkdir()
-        got = _run_case_files(name, d, ex)
+        got, info = _run_case_files(name, d, ex)
         assert got.keys() == base.keys() and len(base) > 0
         for fn in base:
             assert got[fn] == base[fn], (ex, fn)
+        # the communicator's own view: RCCL counts one rank (ncclCommCount), this
+        # rank is its rank 0 on HIP device 0, whose PCI bus id is reported
+        assert info["transport"] == ex and info["comm_ranks"] == 1 and info["comm_rank"] == 0, info
+        assert info["device"] == 0 and info["nranks"] == 1 and len(info["pci_bus_id"]) >= 7, info
 
 
 @pytest.mark.gpu
