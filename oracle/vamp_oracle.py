@@ -306,6 +306,29 @@ class CoupledLD:
         return (1 - self.s) * self.matvec_R(v) + self.s * v
 
 
+_PANEL_LIB = []
+
+
+def _panel_lib():
+    """oracle/libpanel_ld.so (oracle/panel_ld.c, built by oracle/Makefile): the
+    same block product in C, ~3x NumPy's tall-skinny GEMMs per core; None when
+    it is not built (the NumPy form below is the same operator)."""
+    if not _PANEL_LIB:
+        import ctypes
+        import os
+
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpanel_ld.so")
+        lib = None
+        if os.path.exists(path) and os.environ.get("SGV_ORACLE_NUMPY") != "1":
+            lib = ctypes.CDLL(path)
+            lib.oracle_panel_block_matmat.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                                                      ctypes.c_int, ctypes.c_void_p,
+                                                      ctypes.c_void_p]
+            lib.oracle_panel_block_matmat.restype = ctypes.c_int
+        _PANEL_LIB.append(lib)
+    return _PANEL_LIB[0]
+
+
 def _oracle_workers():
     """Threads for the host panel products: the job's CPU share
     (OMP_NUM_THREADS: 16 on the MI355X pool, where os.cpu_count() shows the
@@ -372,6 +395,19 @@ class PanelLD:
     def _block_product(self, blk, V, Y):
         off, n, panels = blk
         Vb, Yb = V[off:off + n], Y[off:off + n]
+        lib = _panel_lib()
+        if lib is not None and V.shape[1] <= 16:
+            import ctypes
+
+            Vc = np.ascontiguousarray(Vb)
+            Yc = np.empty_like(Vc)
+            ptrs = (ctypes.c_void_p * len(panels))(*[P.ctypes.data for P in panels])
+            rc = lib.oracle_panel_block_matmat(n, self.H, ptrs, Vc.shape[1], Vc.ctypes.data,
+                                               Yc.ctypes.data)
+            if rc != 0:
+                raise RuntimeError("oracle_panel_block_matmat failed")
+            Yb[...] = Yc
+            return
         for g, P in enumerate(panels):
             r0 = g * self.H
             h = P.shape[0]
