@@ -10,3 +10,12 @@ for p in (ROOT, PKG):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+
+
+def pytest_runtest_logreport(report):
+    """SGV_TEST_TIMES=<file>: append each test's call time as it finishes (the
+    GPU suite's budget is planned from these; a run cut off still leaves them)."""
+    path = os.environ.get("SGV_TEST_TIMES")
+    if path and report.when == "call":
+        with open(path, "a") as f:
+            f.write("%.2f %s %s\n" % (report.duration, report.outcome, report.nodeid))

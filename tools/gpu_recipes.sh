@@ -23,9 +23,10 @@ B="--steps 5 --warmup 2 --cpu-baseline off --read-bw 0"
 case $recipe in
   suite)
     SEL=${*:-tests}
-    exec_steps=("gputests_$T:1000:python -u -m pytest $SEL -m gpu -x -q -p no:cacheprovider --timeout 600 --timeout-method thread -rs"
+    exec_steps=("gputests_$T:${SUITE_LIMIT:-1000}:SGV_TEST_TIMES=gpurun_out/testtimes_$T.txt python -u -m pytest $SEL -m gpu -x -q -p no:cacheprovider --timeout 900 --timeout-method thread -rs --durations=40"
                 "smoke_$T:300:python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'"
                 "bench_$T:300:python bench.py")
+    [ -n "$NO_BENCH" ] && unset 'exec_steps[2]' 
     tools/gpu_steps.sh "${exec_steps[@]}" ;;
   trace)
     tools/gpu_steps.sh "trace_$T:400:cd /tmp && rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_$T -o bench --output-format csv -- python3 $R/bench.py $B $*" ;;
