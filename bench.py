@@ -604,7 +604,13 @@ def main():
                          "predicted_steps": xs["em_pred_steps"],
                          "predicted_replicated_us": xs["em_pred_replicated_us"],
                          "predicted_per_step_us": xs["em_pred_per_step_us"],
-                         "replicated_possible": xs["em_replicated_possible"]},
+                         "replicated_possible": xs["em_replicated_possible"],
+                         # the device-driven EM loops as they ran (HIP events), the
+                         # slowest rank's mean per loop, to check the prediction
+                         "measured_us_per_loop": (max(x["em_ms"] / max(x["em_loops_timed"], 1)
+                                                      for x in xs_all) * 1e3
+                                                  if xs["em_loops_timed"] else None),
+                         "loops_timed": xs["em_loops_timed"]},
             # exact CG column sets: the device's idle time between an iteration's
             # p update and its passes, which the host enqueues after reading the
             # stop test (HIP events; the slowest rank's)

@@ -400,10 +400,12 @@ int sgv_timers(sgv_ctx* ctx, double* t, int cap, int reset);
  * its passes, which the host enqueues once it has read the stop test (HIP
  * events), out[12] = the latency's source (0 default 25 us, 1 env
  * SGV_XCHG_LAT_US of rank 0, 2 sgv_exchange_probe), out[13] = 1 if the
- * replicated loop can run (K <= 32, <= 128 blocks in all).  Writes
- * min(cap, SGV_EXCHANGE_STATS_N) values; cap < 0 is an error.  reset != 0
- * zeroes out[0..2], out[6..7] and out[11]. */
-#define SGV_EXCHANGE_STATS_N 14
+ * replicated loop can run (K <= 32, <= 128 blocks in all), out[14] / out[15] =
+ * ms / count of the device-driven EM prior loops (HIP events from the loop's
+ * first enqueue to its last step: the cost the model predicts in out[8..9]).
+ * Writes min(cap, SGV_EXCHANGE_STATS_N) values; cap < 0 is an error.  reset != 0
+ * zeroes out[0..2], out[6..7], out[11] and out[14..15]. */
+#define SGV_EXCHANGE_STATS_N 16
 int sgv_exchange_stats(sgv_ctx* ctx, double* out, int cap, int reset);
 
 /* Who this context's exchange talks to, for a launch to prove its topology:

@@ -376,9 +376,17 @@ def launch_from_env(environ=None):
         # the global rank is the node-local one only on a one-node world: the
         # launcher says so (node-local size = world size), or -- RANK/WORLD_SIZE
         # launches that set no LOCAL_WORLD_SIZE -- the ranks meet on this host
+        # -- a loopback rendezvous, or one on an address of this host when the
+        # whole world fits this node's GPUs (in a multi-node job
+        # whose MASTER_ADDR names this host, the ranks here must not take
+        # rank = local rank while the other nodes' ranks fail; the device count
+        # is checked before any name lookup)
+        maddr = env.get("MASTER_ADDR", "127.0.0.1")
+        ngpu = _local_gpu_count(env) if maddr not in _LOOPBACK else None
         one_node = (local_size == size or size == 1 or
                     (source == "env" and local_size is None and
-                     _is_local_addr(env.get("MASTER_ADDR", "127.0.0.1"))))
+                     (maddr in _LOOPBACK or
+                      (ngpu is not None and size <= ngpu and _is_local_addr(maddr)))))
         local_rank = rank if one_node else None
     if local_rank is None:
         raise RuntimeError("launcher environment (%s) gives no node-local rank: set LOCAL_RANK "
@@ -404,10 +412,39 @@ def launch_from_env(environ=None):
                 local_size=local_size, addr=addr, port=int(port), token=token, source=source)
 
 
+_LOOPBACK = ("127.0.0.1", "localhost", "::1")
+
+
+def _local_gpu_count(env):
+    """GPUs this process may use on this node, without initialising HIP: the
+    count of a *_VISIBLE_DEVICES list if one is set (the smallest), else the
+    KFD topology's GPU nodes (gfx_target_version != 0); None if unknown."""
+    counts = []
+    for k in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(k)
+        if v is not None:
+            counts.append(len([x for x in v.split(",") if x.strip()]))
+    if counts:
+        return min(counts)
+    import glob
+
+    n = 0
+    for path in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            with open(path) as f:
+                for line in f:
+                    if line.startswith("gfx_target_version") and int(line.split()[1]) != 0:
+                        n += 1
+                        break
+        except (OSError, ValueError, IndexError):
+            continue
+    return n or None
+
+
 def _is_local_addr(addr):
     """True if `addr` (a name or a literal) is this host: a loopback name, or an
     address some local interface holds (a socket can be bound to it)."""
-    if addr in ("127.0.0.1", "localhost", "::1"):
+    if addr in _LOOPBACK:
         return True
     try:
         infos = socket.getaddrinfo(addr, None)

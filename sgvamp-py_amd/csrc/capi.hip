@@ -84,6 +84,16 @@ void resolve_timers(sgv_ctx* c){
     c->evpool.push_back(pr.second);
   }
   c->gpending.clear();
+  for (auto& pr : c->empending) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) {
+      c->em_ms += ms;
+      c->em_loops_timed += 1.0;
+    }
+    c->evpool.push_back(pr.first);
+    c->evpool.push_back(pr.second);
+  }
+  c->empending.clear();
 }
 
 int event_pair(sgv_ctx* c, hipEvent_t* e0, hipEvent_t* e1){

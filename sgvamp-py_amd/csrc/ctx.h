@@ -308,6 +308,9 @@ struct sgv_ctx {
   // exact CG column sets: the device's idle time between the p update and the
   // passes the host enqueues once it has read the stop test (HIP events)
   double host_wait_ms = 0.0;
+  // device-loop EM prior loops timed with HIP events (first enqueue to the
+  // last step's completion), to check the cost model against
+  double em_ms = 0.0, em_loops_timed = 0.0;
   int nchg = 0, nblkg = 0;
   int64_t mpad_max = 0;
   ChunkDesc* d_chg = nullptr;
@@ -333,6 +336,7 @@ struct sgv_ctx {
   // wall time of the host callback for the host exchange
   std::vector<std::pair<hipEvent_t, hipEvent_t>> xpending;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> gpending;   // exact-CG read gaps
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> empending;  // EM loops
   double xchg_n = 0.0, xchg_ms = 0.0, xchg_bytes = 0.0;
   double ld_ms = 0.0, ld_launches = 0.0, rhs_bytes = 0.0, ld_bytes = 0.0, dense_bytes = 0.0,
          aux_bytes = 0.0;

@@ -166,18 +166,22 @@ int gather_f64(sgv_ctx* c, const double* d_send, double* d_recv, size_t cnt,
 // MI355X), T_rep = 35 us (the one-workgroup reduction + control over every
 // block), T_ps = 15 us (per-block sums, ordered total, control: 3 launches),
 // B = 100 GB/s (an xGMI all-gather of MBs).  L: 25 us by default, env
-// SGV_XCHG_LAT_US (rank 0's value), or measured (sgv_exchange_probe).
+// SGV_XCHG_LAT_US (rank 0's value), or measured (sgv_exchange_probe).  A
+// measured L already holds the per-block sums and ordered-total launches (the
+// probe times a whole ordered reduction), so then T_ps keeps only the control
+// launch, T_CTL = 5 us (counted once).
 // SGV_EM_REP=0/1 (with SGV_AB=1) forces either mode.
 constexpr double EM_K_FIX_US = 5.0, EM_K_PER_CM_US = 1.1e-5, EM_T_REP_US = 35.0,
-                 EM_T_PS_US = 15.0, EM_AG_GBS = 100.0;
-static void em_costs_raw(double km, double n, double L, double steps, double* rep_us,
+                 EM_T_PS_US = 15.0, EM_T_CTL_US = 5.0, EM_AG_GBS = 100.0;
+static void em_costs_raw(double km, double n, double L, double steps, double tps, double* rep_us,
                          double* ps_us) {
   *rep_us = L + 8.0 * km * (n - 1.0) / n / (EM_AG_GBS * 1e3) +
             steps * (EM_K_FIX_US + EM_K_PER_CM_US * km + EM_T_REP_US);
-  *ps_us = steps * (EM_K_FIX_US + EM_K_PER_CM_US * km / n + EM_T_PS_US + L);
+  *ps_us = steps * (EM_K_FIX_US + EM_K_PER_CM_US * km / n + tps + L);
 }
 static void em_costs(const sgv_ctx* c, double steps, double* rep_us, double* ps_us) {
-  em_costs_raw((double)c->K * (double)c->Mtot, (double)c->nranks, c->xlat_us, steps, rep_us, ps_us);
+  em_costs_raw((double)c->K * (double)c->Mtot, (double)c->nranks, c->xlat_us, steps,
+               c->xlat_src == 2 ? EM_T_CTL_US : EM_T_PS_US, rep_us, ps_us);
 }
 // the mode of the next EM loop (maxit steps at most); records the prediction
 bool em_mode_pick(sgv_ctx* c, int maxit){
@@ -335,11 +339,14 @@ extern "C" int sgv_exchange_stats(sgv_ctx* c, double* dst, int cap, int reset) {
   out[11] = c->host_wait_ms;
   out[12] = (double)c->xlat_src;
   out[13] = c->em_rep ? 1.0 : 0.0;
+  out[14] = c->em_ms;
+  out[15] = c->em_loops_timed;
   for (int i = 0; i < std::min(cap, SGV_EXCHANGE_STATS_N); ++i) dst[i] = out[i];
   if (reset) {
     c->xchg_n = c->xchg_ms = c->xchg_bytes = 0.0;
     c->em_loops_rep = c->em_loops_ps = 0.0;
     c->host_wait_ms = 0.0;
+    c->em_ms = c->em_loops_timed = 0.0;
   }
   return SGV_OK;
 }
@@ -419,6 +426,6 @@ extern "C" int sgv_em_cost_model(double cohort_markers, int nranks, double laten
                                  double steps, double* out2) {
   if (!out2 || nranks < 1 || !(cohort_markers >= 0.0) || !(latency_us >= 0.0) || !(steps >= 0.0))
     return SGV_ERR_ARG;
-  em_costs_raw(cohort_markers, (double)nranks, latency_us, steps, &out2[0], &out2[1]);
+  em_costs_raw(cohort_markers, (double)nranks, latency_us, steps, EM_T_PS_US, &out2[0], &out2[1]);
   return SGV_OK;
 }

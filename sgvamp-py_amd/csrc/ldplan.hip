@@ -333,6 +333,10 @@ static int plan_walks(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
     const LdBlock& lb = c->ldb[ld][b];
     if (lb.fmt != 1) continue;
     if (lb.ext <= 0 || lb.ext > (int64_t)WALK_RMAX * SYM_H) return SGV_OK;
+    // the walk kernel addresses a block's Pk rows with 32-bit byte offsets
+    // (row * 8 * PKS, PKS <= 8): a block of 2^31 / 64 rows or more takes the
+    // strips (~33.5M markers, beyond a chromosome of SNPs)
+    if (c->bn[b] + SYM_H >= ((int64_t)1 << 31) / (8 * 8)) return SGV_OK;
     any = true;
   }
   if (!any) return SGV_OK;

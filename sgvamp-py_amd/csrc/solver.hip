@@ -476,6 +476,9 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
     // one-rank loop over every rank's gathered r1.
     const bool rep = em_mode_pick(c, maxit);
     const bool fuse = rep || (!c->comm && !c->host_ag && fused_ctl_pays(EM_NV, c->nblk));
+    hipEvent_t em0, em1;   // the loop on the device: its r1 gather to its last step
+    CHK(event_pair(c, &em0, &em1));
+    HIPCHK(hipEventRecord(em0, c->st));
     const ChunkDesc* ech = rep ? c->d_chg : c->d_ch;
     const int* ebeg = rep ? c->d_chg_begin : c->d_ch_begin;
     const int enb = rep ? c->nblkg : c->nblk, ench = rep ? c->nchg : c->nch;
@@ -505,7 +508,16 @@ extern "C" int sgv_em(sgv_ctx* c, const double* gam1s, const double* a, int nsla
       if (it + 1 < maxit) CHK(enqueue(it + 1));
       CHK(event_spin(c, c->ev_em[it % CG_RING]));
       last = c->h_emm + it % CG_RING;
-      if (last->done) break;
+      if (last->done) {
+        HIPCHK(hipEventRecord(em1, c->st));   // behind the one step queued past the last
+        c->empending.push_back({em0, em1});
+        em0 = em1 = nullptr;
+        break;
+      }
+    }
+    if (em0) {   // maxit reached without convergence: the loop ends with its last step
+      HIPCHK(hipEventRecord(em1, c->st));
+      c->empending.push_back({em0, em1});
     }
     *lam_io = last->lam;
     for (int l = 0; l < nslab; ++l) omegas_io[l] = last->om[l];

@@ -388,7 +388,8 @@ class Engine:
                     em_loops_replicated=int(t[6]), em_loops_per_step=int(t[7]),
                     em_pred_replicated_us=float(t[8]), em_pred_per_step_us=float(t[9]),
                     em_pred_steps=float(t[10]), host_wait_ms=float(t[11]),
-                    em_replicated_possible=bool(t[13]))
+                    em_replicated_possible=bool(t[13]), em_ms=float(t[14]),
+                    em_loops_timed=int(t[15]))
 
     def comm_info(self):
         """Who the exchange talks to (sgv_comm_info): transport, ranks in the

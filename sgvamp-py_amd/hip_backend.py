@@ -23,7 +23,7 @@ OUT_SLOTS = 3
 MAX_COHORTS = 1024
 MAX_SLABS = 8
 ABI_VERSION = 2          # the header's SGV_ABI_VERSION this binding is typed against
-TIMERS_N, EXCHANGE_STATS_N, COMM_INFO_N = 10, 14, 5
+TIMERS_N, EXCHANGE_STATS_N, COMM_INFO_N = 10, 16, 5
 
 _c_int_p = ctypes.POINTER(ctypes.c_int)
 _c_i64_p = ctypes.POINTER(ctypes.c_int64)

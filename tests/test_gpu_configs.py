@@ -51,6 +51,10 @@ _LD = {}      # the host copy of the last configuration's LD (C2 -> C3, C4 -> C5
 
 def _log(*a):
     print("[configs]", *a, file=sys.stderr, flush=True)
+    path = os.environ.get("SGV_GATE_LOG")   # the gates' numbers for profiles/ (GPU suite runs)
+    if path:
+        with open(path, "a") as f:
+            print("[configs]", *a, file=f)
 
 
 def maxrel(a, b):

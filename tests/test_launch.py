@@ -278,7 +278,9 @@ def test_env_launch_requires_rank_and_local_rank():
     with pytest.raises(RuntimeError, match="LOCAL_RANK"):     # remote rendezvous, node size unknown
         cm.launch_from_env(dict(RANK="5", WORLD_SIZE="8", MASTER_ADDR="10.0.0.5"))
     # a MASTER_ADDR naming this host (its name, or an address one of its
-    # interfaces holds) is a one-node launch
+    # interfaces holds) is a one-node launch -- if the world
+    # fits this node's GPUs; otherwise (a multi-node job whose
+    # rendezvous is here) LOCAL_RANK stays required
     import socket
     host = socket.gethostname()
     try:
@@ -287,4 +289,10 @@ def test_env_launch_requires_rank_and_local_rank():
     except OSError:
         resolvable = False
     if resolvable:
-        assert cm.launch_from_env(dict(RANK="1", WORLD_SIZE="2", MASTER_ADDR=host))["local_rank"] == 1
+        two = dict(RANK="1", WORLD_SIZE="2", MASTER_ADDR=host, HIP_VISIBLE_DEVICES="0,1")
+        assert cm.launch_from_env(two)["local_rank"] == 1
+        with pytest.raises(RuntimeError, match="LOCAL_RANK"):  # 16 ranks, 8 GPUs here
+            cm.launch_from_env(dict(RANK="9", WORLD_SIZE="16", MASTER_ADDR=host,
+                                    ROCR_VISIBLE_DEVICES="0,1,2,3,4,5,6,7"))
+    # no device count known: a non-loopback address never implies one node
+    assert cm._local_gpu_count(dict(HIP_VISIBLE_DEVICES="3,5,")) == 2

@@ -23,7 +23,7 @@ B="--steps 5 --warmup 2 --cpu-baseline off --read-bw 0"
 case $recipe in
   suite)
     SEL=${*:-tests}
-    exec_steps=("gputests_$T:${SUITE_LIMIT:-1000}:SGV_TEST_TIMES=gpurun_out/testtimes_$T.txt python -u -m pytest $SEL -m gpu -x -q -p no:cacheprovider --timeout 900 --timeout-method thread -rs --durations=40"
+    exec_steps=("gputests_$T:${SUITE_LIMIT:-1000}:SGV_TEST_TIMES=gpurun_out/testtimes_$T.txt SGV_GATE_LOG=gpurun_out/gates_$T.log python -u -m pytest $SEL -m gpu -x -q -p no:cacheprovider --timeout 900 --timeout-method thread -rs --durations=40"
                 "smoke_$T:300:python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'"
                 "bench_$T:300:python bench.py")
     [ -n "$NO_BENCH" ] && unset 'exec_steps[2]' 
