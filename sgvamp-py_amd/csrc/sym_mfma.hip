@@ -640,33 +640,18 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
 //   16x16x4 f64 C/D layout (cdna_hip_programming.md): D[(l>>4) + 4r][l & 15].
 typedef double d4 __attribute__((ext_vector_type(4)));
 #define MFMA16(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
-// NW: waves per workgroup, each owning 512 / NW chunk columns.  NW = 4: two
-// workgroups per CU (the B operands and column sums of 128 columns per wave:
-// 256 VGPRs with spills at PD = 2); NW = 8: one 8-wave workgroup per CU, 64
-// columns per wave -- half the per-wave B operands and column accumulators,
-// so the same two waves per SIMD fit the register file without spilling.  The
-// column sums are the same MFMA chains (bitwise); the row sums add NW wave
-// parts in wave order.
-// ROW4: the row part on v_mfma_f64_4x4x4f64 (four 4-column groups, the 4
-// blocks' partial rows added by DPP as in k_sym_mfma) instead of 16x16x4: the
-// 4x4x4 form issues the same MACs in ~16 cycles per 256 against ~100 per 1024
-// (tools/mfma_probe.hip at two waves per SIMD), and the row part's B operands
-// (P at the wave's columns) cost the same registers in either form; the
-// column part stays on 16x16x4, whose B operands (P at 4 rows) the 4x4x4 form
-// would replicate over its 4 blocks.  The row fragments come from the XOR-
-// swizzled tile of k_sym_mfma.
-template <int PD, bool RAG = false, int NW = 4, bool ROW4 = false>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void k_sym_mfma16(const SymStrip* __restrict__ strips,
+template <int PD, bool RAG = false>
+__global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
                                                      double* __restrict__ rowpart,
                                                      double* __restrict__ colpart,
                                                      const int* __restrict__ run) {
   constexpr int LDP = MF_LDP;
-  constexpr int MF_WC = MF_CW / NW; // columns per wave
+  constexpr int MF_WC = MF_CW / 4; // columns per wave
   constexpr int MF_NT = MF_WC / 32;
-  __shared__ double red[2][NW][256];
-  __shared__ __attribute__((aligned(16))) double stg[NW][16 * LDP];
+  __shared__ double red[2][4][256];
+  __shared__ __attribute__((aligned(16))) double stg[4][16 * LDP];
   const SymStrip sp = strips[blockIdx.x];
   if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
   const int lane = threadIdx.x & (WAVE - 1);
@@ -680,9 +665,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_sym_mfma16(const SymStrip* 
   const int nta = min(MF_NT, max(0, (ncc - cw0 + 31) / 32));   // as k_sym_mfma
 
   double* sb = stg[wid];
-  const int bq = (lane >> 2) & 3, n4 = lane & 3, pc = hi + 4 * bq;   // ROW4 lane map
-  // row-part B operands (P at this wave's columns), reused by every row group;
-  // ROW4: brow[t][e][q] = P[column cw0 + 32 t + 2 pc + e][4 q + n4]
+  // row-part B operands (P at this wave's columns), reused by every row group
   double brow[MF_NT][4][2];
 #pragma unroll
   for (int t = 0; t < MF_NT; ++t)
@@ -690,15 +673,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_sym_mfma16(const SymStrip* 
     for (int s = 0; s < 4; ++s)
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        if constexpr (ROW4) {   // [t][q = s][e]
-          const int col = cw0 + 32 * t + 2 * pc + e;
-          const double v = ldg(pkb + (int64_t)(c0 + (col < ncc ? col : 0)) * 16 + 4 * s + n4);
-          brow[t][s][e] = col < ncc ? v : 0.0;
-        } else {
-          const int col = cw0 + 32 * t + 8 * s + 2 * hi + e;
-          const double v = ldg(pkb + (int64_t)(c0 + (col < ncc ? col : 0)) * 16 + lo);
-          brow[t][s][e] = col < ncc ? v : 0.0;
-        }
+        const int col = cw0 + 32 * t + 8 * s + 2 * hi + e;
+        const double v = ldg(pkb + (int64_t)(c0 + (col < ncc ? col : 0)) * 16 + lo);
+        brow[t][s][e] = col < ncc ? v : 0.0;
       }
   d4 dcol[MF_NT][2];
 #pragma unroll
@@ -761,11 +738,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_sym_mfma16(const SymStrip* 
 #pragma unroll
       for (int a = 0; a < 4; ++a) bcol[a] = bcn[a];
       d4 drow0 = d4{0.0, 0.0, 0.0, 0.0}, drow1 = drow0;
-      double drow4[ROW4 ? 4 : 1][4];                   // ROW4: [r][q], D row 4 r + m
-#pragma unroll
-      for (int r = 0; r < (ROW4 ? 4 : 1); ++r)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) drow4[r][q] = 0.0;
       const bool colz = dhalf && cur.r0 == c0;
 #pragma unroll
       for (int t = 0; t < MF_NT; ++t) {
@@ -784,19 +756,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_sym_mfma16(const SymStrip* 
         if (RAG && cw0 + 32 * t >= cur.nc) continue;   // as k_sym_mfma
         if (RAG && cur.nc < ncc) band_zero(cur.nc, t, cf);
         lds_order();                                   // previous step's tile reads done
-        if constexpr (ROW4) {   // k_sym_mfma's XOR-swizzled tile and row fragment
 #pragma unroll
-          for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[a];
-          lds_order();
+        for (int a = 0; a < 4; ++a) *(d2*)(sb + (4 * a + hi) * LDP + 2 * lo) = cf[a];
+        lds_order();                                   // tile written
 #pragma unroll
-          for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
-        } else {
-#pragma unroll
-          for (int a = 0; a < 4; ++a) *(d2*)(sb + (4 * a + hi) * LDP + 2 * lo) = cf[a];
-          lds_order();                                 // tile written
-#pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2) rf[s2] = *(const d2*)(sb + lo * LDP + 8 * s2 + 2 * hi);
-        }
+        for (int s2 = 0; s2 < 4; ++s2) rf[s2] = *(const d2*)(sb + lo * LDP + 8 * s2 + 2 * hi);
         if (!colz) {
 #pragma unroll
           for (int a = 0; a < 4; ++a) {
@@ -804,45 +768,21 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void k_sym_mfma16(const SymStrip* 
             dcol[t][1] = MFMA16(cf[a].y, bcol[a], dcol[t][1]);
           }
         }
-        if constexpr (ROW4) {   // x halves of all 16 chains, then the y halves
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) drow4[r][q] = MFMA4(rf[r].x, brow[t][q][0], drow4[r][q]);
-#pragma unroll
-          for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) drow4[r][q] = MFMA4(rf[r].y, brow[t][q][1], drow4[r][q]);
-        } else {
-#pragma unroll
-          for (int s2 = 0; s2 < 4; ++s2) {
-            drow0 = MFMA16(rf[s2].x, brow[t][s2][0], drow0);
-            drow1 = MFMA16(rf[s2].y, brow[t][s2][1], drow1);
-          }
+        for (int s2 = 0; s2 < 4; ++s2) {
+          drow0 = MFMA16(rf[s2].x, brow[t][s2][0], drow0);
+          drow1 = MFMA16(rf[s2].y, brow[t][s2][1], drow1);
         }
       }
-      // row sums of this 16-row group: waves 0..NW-1 in order
+      // row sums of this 16-row group: waves 0..3 in order
       double* rb = red[gg & 1][wid];
-      if constexpr (ROW4) {   // the 4 blocks (DPP row rotations), as k_sym_mfma
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            double v = drow4[r][q];
-            v = v + row_ror<12>(v);
-            v = v + row_ror<8>(v);
-            if (bq == 0) rb[((4 * r + hi) << 4) + 4 * q + n4] = v;
-          }
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) rb[((hi + 4 * r) << 4) + lo] = drow0[r] + drow1[r];
-      }
+      for (int r = 0; r < 4; ++r) rb[((hi + 4 * r) << 4) + lo] = drow0[r] + drow1[r];
       __syncthreads();
-      if (threadIdx.x < 256) {
+      {
         const int t = threadIdx.x, row = t >> 4, cc = t & 15;
-        double v = red[gg & 1][0][t];
-#pragma unroll
-        for (int w = 1; w < NW; ++w) v += red[gg & 1][w][t];
+        const double v = ((red[gg & 1][0][t] + red[gg & 1][1][t]) + red[gg & 1][2][t]) +
+                         red[gg & 1][3][t];
         if (16 * g + row < cur.H && cc < ncol)
           rowpart[((int64_t)cur.item * SYM_H + 16 * g + row) * ncol + cc] = v;
       }
@@ -1037,15 +977,6 @@ hipError_t launch_pk(const PassArgs& pa, int nc, int64_t mpad, double* d_pk, hip
   return hipGetLastError();
 }
 
-// SGV_MF16 (A/B, with SGV_AB=1): the 9-16-column kernel's form -- 2: 4 waves,
-// prefetch depth 2; 1: 4 waves, depth 1; 8: 8 waves of 64 columns, depth 2;
-// 9: as 8 with the row part on 4x4x4
-static int mf16_form() {
-  const char* e = ab_env("SGV_MF16");
-  const int v = e ? std::atoi(e) : 2;
-  return (v == 1 || v == 8 || v == 9) ? v : 2;
-}
-
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                            const PassArgs& pa, const double* d_pk, double* rowpart,
                            double* colpart, bool ragged, int pair, hipStream_t st) {
@@ -1057,46 +988,24 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
   // workgroup re-reading the same R with the default cache policy (+33 %,
   // profiles/r03/s4/mf_sets_ab.jsonl) and three / four 4x4x4 groups at one wave
   // per SIMD with the deferred row MFMAs (+13 % / +28 %, ng4_ab.jsonl):
-  // measured in DESIGN.md.  Prefetch depth 2 (7 VGPRs spilled on band plans,
-  // still faster: profiles/r03/s4/mf16_pd_ab.jsonl, profiles/r04/band2_ab.jsonl)
+  // measured in DESIGN.md.  Prefetch depth 2 (3 / 7 VGPRs spilled on dense /
+  // band plans, still faster: profiles/r03/s4/mf16_pd_ab.jsonl,
+  // profiles/r04/band2_ab.jsonl).  Round 6 measured the spill-free forms on one
+  // box (profiles/r06/mf16_forms_ab.jsonl, _bench_c5conv.jsonl): depth 1 (236
+  // VGPRs) +1.5-2 % per pass, 8 waves of 64 columns per workgroup (188 VGPRs)
+  // +8 %, and the row part on 4x4x4 MFMA in that form (210 VGPRs) +18 % -- the
+  // spills sit outside the row-group loop; the 8-wave row-sum combine and the
+  // 4x4x4 form's DPP reductions and 4x the MFMA issues cost more than they save.
   switch ((nc + 3) / 4) {
     case 1: launch_mf<1>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
     case 2: launch_mf<2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
     default:
-      switch (mf16_form()) {
-        case 1:   // 4 waves, prefetch depth 1
-          if (ragged)
-            hipLaunchKernelGGL((k_sym_mfma16<1, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                               d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-          else
-            hipLaunchKernelGGL((k_sym_mfma16<1>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                               d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-          break;
-        case 9:   // 8 waves of 64 columns, prefetch depth 2, row part on 4x4x4
-          if (ragged)
-            hipLaunchKernelGGL((k_sym_mfma16<2, true, 8, true>), dim3(nstrips), dim3(512), 0, st,
-                               d_strips, d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-          else
-            hipLaunchKernelGGL((k_sym_mfma16<2, false, 8, true>), dim3(nstrips), dim3(512), 0, st,
-                               d_strips, d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-          break;
-        case 8:   // 8 waves of 64 columns, prefetch depth 2
-          if (ragged)
-            hipLaunchKernelGGL((k_sym_mfma16<2, true, 8>), dim3(nstrips), dim3(512), 0, st,
-                               d_strips, d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-          else
-            hipLaunchKernelGGL((k_sym_mfma16<2, false, 8>), dim3(nstrips), dim3(512), 0, st,
-                               d_strips, d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-          break;
-        default:  // 4 waves, prefetch depth 2
-          if (ragged)
-            hipLaunchKernelGGL((k_sym_mfma16<2, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                               d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-          else
-            hipLaunchKernelGGL((k_sym_mfma16<2>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                               d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-          break;
-      }
+      if (ragged)
+        hipLaunchKernelGGL((k_sym_mfma16<2, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
+                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
+      else
+        hipLaunchKernelGGL((k_sym_mfma16<2>), dim3(nstrips), dim3(256), 0, st, d_strips,
+                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       break;
   }
   return hipGetLastError();
