@@ -105,15 +105,9 @@ struct LdPlan {
 // chunk-width class of the packed VALU pass for nc columns (CW = 1024 >> cls)
 static inline int sym_class(int nc) { return nc <= 2 ? 0 : nc <= 4 ? 1 : nc <= 8 ? 2 : 3; }
 // default number of right-hand sides from which packed passes run on the f64
-// matrix cores (sym_mfma.hip, class-1 items); env SGV_MFMA_MIN overrides,
-// 0 disables; per context: sgv_set_mfma_min
-static inline int mfma_min_default() {
-  static const int v = [] {
-    const char* e = ab_env("SGV_MFMA_MIN");
-    return e ? std::atoi(e) : 3;
-  }();
-  return v;
-}
+// matrix cores (sym_mfma.hip, class-1 items); per context: sgv_set_mfma_min
+// (0 disables)
+static inline int mfma_min_default() { return 3; }
 // CG loop driver: 1 (default) = pipelined, device-side control (cg_loop_dev);
 // 0 = host-side stop test per iteration (cg_loop).  Env SGV_CG_PIPE.
 static inline int cg_pipe_default() {

@@ -109,23 +109,19 @@ int grow(sgv_ctx* c, double** buf, size_t* cap, size_t need){
 }
 
 
-// panels per MFMA strip (env SGV_MFMA_STRIP, read when a plan is built; 1 =
-// one (panel, chunk) item per workgroup)
-static int mfma_strip_len() {
-  const char* e = ab_env("SGV_MFMA_STRIP");
-  const int v = e ? std::atoi(e) : 8;
-  return std::max(1, std::min(64, v));
-}
+// panels per MFMA strip (a function of nothing but the block's panels, so the
+// sums are the same on every rank count; 3-32 panels and 5-panel strips for
+// short launches measured in rounds 1-4, profiles/r04/strip5_ab.jsonl)
+constexpr int MFMA_STRIP = 8;
 
-// Block groups of the MFMA pass (SGV_PASS_GROUPS with SGV_AB=1 forces a count):
-// by default one group per ~4 rounds of strips on the device's workgroup slots,
-// at most 4 -- a group's finalize then overlaps the next group's strips on a
-// second stream.  The grouping changes no sum (strips and panels are the same
-// work items in another launch), so products are bitwise the same for every
-// count; it is a function of this rank's plan only.
+// Block groups of the MFMA pass: one group per ~4 rounds of strips on the
+// device's workgroup slots, at most 8 -- a group's finalize then overlaps the
+// next group's strips on a second stream.  The grouping changes no sum (strips
+// and panels are the same work items in another launch), so products are
+// bitwise the same for every count (1, 2, 4, 8 groups: profiles/r05/
+// pass_groups_ab.jsonl); it is a function of this rank's plan only.
 static int pass_groups(int nstrips, int nblk, int slots) {
-  const char* e = ab_env("SGV_PASS_GROUPS");
-  int g = e ? std::atoi(e) : nstrips / std::max(1, 4 * slots);
+  const int g = nstrips / std::max(1, 4 * slots);
   return std::max(1, std::min(std::min(g, 8), nblk));
 }
 
@@ -189,7 +185,7 @@ static int mfma_pair_choice(const std::vector<SymStrip>& strips,
 static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
                         const std::vector<SymPanel>& panels, LdPlan* pl) {
   constexpr int cw = 512;
-  const int S = mfma_strip_len();
+  const int S = MFMA_STRIP;
   constexpr int NPAR = cw / SYM_H;   // 512-column chunks start at 256 p + 512 k
   std::vector<SymItem> sitems;
   std::vector<SymStrip> strips;
@@ -318,11 +314,11 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
 // 9-16 columns stay on the strips' 16x16x4 kernel): at M = 1e6, bw = 1,000
 // 1.68 / 1.71 / 1.99 ms at 3 / 4 / 8 columns against the strips' 1.87 / 1.92
 // / 2.12 (profiles/r05/walk_ab/wvs_a_ab.jsonl).
-// SGV_BAND_WALK (with SGV_AB=1): 0 = the strips for every band pass, 4 = walks
-// up to 4 columns (A/B).
+// SGV_BAND_WALK=0 (with SGV_AB=1): the strips for every band pass (the
+// walks-vs-strips A/B of tools/gpu_walk_vs_strips.sh).
 static int band_walk_max_nc() {
   const char* e = ab_env("SGV_BAND_WALK");
-  return e ? (e[0] == '0' ? 0 : e[0] == '4' ? 4 : 8) : 8;
+  return (e && e[0] == '0') ? 0 : 8;
 }
 
 static int plan_walks(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
@@ -656,7 +652,8 @@ int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa_in){
     const int cls = mf ? 1 : sym_class(nc);
     if (mf) {
       const bool walk = pl.nwalks && nc <= band_walk_max_nc();
-      HIPCHK(launch_pk(pa, nc, c->Mpad, c->d_pk, c->st, walk && nc > 4));
+      HIPCHK(launch_pk(pa, nc, c->Mpad, c->d_pk, c->st,
+                       walk ? nc > 4 : strip_pk_paired(nc, pl.pair)));
       if (walk) {   // band plan: the walks, then the head panels
         HIPCHK(launch_band_walk(nc, pl.d_walks, pl.nwalks, pl.d_wpanels, pl.d_witems, c->d_pk,
                                 c->Mpad, pa,

@@ -92,7 +92,10 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // apart instead of 4 (2 at NG = 1); every chain accumulates in the same order
 // (bitwise the same sums), the row fragments are double-buffered in registers.
 // RAG: some item of the strip stops short of the strip's widest (band plans).
-template <int NG, int PD, bool RAG = false, bool DEF = false>
+// PP (NG = 2): Pk in k_pack's PAIRED layout, so a lane's two column groups
+// (columns n4 and 4 + n4) of one Pk row are one 16-B load: half the P-operand
+// load instructions through the texture-address unit per row group
+template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -134,17 +137,28 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
   double* sb = stg[wid];
 
   // row-part B operands: P at this wave's columns, reused by every row group
+  static_assert(!PP || NG == 2, "paired Pk rows: two column groups");
+  // one Pk row's values of this lane: column 4 q + n4 for each group q
+  auto ld_prow = [&](int64_t row, double* v) {
+    if constexpr (PP) {
+      const d2 x = ldg((const d2*)(pkb + row * PKS + 2 * n4));
+      v[0] = x.x;
+      v[1] = x.y;
+    } else {
+#pragma unroll
+      for (int q = 0; q < NG; ++q) v[q] = ldg(pkb + row * PKS + 4 * q + n4);
+    }
+  };
   double brow[NT][2][NG];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int col = cw0 + 32 * t + 2 * pc + e;
+      double v[NG];
+      ld_prow(c0 + (col < ncc ? col : 0), v);
 #pragma unroll
-      for (int q = 0; q < NG; ++q) {
-        const double v = ldg(pkb + (int64_t)(c0 + (col < ncc ? col : 0)) * PKS + 4 * q + n4);
-        brow[t][e][q] = col < ncc ? v : 0.0;
-      }
+      for (int q = 0; q < NG; ++q) brow[t][e][q] = col < ncc ? v[q] : 0.0;
     }
   double dcol[NT][2][NG];
 #pragma unroll
@@ -178,11 +192,10 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int rB = 16 * g + 4 * a + hi;
+      double v[NG];
+      ld_prow(r0 + (rB < H ? rB : 0), v);
 #pragma unroll
-      for (int q = 0; q < NG; ++q) {
-        const double v = ldg(pkb + (int64_t)(r0 + (rB < H ? rB : 0)) * PKS + 4 * q + n4);
-        bc[a][q] = (rB < H && !zero) ? v : 0.0;
-      }
+      for (int q = 0; q < NG; ++q) bc[a][q] = (rB < H && !zero) ? v[q] : 0.0;
     }
   };
   auto pbase = [&](const SymItem& x) { return (uint64_t)(x.P + (x.c0 - x.r0)); };
@@ -945,21 +958,27 @@ __global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpa
 // kernel (capi.hip build_strips; bitwise the same products) -- 1: 3-4 columns
 // only (at 5-8 the pair form runs ~14 % slower per byte and a short launch's
 // tail does not pay it back), 2 (forced, SGV_MF_PAIR=1): every column count
-template <int NG>
+template <int NG, bool PP = false>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
                       const int* run, int pks, bool ragged, int pair, hipStream_t st) {
   // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
   if (ragged)
-    hipLaunchKernelGGL((k_sym_mfma<NG, 2, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                       d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+    hipLaunchKernelGGL((k_sym_mfma<NG, 2, true, false, PP>), dim3(nstrips), dim3(256), 0, st,
+                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else if (pair >= (NG == 1 ? 1 : 2))
     hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else
-    hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true>), dim3(nstrips), dim3(256), 0, st,
+    hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP>), dim3(nstrips), dim3(256), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
 }
+
+// 5-8-column strip passes read Pk PAIRED (k_pack) unless the plan runs the
+// wave-pair kernel (forced only).  Bitwise the same products; one box,
+// alternating: the 8-block share -0.6...-1.8 % per pass, 64 blocks even to
+// -0.4 % (profiles/r06/pkpair_ab.jsonl, pkpair_bench.jsonl)
+bool strip_pk_paired(int nc, int pair) { return nc > 4 && nc <= 8 && pair < 2; }
 
 hipError_t launch_pk(const PassArgs& pa, int nc, int64_t mpad, double* d_pk, hipStream_t st,
                      bool paired) {
@@ -998,7 +1017,14 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
   // 4x4x4 form's DPP reductions and 4x the MFMA issues cost more than they save.
   switch ((nc + 3) / 4) {
     case 1: launch_mf<1>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
-    case 2: launch_mf<2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
+    case 2:
+      if (strip_pk_paired(nc, pair))
+        launch_mf<2, true>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks,
+                           ragged, pair, st);
+      else
+        launch_mf<2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged,
+                     pair, st);
+      break;
     default:
       if (ragged)
         hipLaunchKernelGGL((k_sym_mfma16<2, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
