@@ -251,7 +251,14 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
   // group, then most panels first, creation order within a count.  Measured
   // slower (profiles/r03/s4/): ordering by stored bytes (2-10 %) and
   // XCD-contiguous eighths of the creation order (north star +5 %, 8 x 25,000
-  // +4-7 %, the 8-block share -1 %)
+  // +4-7 %, the 8-block share -1 %).  Round 6: workgroup i runs on XCD i mod 8
+  // (tools/strip_trace.py), and in creation order a chunk's top strips fall
+  // 8:4 on the even XCDs, whose busy time ran up to 18 % above the odd ones';
+  // dealing each strip kind evenly over the XCDs (by place in its chunk)
+  // evened seven of the eight but left the pass even on the 8-block share and
+  // +0.8 / +2 % on 64 x 15,625 / 8 x 25,000 (profiles/r06/strip_order_*.jsonl,
+  // strip_trace_xcd_*.jsonl): the pass is bound by the HBM side, not by which
+  // XCD drains last.
   {
     std::vector<int> ord(strips.size());
     for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;

@@ -65,7 +65,28 @@ def main():
             if s_cu.size > 2:
                 gaps.extend((s_cu[2:] - e_cu[:-2]).tolist())
         gaps = np.array(gaps) if gaps else np.zeros(1)
+        # per XCD: workgroup i is assumed dispatched to XCD i % 8 (round robin);
+        # the CU id tells where it ran -- the table checks the assumption, and
+        # each XCD's first start / last end / busy show whether the tail is an
+        # XCD running out of work while others still have strips
+        idx = np.nonzero(tr[:, 1] > 0)[0]
+        xcd_of = idx % 8
+        cu = live[:, 2].astype(np.int64)
+        per_xcd = []
+        for x in range(8):
+            m = xcd_of == x
+            if not m.any():
+                continue
+            per_xcd.append(dict(xcd=x, strips=int(m.sum()), busy_us=round(float(dur[m].sum()), 1),
+                                last_start=round(float(st[m].max()), 1),
+                                last_end=round(float(en[m].max()), 1),
+                                mean_us=round(float(dur[m].mean()), 1),
+                                cus=int(np.unique(cu[m]).size),
+                                cu_ids=[int(cu[m].min()), int(cu[m].max())]))
+        if os.environ.get("SGV_TRACE_RAW"):
+            np.save(os.environ["SGV_TRACE_RAW"] + "_%s.npy" % shape, live)
         print(json.dumps(dict(
+            per_xcd=per_xcd,
             active_mean=round(float(act.mean()), 1),
             active_pctl={p: int(np.percentile(act, p)) for p in (1, 10, 50, 90)},
             handover_gap_us={p: round(float(np.percentile(gaps, p)), 1) for p in (10, 50, 90, 99)},
