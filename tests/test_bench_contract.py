@@ -51,3 +51,25 @@ def test_northstar_and_c2_summaries_present():
              for d in sums.values()}
     assert ("k_sym_pass", 2.0e10) in kinds          # C2, K = 1
     assert ("k_sym_mfma", 6.4e10) in kinds          # north star, M = 1e6, K = 4
+
+
+def test_workload_label_names_non_default_flags():
+    """the bench line's workload names every reference CLI
+    flag (src/main.py:27-50) it sets away from the CLI default, instead of
+    claiming the defaults."""
+    import argparse
+
+    def args(**kw):
+        d = dict(band=None, prior="matched", ridge=0.0, lmmse_damp=0)
+        d.update(kw)
+        return argparse.Namespace(**d)
+
+    matched = dict(prior_vars=[0.0, 3.2e-6], prior_probs=[0.5, 0.5])
+    lab = bench.flags_label(args(), matched)
+    assert "--prior-vars 0,3.2e-06 --prior-probs 0.5,0.5" in lab and "except" in lab
+    assert "default flags" not in lab
+    lab = bench.flags_label(args(ridge=0.1, lmmse_damp=1), matched)
+    assert "--s 0.1" in lab and "--lmmse-damp 1" in lab
+    cli = dict(prior_vars=[0.0, 1.0], prior_probs=[0.99, 0.01])
+    assert bench.flags_label(args(prior="cli"), cli) == \
+        "reference CLI default flags (src/main.py:27-50)"
