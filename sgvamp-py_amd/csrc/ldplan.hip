@@ -183,21 +183,30 @@ static int mfma_pair_choice(const std::vector<SymStrip>& strips,
 // carry slot, and the rest, which starts from them (k_sym_mfma: carry_wait /
 // carry_publish) -- every MFMA of every chain as in the one-workgroup strip,
 // so the products are bitwise the same whether or not a plan splits (the
-// choice is free per rank and plan).  Dispatch order: all first segments
-// (SPLIT_AT panels, the longest items) ahead of every second segment, then
-// the second segments and the unsplit strips, most panels first -- each second
-// segment starts after its first has been dispatched, and the tail is made of
-// items of at most SPLIT_AT panels.  Row partials are per item as before.
+// choice is free per rank and plan).
+// Dispatch order.  Workgroup i runs on XCD i mod NXCD (round robin, in order
+// on each XCD: tools/strip_trace.py), so the order is built per XCD and
+// interleaved: chain k's two segments on XCD k mod NXCD, each XCD's queue its
+// first segments (SPLIT_AT panels, the longest items), then its second
+// segments and its share of the unsplit strips (dealt by panel count to the
+// least-loaded XCD), most panels first; queues padded with empty items
+// (npan 0, exit at once) to one length.  A second segment is dispatched on its
+// XCD only after every first segment queued there, ~2 rounds of that XCD's
+// slots earlier: its wait is short, and it ends in any dispatch order (no
+// cycle: first segments wait on nothing).
 constexpr int SPLIT_AT = 4;
+constexpr int NXCD = 8;   // MI355X: 8 XCDs of 32 CUs
 static bool split_wanted(int nstrips, int slots) {
   const char* e = ab_env("SGV_STRIP_SPLIT");   // A/B: 0 never, 1 always (non-ragged, one group)
   if (e) return e[0] == '1';
   return nstrips < 4 * slots;
 }
 static int split_strips(std::vector<SymStrip>& strips) {
-  std::vector<SymStrip> first, rest;
+  std::vector<std::vector<SymStrip>> qa(NXCD), qb(NXCD);
+  std::vector<int64_t> load(NXCD, 0);
+  std::vector<SymStrip> unsplit;
   int ns = 0;
-  for (const SymStrip& st : strips) {
+  for (const SymStrip& st : strips) {   // strips arrive most panels first
     if (st.npan > SPLIT_AT) {
       SymStrip a = st, b = st;
       a.npan = SPLIT_AT;
@@ -205,17 +214,33 @@ static int split_strips(std::vector<SymStrip>& strips) {
       b.it0 = st.it0 + SPLIT_AT;
       b.npan = st.npan - SPLIT_AT;
       b.cin = ns;
+      const int x = ns % NXCD;
       ++ns;
-      first.push_back(a);
-      rest.push_back(b);
+      qa[x].push_back(a);
+      qb[x].push_back(b);
+      load[x] += st.npan;
     } else {
-      rest.push_back(st);
+      unsplit.push_back(st);
     }
   }
-  std::stable_sort(rest.begin(), rest.end(),
-                   [](const SymStrip& x, const SymStrip& y) { return x.npan > y.npan; });
-  strips = first;
-  strips.insert(strips.end(), rest.begin(), rest.end());
+  for (const SymStrip& st : unsplit) {
+    const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    qb[x].push_back(st);
+    load[x] += st.npan;
+  }
+  size_t len = 0;
+  for (int x = 0; x < NXCD; ++x) {
+    std::stable_sort(qb[x].begin(), qb[x].end(),
+                     [](const SymStrip& u, const SymStrip& v) { return u.npan > v.npan; });
+    qa[x].insert(qa[x].end(), qb[x].begin(), qb[x].end());
+    len = std::max(len, qa[x].size());
+  }
+  SymStrip empty = strips.empty() ? SymStrip{} : strips[0];
+  empty.npan = 0;
+  empty.cin = empty.cout = -1;
+  strips.assign(len * NXCD, empty);
+  for (int x = 0; x < NXCD; ++x)
+    for (size_t q = 0; q < qa[x].size(); ++q) strips[q * NXCD + x] = qa[x][q];
   return ns;
 }
 

@@ -152,6 +152,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
   // (rows 4q + (l & 3), pairs 4((l >> 2) & 3) + (l >> 4)) 16 distinct slots mod 16
   __shared__ __attribute__((aligned(16))) double stg[NW][16 * 32];
   const SymStrip sp = strips[blockIdx.x];
+  if (sp.npan <= 0) return;       // padding of a chained-segment plan (split_strips)
   if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
   MF_TRACE_BEGIN
   const int lane = threadIdx.x & (WAVE - 1);
@@ -727,6 +728,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
   __shared__ double red[2][4][256];
   __shared__ __attribute__((aligned(16))) double stg[4][16 * LDP];
   const SymStrip sp = strips[blockIdx.x];
+  if (sp.npan <= 0) return;       // padding of a chained-segment plan (split_strips)
   if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
