@@ -372,7 +372,8 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
   for (const SymStrip& st : strips)
     for (int i = 0; i < st.npan; ++i) pl->ragged |= sitems[st.it0 + i].nc < st.ncmax;
   pl->nsplit = 0;
-  if (!pl->ragged && ngrp == 1 && split_wanted((int)strips.size(), 2 * ncu))
+  if (!pl->ragged && ngrp == 1 && split_wanted((int)strips.size(), 2 * ncu) &&
+      std::any_of(strips.begin(), strips.end(), [](const SymStrip& st) { return st.npan > SPLIT_AT; }))
     pl->nsplit = split_strips(strips);
   pl->nstrips = (int)strips.size();
   pl->pair = (pl->ragged || pl->nsplit) ? 0 : mfma_pair_choice(strips, sitems);

@@ -490,6 +490,7 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
   __shared__ int hready[4], hdone[4];   // row groups handed / taken per segment
   __shared__ __attribute__((aligned(16))) double stg[NW][16 * 32];
   const SymStrip sp = strips[blockIdx.x];
+  if (sp.npan <= 0) return;   // (padding: plans with chained segments never run this kernel)
   if (run && !ldg(run)) return;
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
