@@ -54,9 +54,6 @@ int stream_wait(sgv_ctx* c){
   }
   if (e != hipSuccess)
     return fail(c, SGV_ERR_HIP, "stream wait: %s", hipGetErrorString(e));
-  if (c->h_serr && *(volatile int*)c->h_serr)   // a chained strip segment's wait ran out
-    return fail(c, SGV_ERR_STATE, "LD pass: a chained strip segment waited past its bound for "
-                "its first half (workgroups dispatched out of order?): products are invalid");
   return SGV_OK;
 }
 
@@ -428,9 +425,6 @@ extern "C" void sgv_destroy(sgv_ctx* c) {
   if (c->d_whead) (void)hipFree(c->d_whead);
   if (c->d_wcarry) (void)hipFree(c->d_wcarry);
   if (c->d_colpart) (void)hipFree(c->d_colpart);
-  if (c->d_scarry) (void)hipFree(c->d_scarry);
-  if (c->d_sflag) (void)hipFree(c->d_sflag);
-  if (c->h_serr) (void)hipHostFree(c->h_serr);
   if (c->d_pk) (void)hipFree(c->d_pk);
   if (c->d_out) (void)hipFree(c->d_out);
   for (int i = 0; i < 2; ++i) {

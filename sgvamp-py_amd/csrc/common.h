@@ -114,27 +114,9 @@ struct SymPanel {
 // their (panel, chunk) items are sitems[it0 .. it0 + npan), column sums go to
 // colpart slot `slot`; ncmax = the widest item's columns (a band's first item
 // can be narrower than the others)
-// cin / cout: chained strip segments (ldplan.hip split_strips).  A strip of
-// the plan may run as two workgroups -- the first `npan` panels with cout >= 0
-// (its column sums, the accumulator registers as they stand, go to carry slot
-// cout instead of colpart), the rest with cin = that slot (its accumulators
-// start from the carry, so every column chain is the one-workgroup chain,
-// MFMA for MFMA: bitwise the same sums).  -1: none.
 struct SymStrip {
   int32_t it0, npan, slot, ncmax;
-  int32_t cin, cout;
 };
-// the carry of chained segments: uncached device memory (hipDeviceMallocUncached:
-// no L2 copies on the eight XCDs to write back or invalidate); flag[slot] ==
-// epoch once the slot holds this launch's values; err (pinned host memory)
-// set when a segment waited past its bound for its first half
-struct StripCarry {
-  double* buf;   // [slot][256 threads][32 doubles]
-  int* flag;     // [slot]
-  int* err;
-  int epoch;
-};
-constexpr int CARRY_PER_THREAD = 32;   // k_sym_mfma16's dcol: 4 steps x 2 x d4
 
 // band walks (band_walk.hip): a workgroup walks panels p0 .. p0 + np - 1 (one
 // block, consecutive; entries of the walk panel table) with a ring of R = the
@@ -375,8 +357,7 @@ hipError_t launch_pk(const PassArgs& pa, int nc, int64_t mpad, double* d_pk, hip
 bool strip_pk_paired(int nc, int pair);
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                            const PassArgs& pa, const double* d_pk, double* rowpart,
-                           double* colpart, bool ragged, int pair, const StripCarry& cc,
-                           hipStream_t st);
+                           double* colpart, bool ragged, int pair, hipStream_t st);
 // band walks (NC <= 8, band_walk.hip): the walks, then the head panels' finalize
 hipError_t launch_band_walk(int nc, const SymWalk* d_walks, int nwalks, const SymPanel* d_panels,
                             const SymItem* d_items, const double* d_pk, int64_t pk_rows,

@@ -77,7 +77,6 @@ struct LdPlan {
   // g's finalize runs on the side stream while group g + 1's strips run
   int ngrp = 1;
   std::vector<int> gs, gp;
-  int nsplit = 0;              // strips run as two chained segments (split_strips)
   // band walks (band_walk.hip, 3-8 columns): when every packed block is a band
   // of extent <= WALK_RMAX panels; the walk panel / item tables in creation
   // order, the head panels' finalize table, head / carry slot counts
@@ -182,14 +181,6 @@ struct sgv_ctx {
   double* d_rowpart = nullptr;   // k_sym_pass row partials
   double* d_colpart = nullptr;   // k_sym_pass column partials
   size_t rowpart_cap = 0, colpart_cap = 0, part_cap = 0;
-  // chained strip segments (LdPlan::nsplit): carry slots and their flags in
-  // uncached device memory, the wait-bound error word in pinned host memory,
-  // and the launch epoch the flags are compared with
-  double* d_scarry = nullptr;
-  int* d_sflag = nullptr;
-  int* h_serr = nullptr;
-  size_t scarry_slots = 0;
-  int sepoch = 0;
   int mfma_min = 3;              // see mfma_min_default
   double* d_pk = nullptr;        // RHS interleaved [Mpad][16] for the MFMA pass
   // asynchronous per-iteration outputs (xhat1, r1[k]): device pack buffer and two
@@ -421,7 +412,6 @@ void free_plan(LdPlan& p);
 void free_block(LdBlock& lb);
 int ld_alloc(sgv_ctx* c, int ld, int b, int fmt, int64_t ext = 0);
 int grow(sgv_ctx* c, double** buf, size_t* cap, size_t need);
-int grow_carry(sgv_ctx* c, size_t slots);   // chained strip segments (ldplan.hip)
 int ensure_plan(sgv_ctx* c, int ld);
 const int* ld_parts(sgv_ctx* c, int ld);
 int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa_in);

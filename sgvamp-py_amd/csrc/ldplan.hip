@@ -175,75 +175,6 @@ static int mfma_pair_choice(const std::vector<SymStrip>& strips,
   return pair >= quad + 0.03 ? 1 : 0;
 }
 
-// Chained segments for short launches.  A launch of a few rounds of strips
-// (an 8-block share of the north star: ~2.4 rounds on 512 workgroup slots)
-// drains in a tail as long as its longest strips (8 panels, ~0.6 ms of a
-// ~1.45 ms launch).  Each strip of more than SPLIT_AT panels then runs as two
-// workgroups: the first SPLIT_AT panels, whose column accumulators go to a
-// carry slot, and the rest, which starts from them (k_sym_mfma: carry_wait /
-// carry_publish) -- every MFMA of every chain as in the one-workgroup strip,
-// so the products are bitwise the same whether or not a plan splits (the
-// choice is free per rank and plan).
-// Dispatch order.  Workgroup i runs on XCD i mod NXCD (round robin, in order
-// on each XCD: tools/strip_trace.py), so the order is built per XCD and
-// interleaved: chain k's two segments on XCD k mod NXCD, each XCD's queue its
-// first segments (SPLIT_AT panels, the longest items), then its second
-// segments and its share of the unsplit strips (dealt by panel count to the
-// least-loaded XCD), most panels first; queues padded with empty items
-// (npan 0, exit at once) to one length.  A second segment is dispatched on its
-// XCD only after every first segment queued there, ~2 rounds of that XCD's
-// slots earlier: its wait is short, and it ends in any dispatch order (no
-// cycle: first segments wait on nothing).
-constexpr int SPLIT_AT = 4;
-constexpr int NXCD = 8;   // MI355X: 8 XCDs of 32 CUs
-static bool split_wanted(int nstrips, int slots) {
-  const char* e = ab_env("SGV_STRIP_SPLIT");   // A/B: 0 never, 1 always (non-ragged, one group)
-  if (e) return e[0] == '1';
-  return nstrips < 4 * slots;
-}
-static int split_strips(std::vector<SymStrip>& strips) {
-  std::vector<std::vector<SymStrip>> qa(NXCD), qb(NXCD);
-  std::vector<int64_t> load(NXCD, 0);
-  std::vector<SymStrip> unsplit;
-  int ns = 0;
-  for (const SymStrip& st : strips) {   // strips arrive most panels first
-    if (st.npan > SPLIT_AT) {
-      SymStrip a = st, b = st;
-      a.npan = SPLIT_AT;
-      a.cout = ns;
-      b.it0 = st.it0 + SPLIT_AT;
-      b.npan = st.npan - SPLIT_AT;
-      b.cin = ns;
-      const int x = ns % NXCD;
-      ++ns;
-      qa[x].push_back(a);
-      qb[x].push_back(b);
-      load[x] += st.npan;
-    } else {
-      unsplit.push_back(st);
-    }
-  }
-  for (const SymStrip& st : unsplit) {
-    const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-    qb[x].push_back(st);
-    load[x] += st.npan;
-  }
-  size_t len = 0;
-  for (int x = 0; x < NXCD; ++x) {
-    std::stable_sort(qb[x].begin(), qb[x].end(),
-                     [](const SymStrip& u, const SymStrip& v) { return u.npan > v.npan; });
-    qa[x].insert(qa[x].end(), qb[x].begin(), qb[x].end());
-    len = std::max(len, qa[x].size());
-  }
-  SymStrip empty = strips.empty() ? SymStrip{} : strips[0];
-  empty.npan = 0;
-  empty.cin = empty.cout = -1;
-  strips.assign(len * NXCD, empty);
-  for (int x = 0; x < NXCD; ++x)
-    for (size_t q = 0; q < qa[x].size(); ++q) strips[q * NXCD + x] = qa[x][q];
-  return ns;
-}
-
 // MFMA strips of one LD matrix from the class-1 (512-column) tables.  Chunk
 // (parity p, c0 = 256 p + 512 k) of a block holds the items (g, c0) of panels
 // g = p, p + 2, ..., G = c0 / 256 (the diagonal panel); they are cut into strips
@@ -281,7 +212,6 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
           st.npan = 0;
           st.slot = (int)strips.size();
           st.ncmax = 0;
-          st.cin = st.cout = -1;
           for (int g = g0; g <= G && g < g0 + NPAR * S; g += NPAR) {
             const SymPanel& pn = panels[bp0 + g];
             const int idx = pn.item_begin + (int)((c0 - (int64_t)SYM_H * g) / cw);
@@ -368,15 +298,11 @@ static int build_strips(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
     sp.swap(o);
   }
   pl->ngrp = ngrp;
+  pl->nstrips = (int)strips.size();
   pl->ragged = false;
   for (const SymStrip& st : strips)
     for (int i = 0; i < st.npan; ++i) pl->ragged |= sitems[st.it0 + i].nc < st.ncmax;
-  pl->nsplit = 0;
-  if (!pl->ragged && ngrp == 1 && split_wanted((int)strips.size(), 2 * ncu) &&
-      std::any_of(strips.begin(), strips.end(), [](const SymStrip& st) { return st.npan > SPLIT_AT; }))
-    pl->nsplit = split_strips(strips);
-  pl->nstrips = (int)strips.size();
-  pl->pair = (pl->ragged || pl->nsplit) ? 0 : mfma_pair_choice(strips, sitems);
+  pl->pair = pl->ragged ? 0 : mfma_pair_choice(strips, sitems);
   CHK(upload_table(c, strips, &pl->d_strips));
   CHK(upload_table(c, sitems, &pl->d_sitems));
   CHK(upload_table(c, sp, &pl->d_spanels));
@@ -678,7 +604,6 @@ int ensure_plan(sgv_ctx* c, int ld){
     rowpart_need = std::max(rowpart_need, (size_t)pl.nitems[1] * SYM_H * MAXC);
     colpart_need = std::max(colpart_need, (size_t)pl.nstrips * MAXC * 512);
     CHK(grow(c, &c->d_pk, &c->pk_cap, (size_t)c->Mpad * 16));
-    if ((size_t)pl.nsplit > c->scarry_slots) CHK(grow_carry(c, (size_t)pl.nsplit));
   }
   CHK(grow(c, &c->d_rowpart, &c->rowpart_cap, rowpart_need));
   CHK(grow(c, &c->d_colpart, &c->colpart_cap, colpart_need));
@@ -688,28 +613,6 @@ int ensure_plan(sgv_ctx* c, int ld){
 }
 
 const int* ld_parts(sgv_ctx* c, int ld){ return c->plan[ld].d_pbeg; }
-
-// carry slots of chained strip segments: uncached device memory (the two
-// segments of a chain may run on different XCDs, whose L2s are not coherent),
-// flags zeroed (epochs start at 1), the error word in pinned host memory
-int grow_carry(sgv_ctx* c, size_t slots) {
-  if (c->d_scarry) (void)hipFree(c->d_scarry);
-  if (c->d_sflag) (void)hipFree(c->d_sflag);
-  c->d_scarry = nullptr;
-  c->d_sflag = nullptr;
-  c->scarry_slots = 0;
-  HIPCHK(hipExtMallocWithFlags((void**)&c->d_scarry, slots * 256 * CARRY_PER_THREAD * sizeof(double),
-                               hipDeviceMallocUncached));
-  HIPCHK(hipExtMallocWithFlags((void**)&c->d_sflag, slots * sizeof(int), hipDeviceMallocUncached));
-  HIPCHK(hipMemset(c->d_sflag, 0, slots * sizeof(int)));
-  if (!c->h_serr) {
-    HIPCHK(hipHostMalloc((void**)&c->h_serr, sizeof(int), hipHostMallocCoherent));
-    *c->h_serr = 0;
-  }
-  c->sepoch = 0;   // flags are all 0 now
-  c->scarry_slots = slots;
-  return SGV_OK;
-}
 
 // coupling sums of LD matrix ld's band pieces for this pass (before the
 // finalize that adds them): the halo of a coupling that spans two ranks is
@@ -749,8 +652,6 @@ int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa_in){
     c->evpool.pop_back();
   }
   HIPCHK(hipEventRecord(e0, c->st));
-  StripCarry cc{c->d_scarry, c->d_sflag, c->h_serr, 0};
-  if (pl.nsplit) cc.epoch = ++c->sepoch;   // one launch per pass: this pass's flags
   if (pl.halo || pl.nctasks) CHK(coupling_pass(c, pl, nc, pa));
   if (pl.nrg) HIPCHK(launch_ld_pass(nc, c->d_blks[ld], pl.d_rg, pl.nrg, pa, c->d_part, c->st));
   if (pl.npanels) {
@@ -766,7 +667,7 @@ int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa_in){
                                 c->d_whead, c->d_wcarry, pl.d_wfins, pl.nwfins, c->d_part, c->st));
       } else if (pl.ngrp <= 1) {
         HIPCHK(launch_sym_mfma(nc, pl.d_strips, pl.nstrips, pl.d_sitems, pa, c->d_pk,
-                               c->d_rowpart, c->d_colpart, pl.ragged, pl.pair, cc, c->st));
+                               c->d_rowpart, c->d_colpart, pl.ragged, pl.pair, c->st));
         HIPCHK(launch_sym_finalize_strip(nc, pl.d_spanels, pl.npanels, pa, c->d_rowpart,
                                          c->d_colpart, c->d_part, pl.ragged, c->st));
       } else {
@@ -777,7 +678,7 @@ int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa_in){
         for (int g = 0; g < pl.ngrp; ++g) {
           HIPCHK(launch_sym_mfma(nc, pl.d_strips + pl.gs[g], pl.gs[g + 1] - pl.gs[g],
                                  pl.d_sitems, pa, c->d_pk, c->d_rowpart, c->d_colpart, pl.ragged,
-                                 pl.pair, cc, c->st));
+                                 pl.pair, c->st));
           HIPCHK(hipEventRecord(c->ev_grp[g % MAXGRP], c->st));
           HIPCHK(hipStreamWaitEvent(c->st_fin, c->ev_grp[g % MAXGRP], 0));
           HIPCHK(launch_sym_finalize_strip(nc, pl.d_spanels + pl.gp[g], pl.gp[g + 1] - pl.gp[g],

@@ -71,42 +71,6 @@ __device__ __forceinline__ void lds_order() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// Chained strip segments (SymStrip::cin / cout): the second segment waits
-// for its first (thread 0 polls the flag with agent-scope loads, which miss
-// in the CU's L1; the carry lives in uncached memory, so no L2 holds a copy),
-// then reads the accumulators the first left.  The first half of a chain is
-// dispatched earlier in the launch (lower index: ldplan.hip split_strips), so
-// it is running or done and the wait ends; the wait is bounded anyway (50 ms
-// of wall clock, then err is set -- checked by the host at its next wait --
-// and the segment goes on with what it read: no hang).
-__device__ __forceinline__ void carry_wait(const StripCarry& cc, int slot) {
-  if (threadIdx.x == 0) {
-    const unsigned long long t0 = wall_clock64();
-    while (__hip_atomic_load(cc.flag + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) !=
-           cc.epoch) {
-      __builtin_amdgcn_s_sleep(4);
-      if (wall_clock64() - t0 > 5000000ull) {   // 50 ms at 100 MHz
-        __hip_atomic_store(cc.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ double carry_ld(const double* p) {
-  const unsigned long long v = __hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-  return __builtin_bit_cast(double, v);
-}
-// the first segment's accumulators are out (stores to uncached memory complete
-// at the memory side), then its flag
-__device__ __forceinline__ void carry_publish(const StripCarry& cc, int slot) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0)
-    __hip_atomic_store(cc.flag + slot, cc.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 constexpr int MF_CW = 512;   // chunk width (class 1 items)
 constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conflict-free both ways
 
@@ -137,8 +101,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
                                                      const double* __restrict__ pk, int ncol,
                                                      double* __restrict__ rowpart,
                                                      double* __restrict__ colpart,
-                                                     const int* __restrict__ run, int pks,
-                                                     StripCarry cc) {
+                                                     const int* __restrict__ run, int pks) {
   constexpr int NW = 4;            // waves 0 and 1 own the diagonal half of a chunk
   constexpr int WC = MF_CW / NW;   // columns per wave
   constexpr int NT = WC / 32;      // 32-column steps per wave
@@ -152,7 +115,6 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
   // (rows 4q + (l & 3), pairs 4((l >> 2) & 3) + (l >> 4)) 16 distinct slots mod 16
   __shared__ __attribute__((aligned(16))) double stg[NW][16 * 32];
   const SymStrip sp = strips[blockIdx.x];
-  if (sp.npan <= 0) return;       // padding of a chained-segment plan (split_strips)
   if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
   MF_TRACE_BEGIN
   const int lane = threadIdx.x & (WAVE - 1);
@@ -199,23 +161,12 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
       for (int q = 0; q < NG; ++q) brow[t][e][q] = col < ncc ? v[q] : 0.0;
     }
   double dcol[NT][2][NG];
-  if (sp.cin >= 0) {   // the second segment of a chain: the first's accumulators
-    carry_wait(cc, sp.cin);
-    const double* cb = cc.buf + ((int64_t)sp.cin * 256 + threadIdx.x) * CARRY_PER_THREAD;
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
-      for (int e = 0; e < 2; ++e)
+    for (int e = 0; e < 2; ++e)
 #pragma unroll
-        for (int q = 0; q < NG; ++q) dcol[t][e][q] = carry_ld(cb + (2 * t + e) * NG + q);
-  } else {
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int q = 0; q < NG; ++q) dcol[t][e][q] = 0.0;
-  }
+      for (int q = 0; q < NG; ++q) dcol[t][e][q] = 0.0;
 
   // fragment loads of step (g, t) of a panel (b0 = its element (r0, c0)), 16 B
   // per lane, branch-free: a row past H clamps (its P is 0), a column past the
@@ -422,27 +373,15 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
 
   // column sums over the strip's panels: D_b[m][n] at lane 16m + 4b + n holds
   // column pair 4b + m = pc, column c = 4q + n.  Whole slot, 16-B stores
-  // (columns the finalize never reads: don't care).  The first segment of a
-  // chain leaves its accumulators to the second instead.
-  if (sp.cout >= 0) {
-    double* cb = cc.buf + ((int64_t)sp.cout * 256 + threadIdx.x) * CARRY_PER_THREAD;
+  // (columns the finalize never reads: don't care).
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+  for (int q = 0; q < NG; ++q) {
+    const int cc = 4 * q + n4;
+    if (cc < ncol) {
+      double* out = colpart + ((int64_t)sp.slot * ncol + cc) * MF_CW;
 #pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int q = 0; q < NG; ++q) cb[(2 * t + e) * NG + q] = dcol[t][e][q];
-    carry_publish(cc, sp.cout);
-  } else {
-#pragma unroll
-    for (int q = 0; q < NG; ++q) {
-      const int c4 = 4 * q + n4;
-      if (c4 < ncol) {
-        double* out = colpart + ((int64_t)sp.slot * ncol + c4) * MF_CW;
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          *(d2*)(out + cw0 + 32 * t + 2 * pc) = d2{dcol[t][0][q], dcol[t][1][q]};
-      }
+      for (int t = 0; t < NT; ++t)
+        *(d2*)(out + cw0 + 32 * t + 2 * pc) = d2{dcol[t][0][q], dcol[t][1][q]};
     }
   }
   MF_TRACE_END
@@ -490,7 +429,6 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
   __shared__ int hready[4], hdone[4];   // row groups handed / taken per segment
   __shared__ __attribute__((aligned(16))) double stg[NW][16 * 32];
   const SymStrip sp = strips[blockIdx.x];
-  if (sp.npan <= 0) return;   // (padding: plans with chained segments never run this kernel)
   if (run && !ldg(run)) return;
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
@@ -721,15 +659,13 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
                                                      const double* __restrict__ pk, int ncol,
                                                      double* __restrict__ rowpart,
                                                      double* __restrict__ colpart,
-                                                     const int* __restrict__ run,
-                                                     StripCarry cc) {
+                                                     const int* __restrict__ run) {
   constexpr int LDP = MF_LDP;
   constexpr int MF_WC = MF_CW / 4; // columns per wave
   constexpr int MF_NT = MF_WC / 32;
   __shared__ double red[2][4][256];
   __shared__ __attribute__((aligned(16))) double stg[4][16 * LDP];
   const SymStrip sp = strips[blockIdx.x];
-  if (sp.npan <= 0) return;       // padding of a chained-segment plan (split_strips)
   if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
@@ -755,19 +691,8 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
         brow[t][s][e] = col < ncc ? v : 0.0;
       }
   d4 dcol[MF_NT][2];
-  if (sp.cin >= 0) {   // chained segment: the first's accumulators (as k_sym_mfma)
-    carry_wait(cc, sp.cin);
-    const double* cb = cc.buf + ((int64_t)sp.cin * 256 + threadIdx.x) * CARRY_PER_THREAD;
 #pragma unroll
-    for (int t = 0; t < MF_NT; ++t)
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dcol[t][e][r] = carry_ld(cb + (2 * t + e) * 4 + r);
-  } else {
-#pragma unroll
-    for (int t = 0; t < MF_NT; ++t) dcol[t][0] = dcol[t][1] = d4{0.0, 0.0, 0.0, 0.0};
-  }
+  for (int t = 0; t < MF_NT; ++t) dcol[t][0] = dcol[t][1] = d4{0.0, 0.0, 0.0, 0.0};
 
   auto load_cf = [&](uint64_t b0, int64_t ws, int H, int nci, int g, int t, d2* cf) {
     asm volatile("" : "+s"(b0));
@@ -879,18 +804,8 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
     curb = nxb;
   }
 
-  // column sums over the strip's panels (whole slot, 16-B stores), or the
-  // carry of a chain's first segment
-  if (sp.cout >= 0) {
-    double* cb = cc.buf + ((int64_t)sp.cout * 256 + threadIdx.x) * CARRY_PER_THREAD;
-#pragma unroll
-    for (int t = 0; t < MF_NT; ++t)
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) cb[(2 * t + e) * 4 + r] = dcol[t][e][r];
-    carry_publish(cc, sp.cout);
-  } else if (lo < ncol) {
+  // column sums over the strip's panels (whole slot, 16-B stores)
+  if (lo < ncol) {
     double* out = colpart + ((int64_t)sp.slot * ncol + lo) * MF_CW;
 #pragma unroll
     for (int t = 0; t < MF_NT; ++t)
@@ -1043,22 +958,20 @@ __global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpa
 // kernel (capi.hip build_strips; bitwise the same products) -- 1: 3-4 columns
 // only (at 5-8 the pair form runs ~14 % slower per byte and a short launch's
 // tail does not pay it back), 2 (forced, SGV_MF_PAIR=1): every column count
-// (a plan with chained segments never picks the pair kernel: split_strips)
 template <int NG, bool PP = false>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
-                      const int* run, int pks, bool ragged, int pair, const StripCarry& cc,
-                      hipStream_t st) {
+                      const int* run, int pks, bool ragged, int pair, hipStream_t st) {
   // prefetch depth 2 measured best (PD 1/2/4: 11.64/11.16/12.27 ms at NC=4, M=1e6)
   if (ragged)
     hipLaunchKernelGGL((k_sym_mfma<NG, 2, true, false, PP>), dim3(nstrips), dim3(256), 0, st,
-                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks, cc);
+                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else if (pair >= (NG == 1 ? 1 : 2))
     hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else
     hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP>), dim3(nstrips), dim3(256), 0, st,
-                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks, cc);
+                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
 }
 
 // 5-8-column strip passes read Pk PAIRED (k_pack) unless the plan runs the
@@ -1085,8 +998,7 @@ hipError_t launch_pk(const PassArgs& pa, int nc, int64_t mpad, double* d_pk, hip
 
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                            const PassArgs& pa, const double* d_pk, double* rowpart,
-                           double* colpart, bool ragged, int pair, const StripCarry& cc,
-                           hipStream_t st) {
+                           double* colpart, bool ragged, int pair, hipStream_t st) {
   if (nc < 1 || nc > 16) return hipErrorInvalidValue;
   if (nstrips <= 0) return hipSuccess;
   const int pks = nc > 8 ? 16 : nc <= 4 ? 4 : 8;
@@ -1104,22 +1016,22 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
   // spills sit outside the row-group loop; the 8-wave row-sum combine and the
   // 4x4x4 form's DPP reductions and 4x the MFMA issues cost more than they save.
   switch ((nc + 3) / 4) {
-    case 1: launch_mf<1>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, cc, st); break;
+    case 1: launch_mf<1>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
     case 2:
       if (strip_pk_paired(nc, pair))
         launch_mf<2, true>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks,
-                           ragged, pair, cc, st);
+                           ragged, pair, st);
       else
         launch_mf<2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged,
-                     pair, cc, st);
+                     pair, st);
       break;
     default:
       if (ragged)
         hipLaunchKernelGGL((k_sym_mfma16<2, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                           d_sitems, d_pk, nc, rowpart, colpart, pa.run, cc);
+                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       else
         hipLaunchKernelGGL((k_sym_mfma16<2>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                           d_sitems, d_pk, nc, rowpart, colpart, pa.run, cc);
+                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       break;
   }
   return hipGetLastError();
