@@ -255,6 +255,13 @@ class BlockLD:
             return self.matvec_R(v)
         return (1 - self.s) * self.matvec_R(v) + self.s * v
 
+    def matmat_Rs(self, V):
+        """Column by column (each column exactly its matvec_Rs: the batched
+        reference algebra, cg_scipy_batch, then equals cg_scipy bit for bit)."""
+        V = np.asarray(V, dtype=np.float64)
+        return np.stack([self.matvec_Rs(np.ascontiguousarray(V[:, i])) for i in range(V.shape[1])],
+                        axis=1)
+
 
 class CoupledLD:
     """Band pieces with corner couplings: the layout that lets ranks share one
@@ -325,6 +332,10 @@ def _panel_lib():
                                                       ctypes.c_int, ctypes.c_void_p,
                                                       ctypes.c_void_p]
             lib.oracle_panel_block_matmat.restype = ctypes.c_int
+            lib.oracle_panel_range_matmat.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                                                      ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                                                      ctypes.c_void_p, ctypes.c_void_p]
+            lib.oracle_panel_range_matmat.restype = ctypes.c_int
         _PANEL_LIB.append(lib)
     return _PANEL_LIB[0]
 
@@ -377,6 +388,7 @@ class PanelLD:
         self.s, self.H = s, H
         self.blocks = []          # (offset, n, [panel arrays])
         self.sizes = []
+        self._inner_pool = None
 
     @property
     def bounds(self):
@@ -392,6 +404,8 @@ class PanelLD:
         self.blocks.append((off, n, panels))
         self.sizes.append(n)
 
+    RANGE = 16   # panels per task of the C product (a fixed cut: sums do not depend on threads)
+
     def _block_product(self, blk, V, Y):
         off, n, panels = blk
         Vb, Yb = V[off:off + n], Y[off:off + n]
@@ -400,13 +414,28 @@ class PanelLD:
             import ctypes
 
             Vc = np.ascontiguousarray(Vb)
-            Yc = np.empty_like(Vc)
             ptrs = (ctypes.c_void_p * len(panels))(*[P.ctypes.data for P in panels])
-            rc = lib.oracle_panel_block_matmat(n, self.H, ptrs, Vc.shape[1], Vc.ctypes.data,
-                                               Yc.ctypes.data)
-            if rc != 0:
-                raise RuntimeError("oracle_panel_block_matmat failed")
-            Yb[...] = Yc
+            # the block's panels in fixed ranges, each into its own partial, the
+            # partials added in range order; the ranges of a block with few
+            # blocks in the product run on the pool too (C3: 8 blocks, 16 cores)
+            cuts = list(range(0, len(panels), self.RANGE)) + [len(panels)]
+            parts = [np.empty_like(Vc) for _ in cuts[:-1]]
+
+            def run(i):
+                rc = lib.oracle_panel_range_matmat(n, self.H, ptrs, cuts[i], cuts[i + 1],
+                                                   Vc.shape[1], Vc.ctypes.data, parts[i].ctypes.data)
+                if rc != 0:
+                    raise RuntimeError("oracle_panel_range_matmat failed")
+
+            if len(parts) > 1 and self._inner_pool is not None:
+                list(self._inner_pool.map(run, range(len(parts))))
+            else:
+                for i in range(len(parts)):
+                    run(i)
+            acc = parts[0]
+            for q in parts[1:]:
+                acc += q
+            Yb[...] = acc
             return
         for g, P in enumerate(panels):
             r0 = g * self.H
@@ -425,6 +454,7 @@ class PanelLD:
         V = np.asarray(V, dtype=np.float64)
         Y = np.zeros_like(V)
         nw = _oracle_workers()
+        self._inner_pool = None
         if nw <= 1 or len(self.blocks) < 2:
             for blk in self.blocks:
                 self._block_product(blk, V, Y)
@@ -432,7 +462,13 @@ class PanelLD:
         from concurrent.futures import ThreadPoolExecutor
 
         with _blas_single_thread(), ThreadPoolExecutor(nw) as ex:
-            list(ex.map(lambda blk: self._block_product(blk, V, Y), self.blocks))
+            if len(self.blocks) < nw:   # few big blocks: their panel ranges on a second pool
+                with ThreadPoolExecutor(nw) as inner:
+                    self._inner_pool = inner
+                    list(ex.map(lambda blk: self._block_product(blk, V, Y), self.blocks))
+                    self._inner_pool = None
+            else:
+                list(ex.map(lambda blk: self._block_product(blk, V, Y), self.blocks))
         return Y
 
     def matvec_R(self, v):
@@ -573,6 +609,70 @@ def cg_track(matvec_rs, gw, gam2, b, x0, rsx0, maxiter, red, rtol=1e-5):
     return x, rsx, maxiter, maxiter, nmv
 
 
+def cg_scipy_batch(ld_cols, gws, gam2s, B, X0, maxiter, red, rtol=1e-5):
+    """cg_scipy on A_j = gws[j]*R_s + gam2s[j]*I for several columns in lockstep
+    -- the reference's own algebra (src/sgvamp.py:312-316,332: one con_grad per
+    column, the warm start's residual from a direct product, no carried R_s x)
+    with the products of the columns still iterating on one LD matrix taken
+    together.  An LD object whose matmat_Rs gives each column the bits it gives
+    alone (PanelLD with oracle/panel_ld.c) makes every column exactly its
+    cg_scipy run.  Returns (X, info, n_iter, n_matvec) per column."""
+    nc = len(B)
+    X = [np.array(x, dtype=np.float64).ravel().copy() for x in X0]
+    Bv = [np.asarray(b, dtype=np.float64).ravel() for b in B]
+    info, n_it, n_mv = [maxiter] * nc, [maxiter] * nc, [0] * nc
+    atol, R, P, rho_prev, active = [0.0] * nc, [None] * nc, [None] * nc, [None] * nc, []
+    warm = []
+    for j in range(nc):
+        bnrm2 = red.norm(Bv[j])
+        atol[j] = max(0.0, rtol * bnrm2)
+        if bnrm2 == 0:
+            X[j], info[j], n_it[j] = Bv[j].copy(), 0, 0
+            continue
+        if X[j].any():
+            warm.append(j)
+        else:
+            R[j] = Bv[j].copy()
+        active.append(j)
+
+    def products(js, vecs):
+        out = {}
+        for ld, cols in ld_cols:
+            cols = [j for j in cols if j in js]
+            if cols:
+                Y = ld.matmat_Rs(np.stack([vecs[j] for j in cols], axis=1))
+                for i, j in enumerate(cols):
+                    out[j] = gws[j] * Y[:, i] + gam2s[j] * vecs[j]
+        return out
+
+    for j, q in products(warm, X).items():          # r = b - A x0 (iterative.py:392)
+        R[j] = Bv[j] - q
+        n_mv[j] += 1
+    for it in range(maxiter):
+        still = []
+        for j in active:
+            if red.norm(R[j]) < atol[j]:
+                info[j], n_it[j] = 0, it
+                continue
+            rho_cur = red.dot(R[j], R[j])
+            if it > 0:
+                P[j] *= rho_cur / rho_prev[j]
+                P[j] += R[j]
+            else:
+                P[j] = R[j].copy()
+            rho_prev[j] = rho_cur
+            still.append(j)
+        active = still
+        if not active:
+            break
+        for j, q in products(active, P).items():
+            n_mv[j] += 1
+            alpha = rho_prev[j] / red.dot(P[j], q)
+            X[j] += alpha * P[j]
+            R[j] -= alpha * q
+    return X, info, n_it, n_mv
+
+
 def cg_track_batch(ld_cols, gws, gam2s, B, X0, RSX0, maxiter, red, rtol=1e-5):
     """cg_track on several columns in lockstep: every column runs scipy 1.15.3's
     cg (iterative.py:375-422) with its own stop test, scalars and iteration
@@ -655,7 +755,9 @@ def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-
     each column exactly scipy's cg, the LD products of the columns on one LD
     matrix taken together) -- the same per-column arithmetic apart from the
     products' summation order, at the cost of max(CG iterations) LD sweeps
-    instead of their sum; needs rs_recurrence and LD objects with matmat_Rs.
+    instead of their sum; LD objects with matmat_Rs.  With rs_recurrence off
+    (the reference's algebra) the columns run cg_scipy_batch and gamw's R_s
+    products are direct, taken together per LD matrix.
     For full-size configurations (tests/test_gpu_configs.py).
 
     rs_recurrence: carry R_s x through both CG solves (cg_track) instead of the
@@ -723,8 +825,6 @@ def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-
         der = der_denoiser_meta(r1s, gam1s, a, lam, omegas, sigmas)     # :285
         it_cg, it_info, passes = [], [], 0
         if batched:
-            if not rs_recurrence:
-                raise ValueError("batched CG needs rs_recurrence=True")
             pre = []
             for k in range(K):                     # :285-313 for every cohort first
                 alpha1 = red.mean(der[k], M_tot)
@@ -738,20 +838,41 @@ def infer(lds, ld_of, r_list, N_list, iterations, *, rho=0.5, gamw=5.0, gam1=1e-
             cols = {}
             for k in range(K):
                 cols.setdefault(ld_of[k], []).extend([2 * k, 2 * k + 1])
-            X, RSX, info, nit, nmv = cg_track_batch(
-                [(lds[l], c) for l, c in cols.items()],
-                [gamw_k[k] for k in range(K) for _ in (0, 1)],
-                [pre[k][1] for k in range(K) for _ in (0, 1)],
-                [v for k in range(K) for v in (pre[k][3], pre[k][4])],
-                [v for k in range(K) for v in (xhat2[k], sig2u_prev[k])],
-                [v for k in range(K) for v in (rs_x2[k], rs_s2u[k])], cg_maxit, red)
+            ldc = [(lds[l], c) for l, c in cols.items()]
+            gws2 = [gamw_k[k] for k in range(K) for _ in (0, 1)]
+            g2s = [pre[k][1] for k in range(K) for _ in (0, 1)]
+            Bs = [v for k in range(K) for v in (pre[k][3], pre[k][4])]
+            X0s = [v for k in range(K) for v in (xhat2[k], sig2u_prev[k])]
+            if rs_recurrence:
+                X, RSX, info, nit, nmv = cg_track_batch(
+                    ldc, gws2, g2s, Bs, X0s,
+                    [v for k in range(K) for v in (rs_x2[k], rs_s2u[k])], cg_maxit, red)
+            else:   # the reference's algebra, columns in lockstep (cg_scipy_batch)
+                X, info, nit, nmv = cg_scipy_batch(ldc, gws2, g2s, Bs, X0s, cg_maxit, red)
+                RSX = [None] * (2 * K)
+            xs_new = []
+            for k in range(K):
+                x2 = X[2 * k]
+                if lmmse_damp:                                          # :322-323
+                    x2 = rho * x2 + (1 - rho) * xhat2[k]
+                xs_new.append(x2)
+            if not rs_recurrence and learn_gamw:
+                # gamw learning's R_s xhat2 and R_s Sigma2_u as direct products
+                # (:352,359), every cohort's taken together per LD matrix
+                for l, c in cols.items():
+                    ks = sorted({j // 2 for j in c})
+                    V = np.stack([xs_new[k] for k in ks] + [X[2 * k + 1] for k in ks], axis=1)
+                    Y = lds[l].matmat_Rs(V)
+                    for i, k in enumerate(ks):   # contiguous, as a matvec's result
+                        RSX[2 * k] = np.ascontiguousarray(Y[:, i])
+                        RSX[2 * k + 1] = np.ascontiguousarray(Y[:, len(ks) + i])
+                        nmv[2 * k] += 1
+                        nmv[2 * k + 1] += 1
             for k in range(K):
                 alpha1, gam2, r2, _, u = pre[k]
-                x2, rx2, s2u, rs2 = X[2 * k], RSX[2 * k], X[2 * k + 1], RSX[2 * k + 1]
-                x2_prev = xhat2[k]
-                if lmmse_damp:                                          # :322-323
+                x2, rx2, s2u, rs2 = xs_new[k], RSX[2 * k], X[2 * k + 1], RSX[2 * k + 1]
+                if lmmse_damp and rs_recurrence:                        # :322-323
                     rx2 = rho * rx2 + (1 - rho) * rs_x2[k]
-                    x2 = rho * x2 + (1 - rho) * x2_prev
                 rs_x2[k], xhat2[k] = rx2, x2
                 sig2u_prev[k], rs_s2u[k] = s2u, rs2
                 uf = u.astype(np.float64)

@@ -242,7 +242,7 @@ def _gate_50(nblk, size, K, tmp_path, its=50, ref_algebra=False):
     prior = dict(prior_vars=[0.0, 0.8 / cm * N / (N * K)], prior_probs=[0.5, 0.5])
     x0 = beta * np.sqrt(N)
     r_list = [eng.get_vector(hb.VEC_R, k) for k in range(K)]
-    if ref_algebra:
+    if ref_algebra is True:
         L = vo.BlockLD([eng.get_ld_block(0, b) for b in range(nblk)], s=0.0)
     else:
         L = _host_ld(eng, (nblk, size), nblk)
@@ -257,8 +257,14 @@ def _gate_50(nblk, size, K, tmp_path, its=50, ref_algebra=False):
     eng.close()
     _log("%dx%d K=%d: GPU %d iterations done" % (nblk, size, K, its))
     if ref_algebra:
+        # True: dense blocks and np.dot products, con_grad one column at a time;
+        # "batched": the same algebra on the packed host LD, the columns' CG in
+        # lockstep with each column's products the bits it gets alone
+        # (oracle.cg_scipy_batch) -- fast enough for C3's full size
         t = vo.infer([L], [0] * K, r_list, [N] * K, its, rho=0.5, gamw=5.0, gam1=1e-6, x0=x0,
-                     seed=SEED, reducer=vo.Reducer("numpy"), rs_recurrence=False, batched=False,
+                     seed=SEED, reducer=vo.Reducer("numpy"), rs_recurrence=False,
+                     batched=ref_algebra == "batched",
+                     progress=lambda it: _log("oracle (reference algebra) iteration %d" % it),
                      **prior, **run)
     else:
         t = vo.infer([L], [0] * K, r_list, [N] * K, its, rho=0.5, gamw=5.0, gam1=1e-6, x0=x0,
@@ -312,6 +318,24 @@ def test_50_iterations_vs_reference_algebra(tmp_path):
     (:316,332).  Bar: xhat within 1e-5 relative at every iteration, CG iteration
     counts and EM steps equal at every iteration."""
     errs, cg, em = _gate_50(4, 12500, 4, tmp_path, ref_algebra=True)
+    assert max(errs) < 1e-5, max(errs)
+    assert cg[0] == cg[1]
+    assert em[0] == em[1]
+
+
+@pytest.mark.timeout(1500)
+@pytest.mark.skipif(os.environ.get("SGV_FULL_GATE") != "1",
+                    reason="~4 min of host oracle: run with SGV_FULL_GATE=1 "
+                           "(profiles/r06/c3_ref_algebra_gate.log)")
+def test_c3_50_iterations_vs_reference_algebra(tmp_path):
+    """the reference's own algebra at C3's full size (8 x
+    25,000, K = 4 sharing the LD: the f64 MFMA pass), 50 iterations -- the oracle
+    with direct R_s xhat2 / R_s Sigma2u products (src/sgvamp.py:352,359),
+    scipy's cg per column with its warm-start residual from a direct product
+    (:316,332) and np.dot reductions, against the GPU default path (carried
+    R_s x, batched passes, blocked sums).  Bar: xhat within 1e-5 relative at
+    every iteration, CG iteration counts and EM steps equal at every iteration."""
+    errs, cg, em = _gate_50(8, 25000, 4, tmp_path, ref_algebra="batched")
     assert max(errs) < 1e-5, max(errs)
     assert cg[0] == cg[1]
     assert em[0] == em[1]

@@ -58,6 +58,29 @@ def test_oracle_matches_reference(name, rs):
     np.testing.assert_allclose(np.array(t["metrics"]), c.metrics_csv, rtol=1e-9, atol=1e-12)
 
 
+@pytest.mark.parametrize("name", ["k2_shared", "k4_shared_s_damp", "k10_shared", "k4_long50",
+                                  "k2_distinct"])
+def test_batched_reference_algebra_is_bitwise_cg_scipy(name):
+    """The reference's algebra with the cohorts' CG columns in lockstep
+    (cg_scipy_batch, direct R_s products for gamw -- the form the C3 full-size
+    gate uses) is bit for bit the column-at-a-time run pinned above, when each
+    column's product is the bits it gets alone (BlockLD.matmat_Rs)."""
+    if name not in CASES:
+        pytest.skip("no fixture %s" % name)
+    c = Case(name)
+    lds = [vo.BlockLD(b, s=c.flags["s"]) for b in c.ld_blocks]
+    with np.errstate(all="ignore"):
+        one = vo.infer(lds, c.ld_of, list(c.r), c.N, c.flags["iterations"], x0=c.x0,
+                       **c.kwargs())
+        bat = vo.infer(lds, c.ld_of, list(c.r), c.N, c.flags["iterations"], x0=c.x0,
+                       batched=True, **c.kwargs())
+    for it in range(c.flags["iterations"]):
+        np.testing.assert_array_equal(np.asarray(bat["xhat"][it]), np.asarray(one["xhat"][it]))
+    assert bat["cg_iters"] == one["cg_iters"] and bat["cg_info"] == one["cg_info"]
+    assert list(bat["em_steps"]) == list(one["em_steps"])
+    np.testing.assert_array_equal(np.array(bat["csv"]), np.array(one["csv"]))
+
+
 def test_lam0_repr():
     # the reference's lam is a Python float until the first EM update
     c = Case("k1_dense")

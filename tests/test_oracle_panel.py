@@ -27,7 +27,7 @@ def _blocks(sizes, seed=0):
 @pytest.mark.parametrize("ncol", [1, 3, 8, 16])
 def test_c_panel_product_vs_dense(ncol, monkeypatch):
     assert vo._panel_lib() is not None, "build first: make -C oracle"
-    blocks = _blocks([700, 256, 1, 513])
+    blocks = _blocks([700, 256, 1, 513, 4500])   # 4500: 18 panels, two ranges
     L = vo.PanelLD()
     for B in blocks:
         L.add_block(B)
@@ -40,10 +40,15 @@ def test_c_panel_product_vs_dense(ncol, monkeypatch):
         ref[off:off + n] = B @ V[off:off + n]
         off += n
     outs = {}
-    for th in ("1", "4"):
+    for th in ("1", "4", "8"):   # 8 > 5 blocks: the panel ranges on the inner pool
         monkeypatch.setenv("SGV_ORACLE_THREADS", th)
         outs[th] = L.matmat_R(V)
     np.testing.assert_array_equal(outs["1"], outs["4"])
+    np.testing.assert_array_equal(outs["1"], outs["8"])
+    # a column gives the same bits alone as with others (the batched reference
+    # algebra relies on it)
+    monkeypatch.setenv("SGV_ORACLE_THREADS", "4")
+    np.testing.assert_array_equal(L.matmat_R(V[:, :1])[:, 0], outs["1"][:, 0])
     assert np.max(np.abs(outs["1"] - ref)) <= 1e-12 * np.max(np.abs(ref))
     monkeypatch.setenv("SGV_ORACLE_NUMPY", "1")
     vo._PANEL_LIB.clear()
