@@ -351,7 +351,8 @@ static int plan_walks(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
     if (lb.fmt != 1) continue;
     const int np = (int)lb.poff.size();
     const int R = (int)(lb.ext / SYM_H);
-    const int W = std::max(4, 2 * (R - 1));
+    const char* wl = ab_env("SGV_WALK_LEN");   // A/B: walk length (panels), at least R - 1
+    const int W = wl ? std::max(std::max(1, R - 1), std::atoi(wl)) : std::max(4, 2 * (R - 1));
     int prev_cslot = -1;
     for (int g0 = 0; g0 < np; g0 += W) {
       SymWalk w;
