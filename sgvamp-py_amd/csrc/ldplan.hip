@@ -351,8 +351,11 @@ static int plan_walks(sgv_ctx* c, int ld, const std::vector<SymItem>& items,
     if (lb.fmt != 1) continue;
     const int np = (int)lb.poff.size();
     const int R = (int)(lb.ext / SYM_H);
-    const char* wl = ab_env("SGV_WALK_LEN");   // A/B: walk length (panels), at least R - 1
-    const int W = wl ? std::max(std::max(1, R - 1), std::atoi(wl)) : std::max(4, 2 * (R - 1));
+    // walk length 2 (R - 1): measured against 6, 12 and 16 panels at R = 5 (round 6,
+    // profiles/r06/walklen_*.jsonl): 6 +12 %, 12 +43 % (1.3 rounds of walks on the 256
+    // CUs), 16 even -- the count of walks against the CUs matters more than the
+    // head-panel share
+    const int W = std::max(4, 2 * (R - 1));
     int prev_cslot = -1;
     for (int g0 = 0; g0 < np; g0 += W) {
       SymWalk w;
