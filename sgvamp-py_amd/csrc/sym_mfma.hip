@@ -95,11 +95,7 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // PP (NG = 2): Pk in k_pack's PAIRED layout, so a lane's two column groups
 // (columns n4 and 4 + n4) of one Pk row are one 16-B load: half the P-operand
 // load instructions through the texture-address unit per row group
-// IP (PD == NT): the fragment ring used in place -- step t's registers are read
-// by its LDS write and column MFMAs, then reloaded with the next row group's
-// step t, so PD = 4 steps of registers hold 3 steps of loads in flight while a
-// step computes (the copy form holds PD - 1 ahead in PD + 1 steps of registers)
-template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false, bool IP = false>
+template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -110,7 +106,6 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
   constexpr int WC = MF_CW / NW;   // columns per wave
   constexpr int NT = WC / 32;      // 32-column steps per wave
   static_assert(PD >= 1 && PD <= NT && NT % PD == 0, "prefetch depth divides the steps");
-  static_assert(!IP || PD == NT, "in-place ring: one slot per step");
   constexpr int RW = 4 * NG;       // row-sum stride of wrow
   __shared__ __attribute__((aligned(16))) double rowbuf[NW * SYM_H * RW];   // wrow
   // the per-wave transpose tile: 16 rows x 32 columns, 16-B piece (row r, pair
@@ -259,33 +254,19 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
       d2 rfb[DEF ? 2 : 1][4];                            // row fragments (DEF: this and the previous step)
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        d2 cfc[IP ? 1 : 4];
+        d2 cf[4];
         d2* rf = rfb[DEF ? (t & 1) : 0];
         const int slot = t % PD;                       // compile-time after unrolling
-        d2* cf = IP ? cfq[slot] : cfc;
-        if constexpr (!IP) {
 #pragma unroll
-          for (int a = 0; a < 4; ++a) cfc[a] = cfq[slot][a];
-          // step + PD goes out here, ahead of this step's LDS and MFMA work
-          if (t + PD < NT) {
-            load_cf(curb, cur.w, cur.H, cur.nc, g, t + PD, cfq[slot]);
-          } else {
-            load_cf(gb, gw, gH, gnc, gn, t + PD - NT, cfq[slot]);
-            if (t + PD == NT) load_bcol(gr0, gH, gz, gn, bcn);
-          }
+        for (int a = 0; a < 4; ++a) cf[a] = cfq[slot][a];
+        // step + PD goes out here, ahead of this step's LDS and MFMA work
+        if (t + PD < NT) {
+          load_cf(curb, cur.w, cur.H, cur.nc, g, t + PD, cfq[slot]);
+        } else {
+          load_cf(gb, gw, gH, gnc, gn, t + PD - NT, cfq[slot]);
+          if (t + PD == NT) load_bcol(gr0, gH, gz, gn, bcn);
         }
-        // IP: the next row group's step t goes out once this step's fragments are
-        // used (after its LDS write and column MFMAs), into the same registers
-        auto ip_issue = [&]() {
-          if constexpr (IP) {
-            load_cf(gb, gw, gH, gnc, gn, t, cfq[slot]);
-            if (t == 1) load_bcol(gr0, gH, gz, gn, bcn);
-          }
-        };
-        if (t >= ntp) {                                // wave-uniform: past the chunk / item
-          ip_issue();
-          continue;
-        }
+        if (t >= ntp) continue;                        // wave-uniform: past the chunk / item
         if (RAG && cur.nc < ncc) band_zero(cur.nc, t, cf);   // uniform: a band item's stored end
         lds_order();                                   // previous step's tile reads issued
 #pragma unroll
@@ -349,7 +330,6 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
           row_mfma(rf, t);
         }
         __builtin_amdgcn_s_setprio(0);
-        ip_issue();
       }
       // row sums: the 4 blocks (lanes differing in bits 2,3; DPP row rotations),
       // kept per wave for the panel
@@ -978,12 +958,6 @@ __global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpa
 // kernel (capi.hip build_strips; bitwise the same products) -- 1: 3-4 columns
 // only (at 5-8 the pair form runs ~14 % slower per byte and a short launch's
 // tail does not pay it back), 2 (forced, SGV_MF_PAIR=1): every column count
-// SGV_MF_IP=1 (A/B, with SGV_AB=1): the in-place fragment ring (IP, 4 steps)
-static bool mf_inplace() {
-  const char* e = ab_env("SGV_MF_IP");
-  return e && e[0] == '1';
-}
-
 template <int NG, bool PP = false>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
@@ -995,9 +969,6 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
   else if (pair >= (NG == 1 ? 1 : 2))
     hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_inplace())
-    hipLaunchKernelGGL((k_sym_mfma<NG, 4, false, true, PP, true>), dim3(nstrips), dim3(256), 0,
-                       st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else
     hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP>), dim3(nstrips), dim3(256), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
