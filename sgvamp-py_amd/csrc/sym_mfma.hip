@@ -71,6 +71,26 @@ __device__ __forceinline__ void lds_order() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// the double of the lane of quad a ^ (bq & 2) in this lane's 16-lane row, bq =
+// lane bits 2-3: lane id ((l & ~4) | 4 (a & 1)) ^ 8 (a >> 1) (ds_swizzle bit
+// mask mode within 32 lanes: ((l & and) | or) ^ xor); a is a compile-time
+// constant after unrolling
+template <int A>
+__device__ __forceinline__ int swz_dw(int v) {
+  return __builtin_amdgcn_ds_swizzle(v, 0x1B | ((A & 1) << 7) | ((A >> 1) << 13));
+}
+__device__ __forceinline__ double swz_quad(double v, int a) {
+  const int2 w = __builtin_bit_cast(int2, v);
+  int2 r;
+  switch (a) {
+    case 0: r.x = swz_dw<0>(w.x); r.y = swz_dw<0>(w.y); break;
+    case 1: r.x = swz_dw<1>(w.x); r.y = swz_dw<1>(w.y); break;
+    case 2: r.x = swz_dw<2>(w.x); r.y = swz_dw<2>(w.y); break;
+    default: r.x = swz_dw<3>(w.x); r.y = swz_dw<3>(w.y); break;
+  }
+  return __builtin_bit_cast(double, r);
+}
+
 constexpr int MF_CW = 512;   // chunk width (class 1 items)
 constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conflict-free both ways
 
@@ -95,7 +115,14 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // PP (NG = 2): Pk in k_pack's PAIRED layout, so a lane's two column groups
 // (columns n4 and 4 + n4) of one Pk row are one 16-B load: half the P-operand
 // load instructions through the texture-address unit per row group
-template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false>
+// SW: column-part B operands without the 4x replication over the MFMA blocks --
+// blocks 0-1 take a row group's 4-row sets in the order 0 1 2 3, blocks 2-3 in
+// the order 2 3 0 1 (fragment a of a lane is row set a ^ (bq & 2)), so one
+// Pk load per row group (lane: row set bq) holds every set a block needs and
+// ds_swizzle hands each lane its set for fragment a; the R fragment loads stay
+// whole 128-B lines.  Row sums bitwise unchanged; column sums of blocks 2-3
+// in another order
+template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false, bool SW = false>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -181,14 +208,23 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
     const int xc = cw0 + 32 * t + 2 * lo;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
-      const int rB = 16 * g + 4 * a + hi;
+      const int rB = 16 * g + 4 * (SW ? a ^ (bq & 2) : a) + hi;
       const double* row = (const double*)b0 + (int64_t)(rB < H ? rB : H - 1) * ws;
       cf[a] = ldg_nt((const d2*)(row + (xc < (RAG ? nci : ncc) ? xc : 0)));
     }
   };
   // column-part B operands of row group g of a panel (first row r0): P at its
   // rows; zero past H and, for the diagonal panel, in the diagonal-block waves
+  // (SW: bc[0] = this lane's row set bq, handed out by swz_quad)
   auto load_bcol = [&](int r0, int H, bool zero, int g, double (*bc)[NG]) {
+    if constexpr (SW) {
+      const int rB = 16 * g + 4 * bq + hi;
+      double v[NG];
+      ld_prow(r0 + (rB < H ? rB : 0), v);
+#pragma unroll
+      for (int q = 0; q < NG; ++q) bc[0][q] = (rB < H && !zero) ? v[q] : 0.0;
+      return;
+    }
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int rB = 16 * g + 4 * a + hi;
@@ -236,10 +272,19 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
       const int gr0 = same ? cur.r0 : nx.r0;
       const bool gz = dhalf && gr0 == c0;
       double bcol[4][NG];
+      if constexpr (SW) {
+        // fragment a's set a ^ (bq & 2) from the lane of quad a ^ (bq & 2) of
+        // this 16-lane row
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int q = 0; q < NG; ++q) bcol[a][q] = bcn[a][q];
+          for (int q = 0; q < NG; ++q) bcol[a][q] = swz_quad(bcn[0][q], a);
+      } else {
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int q = 0; q < NG; ++q) bcol[a][q] = bcn[a][q];
+      }
       double drow[4][NG];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -270,7 +315,8 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
         if (RAG && cur.nc < ncc) band_zero(cur.nc, t, cf);   // uniform: a band item's stored end
         lds_order();                                   // previous step's tile reads issued
 #pragma unroll
-        for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[a];
+        for (int a = 0; a < 4; ++a)
+          *(d2*)(sb + 32 * (4 * (SW ? a ^ (bq & 2) : a) + hi) + 2 * (lo ^ hi)) = cf[a];
         lds_order();                                   // tile written
         // the row fragment reads go out right behind the writes (a wave's DS
         // operations execute in order); the column MFMAs cover their latency
@@ -958,6 +1004,12 @@ __global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpa
 // kernel (capi.hip build_strips; bitwise the same products) -- 1: 3-4 columns
 // only (at 5-8 the pair form runs ~14 % slower per byte and a short launch's
 // tail does not pay it back), 2 (forced, SGV_MF_PAIR=1): every column count
+// SGV_MF_SW=1 (A/B, with SGV_AB=1): the de-replicated column B operands (SW)
+static bool mf_swizzled() {
+  const char* e = ab_env("SGV_MF_SW");
+  return e && e[0] == '1';
+}
+
 template <int NG, bool PP = false>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
@@ -969,6 +1021,9 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
   else if (pair >= (NG == 1 ? 1 : 2))
     hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
+  else if (mf_swizzled())
+    hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP, true>), dim3(nstrips), dim3(256), 0,
+                       st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else
     hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP>), dim3(nstrips), dim3(256), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
