@@ -115,14 +115,14 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // PP (NG = 2): Pk in k_pack's PAIRED layout, so a lane's two column groups
 // (columns n4 and 4 + n4) of one Pk row are one 16-B load: half the P-operand
 // load instructions through the texture-address unit per row group
-// SW: column-part B operands without the 4x replication over the MFMA blocks --
+// Column-part B operands without the 4x replication over the MFMA blocks:
 // blocks 0-1 take a row group's 4-row sets in the order 0 1 2 3, blocks 2-3 in
-// the order 2 3 0 1 (fragment a of a lane is row set a ^ (bq & 2)), so one
-// Pk load per row group (lane: row set bq) holds every set a block needs and
-// ds_swizzle hands each lane its set for fragment a; the R fragment loads stay
-// whole 128-B lines.  Row sums bitwise unchanged; column sums of blocks 2-3
-// in another order
-template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false, bool SW = false>
+// the order 2 3 0 1 (fragment a of a lane is row set a ^ (bq & 2)), so one Pk
+// load per row group (lane: row set bq) holds every set a block needs and
+// ds_swizzle hands each lane its set for fragment a (swz_quad); the R fragment
+// loads stay whole 128-B lines.  One box, alternating: the north star
+// -0.4...-0.8 % per pass, the 8-block share -1.4 % (profiles/r06/mf_sw_*.jsonl)
+template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -208,31 +208,20 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
     const int xc = cw0 + 32 * t + 2 * lo;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
-      const int rB = 16 * g + 4 * (SW ? a ^ (bq & 2) : a) + hi;
+      const int rB = 16 * g + 4 * (a ^ (bq & 2)) + hi;
       const double* row = (const double*)b0 + (int64_t)(rB < H ? rB : H - 1) * ws;
       cf[a] = ldg_nt((const d2*)(row + (xc < (RAG ? nci : ncc) ? xc : 0)));
     }
   };
   // column-part B operands of row group g of a panel (first row r0): P at its
   // rows; zero past H and, for the diagonal panel, in the diagonal-block waves
-  // (SW: bc[0] = this lane's row set bq, handed out by swz_quad)
-  auto load_bcol = [&](int r0, int H, bool zero, int g, double (*bc)[NG]) {
-    if constexpr (SW) {
-      const int rB = 16 * g + 4 * bq + hi;
-      double v[NG];
-      ld_prow(r0 + (rB < H ? rB : 0), v);
+  // -- this lane's row set bq, handed to the fragments by swz_quad
+  auto load_bcol = [&](int r0, int H, bool zero, int g, double* bc) {
+    const int rB = 16 * g + 4 * bq + hi;
+    double v[NG];
+    ld_prow(r0 + (rB < H ? rB : 0), v);
 #pragma unroll
-      for (int q = 0; q < NG; ++q) bc[0][q] = (rB < H && !zero) ? v[q] : 0.0;
-      return;
-    }
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int rB = 16 * g + 4 * a + hi;
-      double v[NG];
-      ld_prow(r0 + (rB < H ? rB : 0), v);
-#pragma unroll
-      for (int q = 0; q < NG; ++q) bc[a][q] = (rB < H && !zero) ? v[q] : 0.0;
-    }
+    for (int q = 0; q < NG; ++q) bc[q] = (rB < H && !zero) ? v[q] : 0.0;
   };
   auto pbase = [&](const SymItem& x) { return (uint64_t)(x.P + (x.c0 - x.r0)); };
   // a band panel's item narrower than the strip: its columns past nci (never
@@ -249,7 +238,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
   uint64_t curb = pbase(cur);
   // ring of PD steps in flight per wave
   d2 cfq[PD][4];
-  double bcn[4][NG];
+  double bcn[NG];
 #pragma unroll
   for (int p = 0; p < PD; ++p) load_cf(curb, cur.w, cur.H, cur.nc, 0, p, cfq[p]);
   load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
@@ -272,19 +261,12 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
       const int gr0 = same ? cur.r0 : nx.r0;
       const bool gz = dhalf && gr0 == c0;
       double bcol[4][NG];
-      if constexpr (SW) {
-        // fragment a's set a ^ (bq & 2) from the lane of quad a ^ (bq & 2) of
-        // this 16-lane row
+      // fragment a's set a ^ (bq & 2) from the lane of quad a ^ (bq & 2) of
+      // this 16-lane row
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < 4; ++a)
 #pragma unroll
-          for (int q = 0; q < NG; ++q) bcol[a][q] = swz_quad(bcn[0][q], a);
-      } else {
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-#pragma unroll
-          for (int q = 0; q < NG; ++q) bcol[a][q] = bcn[a][q];
-      }
+        for (int q = 0; q < NG; ++q) bcol[a][q] = swz_quad(bcn[q], a);
       double drow[4][NG];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -316,7 +298,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
         lds_order();                                   // previous step's tile reads issued
 #pragma unroll
         for (int a = 0; a < 4; ++a)
-          *(d2*)(sb + 32 * (4 * (SW ? a ^ (bq & 2) : a) + hi) + 2 * (lo ^ hi)) = cf[a];
+          *(d2*)(sb + 32 * (4 * (a ^ (bq & 2)) + hi) + 2 * (lo ^ hi)) = cf[a];
         lds_order();                                   // tile written
         // the row fragment reads go out right behind the writes (a wave's DS
         // operations execute in order); the column MFMAs cover their latency
@@ -518,27 +500,24 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
     const int xc = cw0 + 32 * t + 2 * lo;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
-      const int rB = 16 * g + 4 * a + hi;
+      const int rB = 16 * g + 4 * (a ^ (bq & 2)) + hi;   // k_sym_mfma's row sets
       const double* row = (const double*)b0 + (int64_t)(rB < H ? rB : H - 1) * ws;
       cf[a] = ldg_nt((const d2*)(row + (xc < ncc ? xc : 0)));
     }
   };
-  auto load_bcol = [&](int r0, int H, bool zero, int g, double (*bc)[NG]) {
+  auto load_bcol = [&](int r0, int H, bool zero, int g, double* bc) {
+    const int rB = 16 * g + 4 * bq + hi;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int rB = 16 * g + 4 * a + hi;
-#pragma unroll
-      for (int q = 0; q < NG; ++q) {
-        const double v = ldg(pkb + (int64_t)(r0 + (rB < H ? rB : 0)) * PKS + 4 * q + n4);
-        bc[a][q] = (rB < H && !zero) ? v : 0.0;
-      }
+    for (int q = 0; q < NG; ++q) {
+      const double v = ldg(pkb + (int64_t)(r0 + (rB < H ? rB : 0)) * PKS + 4 * q + n4);
+      bc[q] = (rB < H && !zero) ? v : 0.0;
     }
   };
   auto pbase = [&](const SymItem& x) { return (uint64_t)(x.P + (x.c0 - x.r0)); };
 
   uint64_t curb = pbase(cur);
   d2 cfq[PD][4];
-  double bcn[4][NG];
+  double bcn[NG];
 #pragma unroll
   for (int p = 0; p < PD; ++p) load_cf(curb, cur.w, cur.H, 0, p, cfq[p]);
   load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
@@ -569,7 +548,7 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int q = 0; q < NG; ++q) bcol[a][q] = bcn[a][q];
+        for (int q = 0; q < NG; ++q) bcol[a][q] = swz_quad(bcn[q], a);
       double drow[4][NG];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -603,7 +582,8 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
         d2* rf = rfs[t];
         lds_order();
 #pragma unroll
-        for (int a = 0; a < 4; ++a) *(d2*)(sb + 32 * (4 * a + hi) + 2 * (lo ^ hi)) = cf[a];
+        for (int a = 0; a < 4; ++a)
+          *(d2*)(sb + 32 * (4 * (a ^ (bq & 2)) + hi) + 2 * (lo ^ hi)) = cf[a];
         lds_order();
 #pragma unroll
         for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
@@ -1004,12 +984,6 @@ __global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpa
 // kernel (capi.hip build_strips; bitwise the same products) -- 1: 3-4 columns
 // only (at 5-8 the pair form runs ~14 % slower per byte and a short launch's
 // tail does not pay it back), 2 (forced, SGV_MF_PAIR=1): every column count
-// SGV_MF_SW=1 (A/B, with SGV_AB=1): the de-replicated column B operands (SW)
-static bool mf_swizzled() {
-  const char* e = ab_env("SGV_MF_SW");
-  return e && e[0] == '1';
-}
-
 template <int NG, bool PP = false>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
@@ -1021,9 +995,6 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
   else if (pair >= (NG == 1 ? 1 : 2))
     hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_swizzled())
-    hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP, true>), dim3(nstrips), dim3(256), 0,
-                       st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else
     hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP>), dim3(nstrips), dim3(256), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
