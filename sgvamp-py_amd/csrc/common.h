@@ -45,6 +45,28 @@ __device__ __forceinline__ double row_ror(double v) {
                                                 (unsigned)lo));
 }
 
+// the double of the lane of quad a ^ (bq & 2) in this lane's 16-lane row, bq =
+// lane bits 2-3: lane id ((l & ~4) | 4 (a & 1)) ^ 8 (a >> 1) (ds_swizzle bit
+// mask mode within 32 lanes: ((l & and) | or) ^ xor); a is a compile-time
+// constant after unrolling (the strip kernels and the band walk
+// take their column-part P operands this way: one load per row group)
+template <int A>
+__device__ __forceinline__ int swz_dw(int v) {
+  return __builtin_amdgcn_ds_swizzle(v, 0x1B | ((A & 1) << 7) | ((A >> 1) << 13));
+}
+__device__ __forceinline__ double swz_quad(double v, int a) {
+  const int2 w = __builtin_bit_cast(int2, v);
+  int2 r;
+  switch (a) {
+    case 0: r.x = swz_dw<0>(w.x); r.y = swz_dw<0>(w.y); break;
+    case 1: r.x = swz_dw<1>(w.x); r.y = swz_dw<1>(w.y); break;
+    case 2: r.x = swz_dw<2>(w.x); r.y = swz_dw<2>(w.y); break;
+    default: r.x = swz_dw<3>(w.x); r.y = swz_dw<3>(w.y); break;
+  }
+  return __builtin_bit_cast(double, r);
+}
+
+
 // One LD block of one LD matrix: n x n dense f64, row-major, row stride lda
 // (multiple of PADV, zero padded); voff = offset of the block's first marker
 // in the padded device vector layout.
