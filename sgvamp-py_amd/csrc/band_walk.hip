@@ -135,6 +135,10 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
     double* __restrict__ partials) {
   constexpr int RW = 4 * NG;                                   // accumulator row stride
   constexpr int CPT = RW / 2;                                  // epilogue columns per thread
+  // column-part P operands de-replicated over the MFMA blocks (as the strips):
+  // at 5-8 columns -2.8 % per pass; at 3-4 columns (8-B operands) +1.5 %, so
+  // not there (M = 1e6, bw = 1,000, one box: profiles/r06/walk_sw_ab.txt)
+  constexpr bool SWZ = NG == 2;
   __shared__ __attribute__((aligned(16))) double ring[WALK_RMAX][SYM_H * RW];
   __shared__ __attribute__((aligned(16))) double red[WK_RD][WK_NW][16 * RW];
   __shared__ int hready[WK_RD], hdone[WK_RD];   // writes into / combines of each buffer
@@ -181,7 +185,7 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
     const int xc = WK_WC * wid + 32 * t + 2 * lo;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
-      const int rB = 16 * g2 + 4 * (a ^ (bq & 2)) + hi;   // the strips' row sets
+      const int rB = 16 * g2 + 4 * (SWZ ? a ^ (bq & 2) : a) + hi;   // SWZ: the strips' row sets
       cf[a] = ldg_nt((const d2*)(u.b0 + (rB < u.H ? rB : u.H - 1) * u.w + (xc < u.nc ? xc : 0)));
     }
   };
@@ -207,13 +211,18 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
       for (int q = 0; q < NG; ++q) v[q] = ldg((const double*)(pb + 8 * (4 * q + n4)));
     }
   };
-  // the masks: bcol: row valid, not the diagonal block (this lane's row set bq,
-  // handed to the fragments by swz_quad: one load per row group); bit 2 t + e
-  // (brow: column inside the item)
-  auto load_bcol = [&](const Cur& u, int g2, double* bc) {
-    const int rB = 16 * g2 + 4 * bq + hi;
-    ld_p((u.r0 + rB) * pbyte, bc);
-    return (rB < u.H && !u.colz) ? 1 : 0;
+  // the masks: bit a (bcol: row valid, not the diagonal block; SWZ: bit 0 for
+  // this lane's row set bq, handed to the fragments by swz_quad -- one load per
+  // row group), bit 2 t + e (brow: column inside the item)
+  auto load_bcol = [&](const Cur& u, int g2, double (*bc)[NG]) {
+    int m = 0;
+#pragma unroll
+    for (int a = 0; a < (SWZ ? 1 : 4); ++a) {
+      const int rB = 16 * g2 + 4 * (SWZ ? bq : a) + hi;
+      m |= (rB < u.H && !u.colz) ? 1 << a : 0;
+      ld_p((u.r0 + rB) * pbyte, bc[a]);
+    }
+    return m;
   };
   // live = false (not the item's last row group: the next item's row operands
   // are not due yet) reads the range's last row instead -- the
@@ -244,7 +253,7 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
   SymPanel pn = panels[wk.p0];
   Cur cu = make(items[pn.item_begin], pn);
   d2 cfn[WK_NT][4];
-  double bcn[NG], brn[WK_NT][2][NG];
+  double bcn[SWZ ? 1 : 4][NG], brn[WK_NT][2][NG];
 #pragma unroll
   for (int t = 0; t < WK_NT; ++t) load_cf(cu, 0, t, cfn[t]);
   int bcm = load_bcol(cu, 0, bcn);
@@ -289,7 +298,8 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
-          for (int q = 0; q < NG; ++q) bcol[a][q] = swz_quad(bcm ? bcn[q] : 0.0, a);
+          for (int q = 0; q < NG; ++q)
+            bcol[a][q] = SWZ ? swz_quad(bcm ? bcn[0][q] : 0.0, a) : (bcm >> a & 1) ? bcn[SWZ ? 0 : a][q] : 0.0;
         // where the next row group's loads come from: this item's next, or the
         // next item's first (then also its row operands).  Branch-free, the same
         // loads on every path (a branch join with different load counts makes
@@ -330,7 +340,7 @@ __global__ __launch_bounds__(WK_NW * 64, 1) void k_band_walk(
             wk_lds_order();
 #pragma unroll
             for (int a = 0; a < 4; ++a)
-              *(d2*)(sb + 32 * (4 * (a ^ (bq & 2)) + hi) + 2 * (lo ^ hi)) = cf[a];
+              *(d2*)(sb + 32 * (4 * (SWZ ? a ^ (bq & 2) : a) + hi) + 2 * (lo ^ hi)) = cf[a];
             wk_lds_order();
 #pragma unroll
             for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));

@@ -95,13 +95,14 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // PP (NG = 2): Pk in k_pack's PAIRED layout, so a lane's two column groups
 // (columns n4 and 4 + n4) of one Pk row are one 16-B load: half the P-operand
 // load instructions through the texture-address unit per row group
-// Column-part B operands without the 4x replication over the MFMA blocks:
-// blocks 0-1 take a row group's 4-row sets in the order 0 1 2 3, blocks 2-3 in
-// the order 2 3 0 1 (fragment a of a lane is row set a ^ (bq & 2)), so one Pk
-// load per row group (lane: row set bq) holds every set a block needs and
-// ds_swizzle hands each lane its set for fragment a (swz_quad); the R fragment
-// loads stay whole 128-B lines.  One box, alternating: the north star
-// -0.4...-0.8 % per pass, the 8-block share -1.4 % (profiles/r06/mf_sw_*.jsonl)
+// SWZ (NG = 2): column-part B operands without the 4x replication over the
+// MFMA blocks: blocks 0-1 take a row group's 4-row sets in the order 0 1 2 3,
+// blocks 2-3 in the order 2 3 0 1 (fragment a of a lane is row set a ^ (bq &
+// 2)), so one Pk load per row group (lane: row set bq) holds every set a block
+// needs and ds_swizzle hands each lane its set for fragment a (swz_quad); the
+// R fragment loads stay whole 128-B lines.  One box, alternating: the north
+// star -0.4...-0.8 % per pass, the 8-block share -1.4 %; at NG = 1 (8-B
+// operands) even to +0.4 %, so not there (profiles/r06/mf_sw_*.jsonl)
 template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
@@ -114,6 +115,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
   constexpr int NT = WC / 32;      // 32-column steps per wave
   static_assert(PD >= 1 && PD <= NT && NT % PD == 0, "prefetch depth divides the steps");
   constexpr int RW = 4 * NG;       // row-sum stride of wrow
+  constexpr bool SWZ = NG == 2;
   __shared__ __attribute__((aligned(16))) double rowbuf[NW * SYM_H * RW];   // wrow
   // the per-wave transpose tile: 16 rows x 32 columns, 16-B piece (row r, pair
   // p) at slot 16 r + (p ^ (r & 3)) -- unpadded (4 KiB, so the 64 KiB of row
@@ -188,20 +190,23 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
     const int xc = cw0 + 32 * t + 2 * lo;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
-      const int rB = 16 * g + 4 * (a ^ (bq & 2)) + hi;
+      const int rB = 16 * g + 4 * (SWZ ? a ^ (bq & 2) : a) + hi;
       const double* row = (const double*)b0 + (int64_t)(rB < H ? rB : H - 1) * ws;
       cf[a] = ldg_nt((const d2*)(row + (xc < (RAG ? nci : ncc) ? xc : 0)));
     }
   };
   // column-part B operands of row group g of a panel (first row r0): P at its
   // rows; zero past H and, for the diagonal panel, in the diagonal-block waves
-  // -- this lane's row set bq, handed to the fragments by swz_quad
-  auto load_bcol = [&](int r0, int H, bool zero, int g, double* bc) {
-    const int rB = 16 * g + 4 * bq + hi;
-    double v[NG];
-    ld_prow(r0 + (rB < H ? rB : 0), v);
+  // (SWZ: bc[0] = this lane's row set bq, handed to the fragments by swz_quad)
+  auto load_bcol = [&](int r0, int H, bool zero, int g, double (*bc)[NG]) {
 #pragma unroll
-    for (int q = 0; q < NG; ++q) bc[q] = (rB < H && !zero) ? v[q] : 0.0;
+    for (int a = 0; a < (SWZ ? 1 : 4); ++a) {
+      const int rB = 16 * g + 4 * (SWZ ? bq : a) + hi;
+      double v[NG];
+      ld_prow(r0 + (rB < H ? rB : 0), v);
+#pragma unroll
+      for (int q = 0; q < NG; ++q) bc[a][q] = (rB < H && !zero) ? v[q] : 0.0;
+    }
   };
   auto pbase = [&](const SymItem& x) { return (uint64_t)(x.P + (x.c0 - x.r0)); };
   // a band panel's item narrower than the strip: its columns past nci (never
@@ -218,7 +223,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
   uint64_t curb = pbase(cur);
   // ring of PD steps in flight per wave
   d2 cfq[PD][4];
-  double bcn[NG];
+  double bcn[SWZ ? 1 : 4][NG];
 #pragma unroll
   for (int p = 0; p < PD; ++p) load_cf(curb, cur.w, cur.H, cur.nc, 0, p, cfq[p]);
   load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
@@ -246,7 +251,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int q = 0; q < NG; ++q) bcol[a][q] = swz_quad(bcn[q], a);
+        for (int q = 0; q < NG; ++q) bcol[a][q] = SWZ ? swz_quad(bcn[0][q], a) : bcn[SWZ ? 0 : a][q];
       double drow[4][NG];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
         lds_order();                                   // previous step's tile reads issued
 #pragma unroll
         for (int a = 0; a < 4; ++a)
-          *(d2*)(sb + 32 * (4 * (a ^ (bq & 2)) + hi) + 2 * (lo ^ hi)) = cf[a];
+          *(d2*)(sb + 32 * (4 * (SWZ ? a ^ (bq & 2) : a) + hi) + 2 * (lo ^ hi)) = cf[a];
         lds_order();                                   // tile written
         // the row fragment reads go out right behind the writes (a wave's DS
         // operations execute in order); the column MFMAs cover their latency
@@ -431,6 +436,7 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
   constexpr int NT = WC / 32;      // 32-column steps per wave
   static_assert(PD >= 1 && PD <= NT && NT % PD == 0, "prefetch depth divides the steps");
   constexpr int RW = 4 * NG;
+  constexpr bool SWZ = NG == 2;   // k_sym_mfma's row sets
   __shared__ __attribute__((aligned(16))) double wrow[4 * SYM_H * RW];   // [segment][row][4 NG]
   constexpr int HS = 3;                                                    // hand-off slots
   __shared__ __attribute__((aligned(16))) double hand[HS][4][4 * NG][WAVE];   // [gg % HS][segment][r, q][lane]
@@ -480,24 +486,27 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
     const int xc = cw0 + 32 * t + 2 * lo;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
-      const int rB = 16 * g + 4 * (a ^ (bq & 2)) + hi;   // k_sym_mfma's row sets
+      const int rB = 16 * g + 4 * (SWZ ? a ^ (bq & 2) : a) + hi;
       const double* row = (const double*)b0 + (int64_t)(rB < H ? rB : H - 1) * ws;
       cf[a] = ldg_nt((const d2*)(row + (xc < ncc ? xc : 0)));
     }
   };
-  auto load_bcol = [&](int r0, int H, bool zero, int g, double* bc) {
-    const int rB = 16 * g + 4 * bq + hi;
+  auto load_bcol = [&](int r0, int H, bool zero, int g, double (*bc)[NG]) {
 #pragma unroll
-    for (int q = 0; q < NG; ++q) {
-      const double v = ldg(pkb + (int64_t)(r0 + (rB < H ? rB : 0)) * PKS + 4 * q + n4);
-      bc[q] = (rB < H && !zero) ? v : 0.0;
+    for (int a = 0; a < (SWZ ? 1 : 4); ++a) {
+      const int rB = 16 * g + 4 * (SWZ ? bq : a) + hi;
+#pragma unroll
+      for (int q = 0; q < NG; ++q) {
+        const double v = ldg(pkb + (int64_t)(r0 + (rB < H ? rB : 0)) * PKS + 4 * q + n4);
+        bc[a][q] = (rB < H && !zero) ? v : 0.0;
+      }
     }
   };
   auto pbase = [&](const SymItem& x) { return (uint64_t)(x.P + (x.c0 - x.r0)); };
 
   uint64_t curb = pbase(cur);
   d2 cfq[PD][4];
-  double bcn[NG];
+  double bcn[SWZ ? 1 : 4][NG];
 #pragma unroll
   for (int p = 0; p < PD; ++p) load_cf(curb, cur.w, cur.H, 0, p, cfq[p]);
   load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
@@ -528,7 +537,7 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
-        for (int q = 0; q < NG; ++q) bcol[a][q] = swz_quad(bcn[q], a);
+        for (int q = 0; q < NG; ++q) bcol[a][q] = SWZ ? swz_quad(bcn[0][q], a) : bcn[SWZ ? 0 : a][q];
       double drow[4][NG];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
@@ -563,7 +572,7 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
         lds_order();
 #pragma unroll
         for (int a = 0; a < 4; ++a)
-          *(d2*)(sb + 32 * (4 * (a ^ (bq & 2)) + hi) + 2 * (lo ^ hi)) = cf[a];
+          *(d2*)(sb + 32 * (4 * (SWZ ? a ^ (bq & 2) : a) + hi) + 2 * (lo ^ hi)) = cf[a];
         lds_order();
 #pragma unroll
         for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
