@@ -103,7 +103,7 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // R fragment loads stay whole 128-B lines.  One box, alternating: the north
 // star -0.4...-0.8 % per pass, the 8-block share -1.4 %; at NG = 1 (8-B
 // operands) even to +0.4 %, so not there (profiles/r06/mf_sw_*.jsonl)
-template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false, int LP = -1>
+template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -188,17 +188,6 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
   auto load_cf = [&](uint64_t b0, int64_t ws, int H, int nci, int g, int t, d2* cf) {
     asm volatile("" : "+s"(b0));
     const int xc = cw0 + 32 * t + 2 * lo;
-    if constexpr (LP >= 0) {
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc((void*)b0, (short)0, 0x7FFFFFFF, 0x00020000);
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const int rB = 16 * g + 4 * (SWZ ? a ^ (bq & 2) : a) + hi;
-        const int off = 8 * ((rB < H ? rB : H - 1) * (int)ws + (xc < (RAG ? nci : ncc) ? xc : 0));
-        cf[a] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, LP));
-      }
-      return;
-    }
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       const int rB = 16 * g + 4 * (SWZ ? a ^ (bq & 2) : a) + hi;
@@ -984,13 +973,6 @@ __global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpa
 // kernel (capi.hip build_strips; bitwise the same products) -- 1: 3-4 columns
 // only (at 5-8 the pair form runs ~14 % slower per byte and a short launch's
 // tail does not pay it back), 2 (forced, SGV_MF_PAIR=1): every column count
-// SGV_MF_LP (A/B, with SGV_AB=1): the R fragments by buffer loads with cache
-// policy bits (2 nt, 18 nt sc1, 19 sc0 nt sc1, 3 sc0 nt); unset: global nt loads
-static int mf_lp() {
-  const char* e = ab_env("SGV_MF_LP");
-  return e ? atoi(e) : -1;
-}
-
 template <int NG, bool PP = false>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
@@ -1002,18 +984,6 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
   else if (pair >= (NG == 1 ? 1 : 2))
     hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_lp() == 2)
-    hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP, 2>), dim3(nstrips), dim3(256), 0, st,
-                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_lp() == 18)
-    hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP, 18>), dim3(nstrips), dim3(256), 0, st,
-                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_lp() == 19)
-    hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP, 19>), dim3(nstrips), dim3(256), 0, st,
-                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_lp() == 3)
-    hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP, 3>), dim3(nstrips), dim3(256), 0, st,
-                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else
     hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP>), dim3(nstrips), dim3(256), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
