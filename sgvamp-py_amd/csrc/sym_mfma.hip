@@ -103,7 +103,7 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // R fragment loads stay whole 128-B lines.  One box, alternating: the north
 // star -0.4...-0.8 % per pass, the 8-block share -1.4 %; at NG = 1 (8-B
 // operands) even to +0.4 %, so not there (profiles/r06/mf_sw_*.jsonl)
-template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false, int ABL = 0>
+template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -123,11 +123,6 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
   // a write's 16-lane quarter covers one row, a row-fragment read's quarter
   // (rows 4q + (l & 3), pairs 4((l >> 2) & 3) + (l >> 4)) 16 distinct slots mod 16
   __shared__ __attribute__((aligned(16))) double stg[NW][16 * 32];
-  // ablation 1: each MFMA replaced by one f64 add (operands kept alive)
-  auto MFK = [](double x, double y, double c) {
-    if constexpr (ABL & 1) return c + x;
-    else return MFMA4(x, y, c);
-  };
   const SymStrip sp = strips[blockIdx.x];
   if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
   MF_TRACE_BEGIN
@@ -285,10 +280,6 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
         }
         if (t >= ntp) continue;                        // wave-uniform: past the chunk / item
         if (RAG && cur.nc < ncc) band_zero(cur.nc, t, cf);   // uniform: a band item's stored end
-        if constexpr (ABL & 2) {   // ablation: no LDS transpose
-#pragma unroll
-          for (int r = 0; r < 4; ++r) rf[r] = d2{brow[t][0][0], brow[t][1][NG - 1]};
-        } else {
         lds_order();                                   // previous step's tile reads issued
 #pragma unroll
         for (int a = 0; a < 4; ++a)
@@ -298,8 +289,6 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
         // operations execute in order); the column MFMAs cover their latency
 #pragma unroll
         for (int r = 0; r < 4; ++r) rf[r] = *(const d2*)(sb + 32 * (4 * r + n4) + 2 * (pc ^ n4));
-        }
-
         // the MFMA burst at raised wave priority: the SIMD's other wave, whose
         // loads are in flight, takes the issue slots back when this one drains
         // (NC = 4/8 0.7-1.5 % faster per pass on two boxes; NC = 16 1 % slower,
@@ -311,11 +300,11 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
 #pragma unroll
           for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int q = 0; q < NG; ++q) drow[r][q] = MFK(f[r].x, brow[tt][0][q], drow[r][q]);
+            for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(f[r].x, brow[tt][0][q], drow[r][q]);
 #pragma unroll
           for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int q = 0; q < NG; ++q) drow[r][q] = MFK(f[r].y, brow[tt][1][q], drow[r][q]);
+            for (int q = 0; q < NG; ++q) drow[r][q] = MFMA4(f[r].y, brow[tt][1][q], drow[r][q]);
         };
         if constexpr (DEF) {
           // column level a of this step, then a quarter of the previous step's
@@ -326,8 +315,8 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
             if (!colz) {
 #pragma unroll
               for (int q = 0; q < NG; ++q) {
-                dcol[t][0][q] = MFK(cf[a].x, bcol[a][q], dcol[t][0][q]);
-                dcol[t][1][q] = MFK(cf[a].y, bcol[a][q], dcol[t][1][q]);
+                dcol[t][0][q] = MFMA4(cf[a].x, bcol[a][q], dcol[t][0][q]);
+                dcol[t][1][q] = MFMA4(cf[a].y, bcol[a][q], dcol[t][1][q]);
               }
             }
             if (t > 0) {
@@ -336,7 +325,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
               for (int r = 2 * (a & 1); r < 2 * (a & 1) + 2; ++r)
 #pragma unroll
                 for (int q = 0; q < NG; ++q)
-                  drow[r][q] = MFK(a < 2 ? rp[r].x : rp[r].y, brow[tp][a < 2 ? 0 : 1][q], drow[r][q]);
+                  drow[r][q] = MFMA4(a < 2 ? rp[r].x : rp[r].y, brow[tp][a < 2 ? 0 : 1][q], drow[r][q]);
             }
           }
           // the row group's last active step: its own row MFMAs now
@@ -347,8 +336,8 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
             for (int a = 0; a < 4; ++a)
 #pragma unroll
               for (int q = 0; q < NG; ++q) {
-                dcol[t][0][q] = MFK(cf[a].x, bcol[a][q], dcol[t][0][q]);
-                dcol[t][1][q] = MFK(cf[a].y, bcol[a][q], dcol[t][1][q]);
+                dcol[t][0][q] = MFMA4(cf[a].x, bcol[a][q], dcol[t][0][q]);
+                dcol[t][1][q] = MFMA4(cf[a].y, bcol[a][q], dcol[t][1][q]);
               }
           }
           row_mfma(rf, t);
@@ -984,13 +973,6 @@ __global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpa
 // kernel (capi.hip build_strips; bitwise the same products) -- 1: 3-4 columns
 // only (at 5-8 the pair form runs ~14 % slower per byte and a short launch's
 // tail does not pay it back), 2 (forced, SGV_MF_PAIR=1): every column count
-// SGV_MF_ABL (A/B, with SGV_AB=1): timing ablations, WRONG products -- 1 no
-// MFMA, 2 no LDS transpose, 3 neither (the loads and their waits only)
-static int mf_abl() {
-  const char* e = ab_env("SGV_MF_ABL");
-  return e ? atoi(e) : 0;
-}
-
 template <int NG, bool PP = false>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
@@ -1002,15 +984,6 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
   else if (pair >= (NG == 1 ? 1 : 2))
     hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_abl() == 1)
-    hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP, 1>), dim3(nstrips), dim3(256), 0, st,
-                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_abl() == 2)
-    hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP, 2>), dim3(nstrips), dim3(256), 0, st,
-                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_abl() == 3)
-    hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP, 3>), dim3(nstrips), dim3(256), 0, st,
-                       d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else
     hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP>), dim3(nstrips), dim3(256), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
