@@ -811,7 +811,7 @@ def _band_matrix(parts, seed=0):
 
 @pytest.mark.parametrize("parts", [[(5000, 300)], [(2100, 100), (700, None), (3000, 1000)],
                                    [(1030, 5), (4000, 40)], [(4000, 1200)], [(3000, 0), (2050, 1)]])
-@pytest.mark.parametrize("ncol", [1, 2, 3, 8, 13, 16])
+@pytest.mark.parametrize("ncol", [1, 2, 3, 5, 8, 13, 16])
 @pytest.mark.parametrize("s", [0.0, 0.1])
 @pytest.mark.parametrize("kern", ["packed", "packed_valu"])
 def test_ld_matvec_band_vs_scipy(parts, ncol, s, kern):
