@@ -668,7 +668,9 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
 //   16x16x4 f64 C/D layout (cdna_hip_programming.md): D[(l>>4) + 4r][l & 15].
 typedef double d4 __attribute__((ext_vector_type(4)));
 #define MFMA16(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
-template <int PD, bool RAG = false>
+// BL: the row-part B operands of steps 2-3 kept in LDS (16 doubles per lane, 8
+// KiB per wave, read back per step as 4 x 16 B) instead of registers
+template <int PD, bool RAG = false, bool BL = false>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -680,6 +682,8 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
   constexpr int MF_NT = MF_WC / 32;
   __shared__ double red[2][4][256];
   __shared__ __attribute__((aligned(16))) double stg[4][16 * LDP];
+  constexpr int TB = BL ? 2 : 0;                       // steps whose B operands live in LDS
+  __shared__ __attribute__((aligned(16))) double bls[BL ? 4 : 1][TB * 8 / 2][WAVE][2];
   const SymStrip sp = strips[blockIdx.x];
   if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
   const int lane = threadIdx.x & (WAVE - 1);
@@ -694,7 +698,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
 
   double* sb = stg[wid];
   // row-part B operands (P at this wave's columns), reused by every row group
-  double brow[MF_NT][4][2];
+  double brow[MF_NT - TB][4][2];
 #pragma unroll
   for (int t = 0; t < MF_NT; ++t)
 #pragma unroll
@@ -703,7 +707,8 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
       for (int e = 0; e < 2; ++e) {
         const int col = cw0 + 32 * t + 8 * s + 2 * hi + e;
         const double v = ldg(pkb + (int64_t)(c0 + (col < ncc ? col : 0)) * 16 + lo);
-        brow[t][s][e] = col < ncc ? v : 0.0;
+        if (t < MF_NT - TB) brow[t < MF_NT - TB ? t : 0][s][e] = col < ncc ? v : 0.0;
+        else if constexpr (BL) bls[wid][(t - (MF_NT - TB)) * 4 + s][lane][e] = col < ncc ? v : 0.0;
       }
   d4 dcol[MF_NT][2];
 #pragma unroll
@@ -789,6 +794,12 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
         lds_order();                                   // tile written
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) rf[s2] = *(const d2*)(sb + lo * LDP + 8 * s2 + 2 * hi);
+        d2 bt[4];   // this step's row-part B operands
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+          if (t < MF_NT - TB) bt[s2] = d2{brow[t < MF_NT - TB ? t : 0][s2][0], brow[t < MF_NT - TB ? t : 0][s2][1]};
+          else if constexpr (BL) bt[s2] = *(const d2*)&bls[wid][(t - (MF_NT - TB)) * 4 + s2][lane][0];
+        }
         if (!colz) {
 #pragma unroll
           for (int a = 0; a < 4; ++a) {
@@ -798,8 +809,8 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
         }
 #pragma unroll
         for (int s2 = 0; s2 < 4; ++s2) {
-          drow0 = MFMA16(rf[s2].x, brow[t][s2][0], drow0);
-          drow1 = MFMA16(rf[s2].y, brow[t][s2][1], drow1);
+          drow0 = MFMA16(rf[s2].x, bt[s2].x, drow0);
+          drow1 = MFMA16(rf[s2].y, bt[s2].y, drow1);
         }
       }
       // row sums of this 16-row group: waves 0..3 in order
@@ -1040,14 +1051,23 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
         launch_mf<2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged,
                      pair, st);
       break;
-    default:
-      if (ragged)
+    default: {
+      const char* e = ab_env("SGV_MF16_BL");
+      const bool bl = e && e[0] == '1';
+      if (ragged && bl)
+        hipLaunchKernelGGL((k_sym_mfma16<2, true, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
+                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
+      else if (ragged)
         hipLaunchKernelGGL((k_sym_mfma16<2, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
+                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
+      else if (bl)
+        hipLaunchKernelGGL((k_sym_mfma16<2, false, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
                            d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       else
         hipLaunchKernelGGL((k_sym_mfma16<2>), dim3(nstrips), dim3(256), 0, st, d_strips,
                            d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       break;
+    }
   }
   return hipGetLastError();
 }
