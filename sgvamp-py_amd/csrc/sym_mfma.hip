@@ -1051,23 +1051,18 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
         launch_mf<2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged,
                      pair, st);
       break;
-    default: {
-      const char* e = ab_env("SGV_MF16_BL");
-      const bool bl = e && e[0] == '1';
-      if (ragged && bl)
+    default:
+      // band plans keep steps 2-3's row operands in LDS (BL: 0 spills instead of
+      // 7; -0.6 % per 16-column band pass); dense plans do not (+2 % at 64 x
+      // 15,625, C5 +1.5 %: profiles/r06/mf16_bl_*.jsonl) and spill 3 VGPRs
+      // outside the row-group loop
+      if (ragged)
         hipLaunchKernelGGL((k_sym_mfma16<2, true, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-      else if (ragged)
-        hipLaunchKernelGGL((k_sym_mfma16<2, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-      else if (bl)
-        hipLaunchKernelGGL((k_sym_mfma16<2, false, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
                            d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       else
         hipLaunchKernelGGL((k_sym_mfma16<2>), dim3(nstrips), dim3(256), 0, st, d_strips,
                            d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       break;
-    }
   }
   return hipGetLastError();
 }
