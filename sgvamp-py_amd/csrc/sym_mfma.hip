@@ -668,9 +668,9 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
 //   16x16x4 f64 C/D layout (cdna_hip_programming.md): D[(l>>4) + 4r][l & 15].
 typedef double d4 __attribute__((ext_vector_type(4)));
 #define MFMA16(a, b, c) __builtin_amdgcn_mfma_f64_16x16x4f64((a), (b), (c), 0, 0, 0)
-// BL: the row-part B operands of steps 2-3 kept in LDS (16 doubles per lane, 8
-// KiB per wave, read back per step as 4 x 16 B) instead of registers
-template <int PD, bool RAG = false, bool BL = false>
+// TB: the row-part B operands of the last TB steps kept in LDS (8 TB doubles per
+// lane, 4 TB KiB per wave, read back per step as 4 x 16 B) instead of registers
+template <int PD, bool RAG = false, int TB = 0>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -682,8 +682,8 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma16(const SymStrip* __restric
   constexpr int MF_NT = MF_WC / 32;
   __shared__ double red[2][4][256];
   __shared__ __attribute__((aligned(16))) double stg[4][16 * LDP];
-  constexpr int TB = BL ? 2 : 0;                       // steps whose B operands live in LDS
-  __shared__ __attribute__((aligned(16))) double bls[BL ? 4 : 1][TB * 8 / 2][WAVE][2];
+  constexpr bool BL = TB > 0;
+  __shared__ __attribute__((aligned(16))) double bls[BL ? 4 : 1][BL ? TB * 4 : 1][WAVE][2];
   const SymStrip sp = strips[blockIdx.x];
   if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
   const int lane = threadIdx.x & (WAVE - 1);
@@ -1057,7 +1057,10 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
       // 15,625, C5 +1.5 %: profiles/r06/mf16_bl_*.jsonl) and spill 3 VGPRs
       // outside the row-group loop
       if (ragged)
-        hipLaunchKernelGGL((k_sym_mfma16<2, true, true>), dim3(nstrips), dim3(256), 0, st, d_strips,
+        hipLaunchKernelGGL((k_sym_mfma16<2, true, 2>), dim3(nstrips), dim3(256), 0, st, d_strips,
+                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
+      else if (ab_env("SGV_MF16_TB") && ab_env("SGV_MF16_TB")[0] == '1')
+        hipLaunchKernelGGL((k_sym_mfma16<2, false, 1>), dim3(nstrips), dim3(256), 0, st, d_strips,
                            d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       else
         hipLaunchKernelGGL((k_sym_mfma16<2>), dim3(nstrips), dim3(256), 0, st, d_strips,
