@@ -1033,14 +1033,16 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
   // workgroup re-reading the same R with the default cache policy (+33 %,
   // profiles/r03/s4/mf_sets_ab.jsonl) and three / four 4x4x4 groups at one wave
   // per SIMD with the deferred row MFMAs (+13 % / +28 %, ng4_ab.jsonl):
-  // measured in DESIGN.md.  Prefetch depth 2 (3 / 7 VGPRs spilled on dense /
-  // band plans, still faster: profiles/r03/s4/mf16_pd_ab.jsonl,
-  // profiles/r04/band2_ab.jsonl).  Round 6 measured the spill-free forms on one
+  // measured in DESIGN.md.  Prefetch depth 2 (with every row operand in
+  // registers it spilled 3 / 7 VGPRs on dense / band plans and was still faster
+  // than depth 1: profiles/r03/s4/mf16_pd_ab.jsonl, profiles/r04/band2_ab.jsonl).
+  // Round 6 measured the spill-free forms on one
   // box (profiles/r06/mf16_forms_ab.jsonl, _bench_c5conv.jsonl): depth 1 (236
   // VGPRs) +1.5-2 % per pass, 8 waves of 64 columns per workgroup (188 VGPRs)
   // +8 %, and the row part on 4x4x4 MFMA in that form (210 VGPRs) +18 % -- the
-  // spills sit outside the row-group loop; the 8-wave row-sum combine and the
-  // 4x4x4 form's DPP reductions and 4x the MFMA issues cost more than they save.
+  // 8-wave row-sum combine and the 4x4x4 form's DPP reductions and 4x the MFMA
+  // issues cost more than they save; the spill-free form kept is the row
+  // operands of the last step(s) in LDS (below).
   switch ((nc + 3) / 4) {
     case 1: launch_mf<1>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
     case 2:
@@ -1052,18 +1054,15 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
                      pair, st);
       break;
     default:
-      // band plans keep steps 2-3's row operands in LDS (BL: 0 spills instead of
-      // 7; -0.6 % per 16-column band pass); dense plans do not (+2 % at 64 x
-      // 15,625, C5 +1.5 %: profiles/r06/mf16_bl_*.jsonl) and spill 3 VGPRs
-      // outside the row-group loop
+      // the row operands of the last steps in LDS, so nothing spills (256 VGPRs
+      // with 3 / 7 spilled before): band plans the last 2 steps (-0.6 % per
+      // 16-column band pass), dense plans the last one (even; 2 steps there +2 %)
+      // -- profiles/r06/mf16_bl_*.jsonl, mf16_tb_*.jsonl; products bitwise equal
       if (ragged)
         hipLaunchKernelGGL((k_sym_mfma16<2, true, 2>), dim3(nstrips), dim3(256), 0, st, d_strips,
                            d_sitems, d_pk, nc, rowpart, colpart, pa.run);
-      else if (ab_env("SGV_MF16_TB") && ab_env("SGV_MF16_TB")[0] == '1')
-        hipLaunchKernelGGL((k_sym_mfma16<2, false, 1>), dim3(nstrips), dim3(256), 0, st, d_strips,
-                           d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       else
-        hipLaunchKernelGGL((k_sym_mfma16<2>), dim3(nstrips), dim3(256), 0, st, d_strips,
+        hipLaunchKernelGGL((k_sym_mfma16<2, false, 1>), dim3(nstrips), dim3(256), 0, st, d_strips,
                            d_sitems, d_pk, nc, rowpart, colpart, pa.run);
       break;
   }
