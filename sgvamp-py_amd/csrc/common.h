@@ -372,11 +372,11 @@ hipError_t launch_sym_pass(int nc, int cls, const SymItem* d_items, int nitems,
                            const PassArgs& pa, double* rowpart, double* colpart, hipStream_t st);
 // MFMA pass (sym_mfma.hip): launch_pk interleaves the columns into Pk, then
 // launch_sym_mfma runs strips d_strips[0 .. nstrips) (one block group or all)
-// paired: the 5-8-column passes' Pk layout (band walks; strips unless the
-// plan runs the wave-pair kernel: strip_pk_paired)
+// paired: the 5-8-column passes' Pk layout (band walks and strips:
+// strip_pk_paired)
 hipError_t launch_pk(const PassArgs& pa, int nc, int64_t mpad, double* d_pk, hipStream_t st,
                      bool paired = false);
-bool strip_pk_paired(int nc, int pair);
+bool strip_pk_paired(int nc);
 hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                            const PassArgs& pa, const double* d_pk, double* rowpart,
                            double* colpart, bool ragged, int pair, hipStream_t st);

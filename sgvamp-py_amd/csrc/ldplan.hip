@@ -154,10 +154,11 @@ static double lpt_efficiency(std::vector<double> cost, int slots) {
 // NC <= 8 MFMA passes: the 4-wave kernel (two 4-wave workgroups per CU, 512
 // slots) or the wave-pair kernel (one 8-wave workgroup per CU, a strip in half
 // the time: 256 slots at half the cost) -- bitwise the same products, so the
-// choice is free per plan.  Auto (1): the pair kernel for 3-4-column passes
-// when its launch drains with at least 3 % less tail by the strips' model cost
-// (a few strips per slot: an 8-block share of the north star); SGV_MF_PAIR=0 / 1
-// (with SGV_AB=1) forces none / every 3-8-column pass (2).
+// choice is free per plan.  Auto (1): the pair kernel for the plan's 3-8-column
+// passes when its launch drains with at least 3 % less tail by the strips'
+// model cost (a few strips per slot: an 8-block share of the north star, 0.924
+// against 0.986 of a perfect split; 16 blocks and 8 x 25,000 stay on the 4-wave
+// kernel); SGV_MF_PAIR=0 / 1 (with SGV_AB=1) forces none / every pass (2).
 static int mfma_pair_choice(const std::vector<SymStrip>& strips,
                             const std::vector<SymItem>& sitems) {
   const char* e = ab_env("SGV_MF_PAIR");
@@ -664,7 +665,7 @@ int ld_pass(sgv_ctx* c, int ld, int nc, const PassArgs& pa_in){
     if (mf) {
       const bool walk = pl.nwalks && nc <= band_walk_max_nc();
       HIPCHK(launch_pk(pa, nc, c->Mpad, c->d_pk, c->st,
-                       walk ? nc > 4 : strip_pk_paired(nc, pl.pair)));
+                       walk ? nc > 4 : strip_pk_paired(nc)));
       if (walk) {   // band plan: the walks, then the head panels
         HIPCHK(launch_band_walk(nc, pl.d_walks, pl.nwalks, pl.d_wpanels, pl.d_witems, c->d_pk,
                                 c->Mpad, pa,

@@ -424,7 +424,7 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
 // ahead, a ring of HS hand-off slots), barriers only at panel ends.  The other
 // forms measured -- pair on two SIMDs, a barrier per row group -- were slower
 // 
-template <int NG, int PD>
+template <int NG, int PD, bool PP = false>
 __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __restrict__ strips,
                                                           const SymItem* __restrict__ sitems,
                                                           const double* __restrict__ pk, int ncol,
@@ -461,17 +461,27 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
   const int nta = min(NT, max(0, nta_seg - NT * h));
   double* sb = stg[wid];
 
+  static_assert(!PP || NG == 2, "paired Pk rows: two column groups");
+  auto ld_prow = [&](int64_t row, double* v) {   // as k_sym_mfma's
+    if constexpr (PP) {
+      const d2 x = ldg((const d2*)(pkb + row * PKS + 2 * n4));
+      v[0] = x.x;
+      v[1] = x.y;
+    } else {
+#pragma unroll
+      for (int q = 0; q < NG; ++q) v[q] = ldg(pkb + row * PKS + 4 * q + n4);
+    }
+  };
   double brow[NT][2][NG];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int col = cw0 + 32 * t + 2 * pc + e;
+      double v[NG];
+      ld_prow(c0 + (col < ncc ? col : 0), v);
 #pragma unroll
-      for (int q = 0; q < NG; ++q) {
-        const double v = ldg(pkb + (int64_t)(c0 + (col < ncc ? col : 0)) * PKS + 4 * q + n4);
-        brow[t][e][q] = col < ncc ? v : 0.0;
-      }
+      for (int q = 0; q < NG; ++q) brow[t][e][q] = col < ncc ? v[q] : 0.0;
     }
   double dcol[NT][2][NG];
 #pragma unroll
@@ -495,11 +505,10 @@ __global__ __launch_bounds__(512, 1) void k_sym_mfma_pair(const SymStrip* __rest
 #pragma unroll
     for (int a = 0; a < (SWZ ? 1 : 4); ++a) {
       const int rB = 16 * g + 4 * (SWZ ? bq : a) + hi;
+      double v[NG];
+      ld_prow(r0 + (rB < H ? rB : 0), v);
 #pragma unroll
-      for (int q = 0; q < NG; ++q) {
-        const double v = ldg(pkb + (int64_t)(r0 + (rB < H ? rB : 0)) * PKS + 4 * q + n4);
-        bc[a][q] = (rB < H && !zero) ? v : 0.0;
-      }
+      for (int q = 0; q < NG; ++q) bc[a][q] = (rB < H && !zero) ? v[q] : 0.0;
     }
   };
   auto pbase = [&](const SymItem& x) { return (uint64_t)(x.P + (x.c0 - x.r0)); };
@@ -981,9 +990,12 @@ __global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpa
 // ragged: some strip item stops short of its strip's widest (band blocks):
 // the RAG kernels, without the deferred row MFMAs (even there,
 // profiles/r04/band2_ab.jsonl).  pair: the plan's choice of the wave-pair
-// kernel (capi.hip build_strips; bitwise the same products) -- 1: 3-4 columns
-// only (at 5-8 the pair form runs ~14 % slower per byte and a short launch's
-// tail does not pay it back), 2 (forced, SGV_MF_PAIR=1): every column count
+// kernel (ldplan.hip mfma_pair_choice; bitwise the same products) -- 1: by the
+// launch-tail model (a short launch: the 8-block share of the north star), 2
+// (forced, SGV_MF_PAIR=1): every launch.  Since the column operands are loaded
+// once per row group the pair form costs ~1.4 % per byte at 5-8 columns (14 %
+// before), so the model's choice holds there too: the 8-block share -1.4 % per
+// pass at 8 columns (profiles/r06/pair58_*.jsonl)
 template <int NG, bool PP = false>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
@@ -992,19 +1004,19 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
   if (ragged)
     hipLaunchKernelGGL((k_sym_mfma<NG, 2, true, false, PP>), dim3(nstrips), dim3(256), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (pair >= (NG == 1 ? 1 : 2))
-    hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2>), dim3(nstrips), dim3(512), 0, st, d_strips,
+  else if (pair >= 1)
+    hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, PP>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else
     hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP>), dim3(nstrips), dim3(256), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
 }
 
-// 5-8-column strip passes read Pk PAIRED (k_pack) unless the plan runs the
-// wave-pair kernel (forced only).  Bitwise the same products; one box,
+// 5-8-column strip passes read Pk PAIRED (k_pack), in either strip kernel.
+// Bitwise the same products; one box,
 // alternating: the 8-block share -0.6...-1.8 % per pass, 64 blocks even to
 // -0.4 % (profiles/r06/pkpair_ab.jsonl, pkpair_bench.jsonl)
-bool strip_pk_paired(int nc, int pair) { return nc > 4 && nc <= 8 && pair < 2; }
+bool strip_pk_paired(int nc) { return nc > 4 && nc <= 8; }
 
 hipError_t launch_pk(const PassArgs& pa, int nc, int64_t mpad, double* d_pk, hipStream_t st,
                      bool paired) {
@@ -1045,13 +1057,9 @@ hipError_t launch_sym_mfma(int nc, const SymStrip* d_strips, int nstrips, const 
   // operands of the last step(s) in LDS (below).
   switch ((nc + 3) / 4) {
     case 1: launch_mf<1>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged, pair, st); break;
-    case 2:
-      if (strip_pk_paired(nc, pair))
-        launch_mf<2, true>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks,
-                           ragged, pair, st);
-      else
-        launch_mf<2>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks, ragged,
-                     pair, st);
+    case 2:   // Pk paired (strip_pk_paired)
+      launch_mf<2, true>(d_strips, nstrips, d_sitems, d_pk, nc, rowpart, colpart, pa.run, pks,
+                         ragged, pair, st);
       break;
     default:
       // the row operands of the last steps in LDS, so nothing spills (256 VGPRs
