@@ -993,9 +993,9 @@ __global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpa
 // kernel (ldplan.hip mfma_pair_choice; bitwise the same products) -- 1: by the
 // launch-tail model (a short launch: the 8-block share of the north star), 2
 // (forced, SGV_MF_PAIR=1): every launch.  Since the column operands are loaded
-// once per row group the pair form costs ~1.4 % per byte at 5-8 columns (14 %
-// before), so the model's choice holds there too: the 8-block share -1.4 % per
-// pass at 8 columns (profiles/r06/pair58_*.jsonl)
+// once per row group the model's choice holds at 5-8 columns too: the 8-block
+// share -2...-8 %, 4 x 25,000 -2.6 % per 8-column pass; launches it does not
+// pick run +1.4...+9 % with the pair form (profiles/r06/pair58_*.jsonl)
 template <int NG, bool PP = false>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
