@@ -103,13 +103,7 @@ constexpr int MF_LDP = 34;   // k_sym_mfma16's staging row pitch (doubles): conf
 // R fragment loads stay whole 128-B lines.  One box, alternating: the north
 // star -0.4...-0.8 % per pass, the 8-block share -1.4 %; at NG = 1 (8-B
 // operands) even to +0.4 %, so not there (profiles/r06/mf_sw_*.jsonl)
-// RC: no panel-end barriers -- each row group's panel row sums are combined
-// (waves in order, as below) by the last wave to finish that row group, found
-// by an LDS arrival counter.  The row groups of the strip, numbered L = 16 s +
-// g (panel s), keep their per-wave sums in a ring of RCS slots (L mod RCS): a
-// wave writes group L only after the combine of L - RCS has read its slot
-// (half the LDS of the panel-wide buffer; bitwise the same sums)
-template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false, bool RC = false>
+template <int NG, int PD, bool RAG = false, bool DEF = false, bool PP = false>
 __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict__ strips,
                                                      const SymItem* __restrict__ sitems,
                                                      const double* __restrict__ pk, int ncol,
@@ -122,22 +116,15 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
   static_assert(PD >= 1 && PD <= NT && NT % PD == 0, "prefetch depth divides the steps");
   constexpr int RW = 4 * NG;       // row-sum stride of wrow
   constexpr bool SWZ = NG == 2;
-  constexpr int RCS = 8;                                // RC: ring slots (row groups)
-  constexpr int RBR = RC ? 16 * RCS : SYM_H;           // rows per wave in rowbuf
-  __shared__ __attribute__((aligned(16))) double rowbuf[NW * RBR * RW];   // wrow
+  __shared__ __attribute__((aligned(16))) double rowbuf[NW * SYM_H * RW];   // wrow
   // the per-wave transpose tile: 16 rows x 32 columns, 16-B piece (row r, pair
   // p) at slot 16 r + (p ^ (r & 3)) -- unpadded (4 KiB, so the 64 KiB of row
   // sums and the tiles fit two workgroups per CU) and conflict-free both ways:
   // a write's 16-lane quarter covers one row, a row-fragment read's quarter
   // (rows 4q + (l & 3), pairs 4((l >> 2) & 3) + (l >> 4)) 16 distinct slots mod 16
   __shared__ __attribute__((aligned(16))) double stg[NW][16 * 32];
-  __shared__ int rc_arr[RC ? RCS : 1], rc_done[RC ? RCS : 1];   // RC: arrivals, combines done
   const SymStrip sp = strips[blockIdx.x];
   if (run && !ldg(run)) return;   // no-op pass (pipelined CG past its stop test)
-  if constexpr (RC) {
-    if (threadIdx.x < RCS) rc_arr[threadIdx.x] = rc_done[threadIdx.x] = 0;
-    __syncthreads();
-  }
   MF_TRACE_BEGIN
   const int lane = threadIdx.x & (WAVE - 1);
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
@@ -240,40 +227,6 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
 #pragma unroll
   for (int p = 0; p < PD; ++p) load_cf(curb, cur.w, cur.H, cur.nc, 0, p, cfq[p]);
   load_bcol(cur.r0, cur.H, dhalf && cur.r0 == c0, 0, bcn);
-  // RC: wait until row group L's ring slot is free (the combine of L - RCS read
-  // it); then, with this wave's sums of L written, arrive: the last of the four
-  // waves adds the four in wave order into rowpart (rows of the group below H)
-  // and marks the slot's combine done.  The LDS counter ops are ordered after
-  // the wave's LDS writes / reads by explicit lgkmcnt waits (no vmcnt wait: the
-  // fragment loads stay in flight)
-  auto rc_wait = [&](int L) {
-    while (__hip_atomic_load(&rc_done[L % RCS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
-           L / RCS)
-      __builtin_amdgcn_s_sleep(1);
-  };
-  auto rc_arrive = [&](int L, int g, int H, int item) {
-    const int j = L % RCS, use = L / RCS;
-    __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): this wave's rows written
-    int old = 0;
-    if (lane == 0)
-      old = __hip_atomic_fetch_add(&rc_arr[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    old = __builtin_amdgcn_readfirstlane(old);
-    if (old != 4 * use + 3) return;                     // not the last wave
-    const int rows = min(16, max(0, H - 16 * g));
-    const int n = rows * ncol;
-    double* dst = rowpart + ((int64_t)item * SYM_H + 16 * g) * ncol;
-    for (int k = lane; k < n; k += WAVE) {
-      const int row = k / ncol, cc = k - row * ncol;
-      const double* src = rowbuf + (16 * j + row) * RW + cc;
-      double x = src[0];
-#pragma unroll
-      for (int w = 1; w < NW; ++w) x += src[w * RBR * RW];
-      dst[k] = x;
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);                // lgkmcnt(0): the rows read
-    if (lane == 0)
-      __hip_atomic_store(&rc_done[j], use + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  };
 
 #pragma unroll 1
   for (int s = 0; s < sp.npan; ++s) {                  // uniform over the workgroup
@@ -393,32 +346,18 @@ __global__ __launch_bounds__(256, 2) void k_sym_mfma(const SymStrip* __restrict_
       }
       // row sums: the 4 blocks (lanes differing in bits 2,3; DPP row rotations),
       // kept per wave for the panel
-      double* wb = rowbuf + (wid * RBR + 16 * (RC ? (16 * s + g) % RCS : g)) * RW;
-      double rv[4][NG];
+      double* wb = rowbuf + (wid * SYM_H + 16 * g) * RW;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
         for (int q = 0; q < NG; ++q) {
           double v = drow[r][q];
           v = v + row_ror<12>(v);
-          rv[r][q] = v + row_ror<8>(v);
+          v = v + row_ror<8>(v);
+          if (bq == 0) wb[(4 * r + hi) * RW + 4 * q + n4] = v;   // D row 4r + m (m = hi)
         }
-      if constexpr (RC) rc_wait(16 * s + g);            // the slot's previous group combined
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int q = 0; q < NG; ++q)
-          if (bq == 0) wb[(4 * r + hi) * RW + 4 * q + n4] = rv[r][q];   // D row 4r + m (m = hi)
-      if constexpr (RC) rc_arrive(16 * s + g, g, cur.H, cur.item);
     }
-    if constexpr (RC) {
-      // a panel shorter than 16 row groups (a block's last): its missing row
-      // groups arrive empty, so the next panel's waits see this one done
-      for (int g = ng; g < 16; ++g) {
-        rc_wait(16 * s + g);
-        rc_arrive(16 * s + g, g, 0, cur.item);
-      }
-    } else {   // the item's H x ncol row sums: waves in order, contiguous in rowpart
+    {   // the item's H x ncol row sums: waves in order, contiguous in rowpart
       __syncthreads();
       const int n = cur.H * ncol;
       double* dst = rowpart + (int64_t)cur.item * SYM_H * ncol;
@@ -1057,12 +996,6 @@ __global__ __launch_bounds__(256) void k_pack(PassArgs pa, int ncol, int64_t mpa
 // once per row group the model's choice holds at 5-8 columns too: the 8-block
 // share -2...-8 %, 4 x 25,000 -2.6 % per 8-column pass; launches it does not
 // pick run +1.4...+9 % with the pair form (profiles/r06/pair58_*.jsonl)
-// SGV_MF_RC=1 (A/B, with SGV_AB=1): the barrier-free row-sum combine (RC)
-static bool mf_rc() {
-  const char* e = ab_env("SGV_MF_RC");
-  return e && e[0] == '1';
-}
-
 template <int NG, bool PP = false>
 static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_sitems,
                       const double* d_pk, int nc, double* rowpart, double* colpart,
@@ -1074,9 +1007,6 @@ static void launch_mf(const SymStrip* d_strips, int nstrips, const SymItem* d_si
   else if (pair >= 1)
     hipLaunchKernelGGL((k_sym_mfma_pair<NG, 2, PP>), dim3(nstrips), dim3(512), 0, st, d_strips,
                        d_sitems, d_pk, nc, rowpart, colpart, run, pks);
-  else if (mf_rc())
-    hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP, true>), dim3(nstrips), dim3(256), 0,
-                       st, d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
   else
     hipLaunchKernelGGL((k_sym_mfma<NG, 2, false, true, PP>), dim3(nstrips), dim3(256), 0, st,
                        d_strips, d_sitems, d_pk, nc, rowpart, colpart, run, pks);
