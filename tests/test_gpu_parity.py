@@ -710,7 +710,7 @@ def test_mfma_pair_kernel_bitwise(strip, monkeypatch):
     segment, the row chains handed from one to the other through LDS) gives
     products bitwise identical to the 4-wave kernel's for 3-8 columns -- which
     is what lets a plan pick either by its launch tail -- and both match numpy
-    (the 5-8-column 4-wave passes read Pk paired, the forced pair kernel not)."""
+    (both read Pk paired at 5-8 columns)."""
     monkeypatch.setenv("SGV_AB", "1")
     sizes = [5000, 513, 2600, 1, 4097]
     blocks = rand_blocks(sizes, seed=strip, symmetric=True)
